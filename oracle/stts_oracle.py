@@ -1,0 +1,336 @@
+"""ORACLE — test infrastructure only.  CPU restatement of the StyleTTS2-lite synthesis path.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker / CPU baseline; the product path (the HIP library
+behind include/stts2.h) never calls it.
+
+Each function restates one reference function op for op with stock PyTorch-CPU ops
+on a plain state dict (the reference modules themselves never leave the survey
+container).  Pinning: tests/golden/*.npz were produced by importing the reference
+modules (tests/golden/make_golden.py) on formula weights/inputs/noise
+(stts2_mi355x/synth.py); tests/test_oracle_golden.py checks this file against them.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+SQRT2 = math.sqrt(2)
+
+
+def _t(sd, k):
+    v = sd[k]
+    return v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
+
+
+def wn(sd, p):
+    """torch.nn.utils.weight_norm(dim=0) fold, as the reference's forward pre-hook computes it."""
+    return torch._weight_norm(_t(sd, p + ".weight_v"), _t(sd, p + ".weight_g"), 0)
+
+
+def _bias(sd, p):
+    k = p + ".bias"
+    return _t(sd, k) if k in sd else None
+
+
+def snake(x, a):
+    """Snake1D, reference hifigan.py:68 / :329: x + (1/a) * sin(a*x)**2."""
+    return x + (1 / a) * (torch.sin(a * x) ** 2)
+
+
+def adain1d(x, s, sd, p):
+    """reference hifigan.py:14-24 (AdaIN1d): (1+gamma)*InstanceNorm(x)+beta, h = fc(s)."""
+    h = F.linear(s, _t(sd, p + ".fc.weight"), _t(sd, p + ".fc.bias"))
+    h = h.view(h.size(0), h.size(1), 1)
+    gamma, beta = torch.chunk(h, chunks=2, dim=1)
+    return (1 + gamma) * F.instance_norm(x, eps=1e-5) + beta
+
+
+def adain_resblock1(x, s, sd, p, kernel_size, dilation):
+    """reference hifigan.py:65-74 (AdaINResBlock1.forward)."""
+    for j, d in enumerate(dilation):
+        a1 = _t(sd, f"{p}.alpha1.{j}")
+        a2 = _t(sd, f"{p}.alpha2.{j}")
+        xt = adain1d(x, s, sd, f"{p}.adain1.{j}")
+        xt = xt + (1 / a1) * (torch.sin(a1 * xt) ** 2)
+        xt = F.conv1d(xt, wn(sd, f"{p}.convs1.{j}"), _bias(sd, f"{p}.convs1.{j}"), 1,
+                      (kernel_size * d - d) // 2, d)
+        xt = adain1d(xt, s, sd, f"{p}.adain2.{j}")
+        xt = xt + (1 / a2) * (torch.sin(a2 * xt) ** 2)
+        xt = F.conv1d(xt, wn(sd, f"{p}.convs2.{j}"), _bias(sd, f"{p}.convs2.{j}"), 1, (kernel_size - 1) // 2, 1)
+        x = xt + x
+    return x
+
+
+def adain_resblk1d(x, s, sd, p, upsample: bool, learned_sc: bool):
+    """reference hifigan.py:359-403 == models.py:326-370 (AdainResBlk1d, eval: dropout = identity)."""
+    r = adain1d(x, s, sd, p + ".norm1")
+    r = F.leaky_relu(r, 0.2)
+    if upsample:
+        C = r.shape[1]
+        r = F.conv_transpose1d(r, wn(sd, p + ".pool"), _bias(sd, p + ".pool"), stride=2, padding=1,
+                               output_padding=1, groups=C)
+    r = F.conv1d(r, wn(sd, p + ".conv1"), _bias(sd, p + ".conv1"), 1, 1)
+    r = adain1d(r, s, sd, p + ".norm2")
+    r = F.leaky_relu(r, 0.2)
+    r = F.conv1d(r, wn(sd, p + ".conv2"), _bias(sd, p + ".conv2"), 1, 1)
+    sc = F.interpolate(x, scale_factor=2, mode="nearest") if upsample else x
+    if learned_sc:
+        sc = F.conv1d(sc, wn(sd, p + ".conv1x1"), None)
+    return (r + sc) / SQRT2
+
+
+# ----------------------------------------------------------------------------------
+# harmonic-plus-noise source
+# ----------------------------------------------------------------------------------
+
+def sine_source(f0_curve, sd, p, upsample_scale: int, noise):
+    """reference hifigan.py:189-218 (SineGen.forward) + :254-268 (SourceModuleHnNSF) + :323.
+
+    f0_curve [B, 2T]; noise [B, L, 9] = the randn_like(sine_waves) draw (hifigan.py:213).
+    rand_ini (hifigan.py:126-129) is added to sample 0 only and the ÷upsample_scale linear
+    downsample reads samples 300j+149/150 only, so it never reaches the output (measured
+    diff 0.0); it is omitted.  Returns har [B, L, 1] (pre-transpose)."""
+    f0 = F.interpolate(f0_curve[:, None], scale_factor=upsample_scale).transpose(1, 2)  # nearest, [B,L,1]
+    fn = torch.multiply(f0, torch.FloatTensor([[range(1, 10)]]))
+    rad_values = (fn / 24000) % 1
+    rad_values = F.interpolate(rad_values.transpose(1, 2), scale_factor=1 / upsample_scale,
+                               mode="linear").transpose(1, 2)
+    phase = torch.cumsum(rad_values, dim=1) * 2 * np.pi
+    phase = F.interpolate(phase.transpose(1, 2) * upsample_scale, scale_factor=upsample_scale,
+                          mode="linear").transpose(1, 2)
+    sine_waves = torch.sin(phase) * 0.1
+    uv = (f0 > 10).type(torch.float32)
+    noise_amp = uv * 0.003 + (1 - uv) * 0.1 / 3
+    sine_waves = sine_waves * uv + noise_amp * noise
+    return torch.tanh(F.linear(sine_waves, _t(sd, p + ".l_linear.weight"), _t(sd, p + ".l_linear.bias")))
+
+
+# ----------------------------------------------------------------------------------
+# HiFi-GAN decoder
+# ----------------------------------------------------------------------------------
+
+def generator_hifigan(x, s, f0_curve, sd, cfg, noise, taps=None):
+    """reference hifigan.py:321-347 (Generator.forward)."""
+    rates, kernels = cfg["upsample_rates"], cfg["upsample_kernel_sizes"]
+    rks, rds = cfg["resblock_kernel_sizes"], cfg["resblock_dilation_sizes"]
+    nk = len(rks)
+    scale = int(np.prod(rates))
+    src = sine_source(f0_curve, sd, "generator.m_source", scale, noise)
+    har = src.transpose(1, 2)
+    if taps is not None:
+        taps["source"] = src
+    for i, (u, k) in enumerate(zip(rates, kernels)):
+        a = _t(sd, f"generator.alphas.{i}")
+        x = x + (1 / a) * (torch.sin(a * x) ** 2)
+        if i + 1 < len(rates):
+            sf = int(np.prod(rates[i + 1:]))
+            xs_src = F.conv1d(har, _t(sd, f"generator.noise_convs.{i}.weight"),
+                              _t(sd, f"generator.noise_convs.{i}.bias"), sf, (sf + 1) // 2)
+            xs_src = adain_resblock1(xs_src, s, sd, f"generator.noise_res.{i}", 7, [1, 3, 5])
+        else:
+            xs_src = F.conv1d(har, _t(sd, f"generator.noise_convs.{i}.weight"),
+                              _t(sd, f"generator.noise_convs.{i}.bias"))
+            xs_src = adain_resblock1(xs_src, s, sd, f"generator.noise_res.{i}", 11, [1, 3, 5])
+        x = F.conv_transpose1d(x, wn(sd, f"generator.ups.{i}"), _bias(sd, f"generator.ups.{i}"), u,
+                               u // 2 + u % 2, u % 2)
+        x = x + xs_src
+        xs = None
+        for j in range(nk):
+            r = adain_resblock1(x, s, sd, f"generator.resblocks.{i * nk + j}", rks[j], rds[j])
+            xs = r if xs is None else xs + r
+        x = xs / nk
+        if taps is not None:
+            taps[f"stage{i}"] = x
+    a = _t(sd, f"generator.alphas.{len(rates)}")
+    x = x + (1 / a) * (torch.sin(a * x) ** 2)
+    x = F.conv1d(x, wn(sd, "generator.conv_post"), _bias(sd, "generator.conv_post"), 1, 3)
+    if taps is not None:
+        taps["pre_tanh"] = x
+    return torch.tanh(x)
+
+
+def decoder_frontend(asr, F0_curve, N, s, sd):
+    """reference hifigan.py:458-472 == istftnet.py:704-718 (eval branch)."""
+    F0 = F.conv1d(F0_curve.unsqueeze(1), wn(sd, "F0_conv"), _bias(sd, "F0_conv"), 2, 1)
+    Nc = F.conv1d(N.unsqueeze(1), wn(sd, "N_conv"), _bias(sd, "N_conv"), 2, 1)
+    x = torch.cat([asr, F0, Nc], axis=1)
+    x = adain_resblk1d(x, s, sd, "encode", False, True)
+    asr_res = F.conv1d(asr, wn(sd, "asr_res.0"), _bias(sd, "asr_res.0"))
+    res = True
+    for i in range(4):
+        if res:
+            x = torch.cat([x, asr_res, F0, Nc], axis=1)
+        up = i == 3
+        x = adain_resblk1d(x, s, sd, f"decode.{i}", up, True)  # dim_in 1090 != dim_out
+        if up:
+            res = False
+    return x
+
+
+def decoder_hifigan(asr, F0_curve, N, s, sd, cfg, noise, taps=None):
+    """reference hifigan.py:446-475 (Decoder.forward, eval)."""
+    x = decoder_frontend(asr, F0_curve, N, s, sd)
+    if taps is not None:
+        taps["frontend"] = x
+    return generator_hifigan(x, s, F0_curve, sd, cfg, noise, taps)
+
+
+# ----------------------------------------------------------------------------------
+# iSTFTNet decoder
+# ----------------------------------------------------------------------------------
+
+def stft_transform(wave, sd, n_fft, hop):
+    """reference istftnet.py:207-243 (CustomSTFT.transform, center=True, replicate pad)."""
+    pad = n_fft // 2
+    wave = F.pad(wave, (pad, pad), mode="replicate")
+    x = wave.unsqueeze(1)
+    re = F.conv1d(x, _t(sd, "generator.stft.weight_forward_real"), None, stride=hop, padding=0)
+    im = F.conv1d(x, _t(sd, "generator.stft.weight_forward_imag"), None, stride=hop, padding=0)
+    mag = torch.sqrt(re ** 2 + im ** 2 + 1e-14)
+    phase = torch.atan2(im, re)
+    phase[(im == 0) & (re < 0)] = torch.pi
+    return mag, phase
+
+
+def stft_inverse(mag, phase, sd, n_fft, hop):
+    """reference istftnet.py:246-293 (CustomSTFT.inverse; no window-sum normalisation)."""
+    re = mag * torch.cos(phase)
+    im = mag * torch.sin(phase)
+    rr = F.conv_transpose1d(re, _t(sd, "generator.stft.weight_backward_real"), None, stride=hop, padding=0)
+    ii = F.conv_transpose1d(im, _t(sd, "generator.stft.weight_backward_imag"), None, stride=hop, padding=0)
+    w = rr - ii
+    pad = n_fft // 2
+    return w[..., pad:-pad]
+
+
+def generator_istft(x, s, f0_curve, sd, cfg, noise, taps=None):
+    """reference istftnet.py:543-573 (Generator.forward)."""
+    rates, kernels = cfg["upsample_rates"], cfg["upsample_kernel_sizes"]
+    rks, rds = cfg["resblock_kernel_sizes"], cfg["resblock_dilation_sizes"]
+    n_fft, hop = cfg["gen_istft_n_fft"], cfg["gen_istft_hop_size"]
+    nk = len(rks)
+    scale = int(np.prod(rates)) * hop
+    src = sine_source(f0_curve, sd, "generator.m_source", scale, noise)
+    if taps is not None:
+        taps["source"] = src
+    har_source = src.transpose(1, 2).squeeze(1)
+    spec, ph = stft_transform(har_source, sd, n_fft, hop)
+    har = torch.cat([spec, ph], dim=1)
+    if taps is not None:
+        taps["har"] = har
+    for i, (u, k) in enumerate(zip(rates, kernels)):
+        x = F.leaky_relu(x, 0.1)
+        if i + 1 < len(rates):
+            sf = int(np.prod(rates[i + 1:]))
+            xs_src = F.conv1d(har, _t(sd, f"generator.noise_convs.{i}.weight"),
+                              _t(sd, f"generator.noise_convs.{i}.bias"), sf, (sf + 1) // 2)
+            xs_src = adain_resblock1(xs_src, s, sd, f"generator.noise_res.{i}", 7, [1, 3, 5])
+        else:
+            xs_src = F.conv1d(har, _t(sd, f"generator.noise_convs.{i}.weight"),
+                              _t(sd, f"generator.noise_convs.{i}.bias"))
+            xs_src = adain_resblock1(xs_src, s, sd, f"generator.noise_res.{i}", 11, [1, 3, 5])
+        x = F.conv_transpose1d(x, wn(sd, f"generator.ups.{i}"), _bias(sd, f"generator.ups.{i}"), u, (k - u) // 2)
+        if i == len(rates) - 1:
+            x = F.pad(x, (1, 0), mode="reflect")
+        x = x + xs_src
+        xs = None
+        for j in range(nk):
+            r = adain_resblock1(x, s, sd, f"generator.resblocks.{i * nk + j}", rks[j], rds[j])
+            xs = r if xs is None else xs + r
+        x = xs / nk
+        if taps is not None:
+            taps[f"stage{i}"] = x
+    x = F.leaky_relu(x)
+    x = F.conv1d(x, wn(sd, "generator.conv_post"), _bias(sd, "generator.conv_post"), 1, 3)
+    if taps is not None:
+        taps["post"] = x
+    nb = n_fft // 2 + 1
+    spec = torch.exp(x[:, :nb, :])
+    phase = torch.sin(x[:, nb:, :])
+    return stft_inverse(spec, phase, sd, n_fft, hop)
+
+
+def decoder_istft(asr, F0_curve, N, s, sd, cfg, noise, taps=None):
+    """reference istftnet.py:692-721 (Decoder.forward, eval)."""
+    x = decoder_frontend(asr, F0_curve, N, s, sd)
+    if taps is not None:
+        taps["frontend"] = x
+    return generator_istft(x, s, F0_curve, sd, cfg, noise, taps)
+
+
+# ----------------------------------------------------------------------------------
+# ProsodyPredictor.F0Ntrain and StyleEncoder
+# ----------------------------------------------------------------------------------
+
+def f0n_convstacks(xl, s, sd, prefix="", taps=None):
+    """reference models.py:451-461: F0 / N AdainResBlk1d stacks + 1x1 projections.
+    xl = shared-LSTM output, [B, d_hid, T] (models.py:449-451)."""
+    out = []
+    for br in ("F0", "N"):
+        h = xl
+        for i in range(3):
+            p = f"{prefix}{br}.{i}"
+            ls = (p + ".conv1x1.weight_v") in sd
+            h = adain_resblk1d(h, s, sd, p, upsample=(i == 1), learned_sc=ls)
+        h = F.conv1d(h, _t(sd, f"{prefix}{br}_proj.weight"), _t(sd, f"{prefix}{br}_proj.bias"))
+        out.append(h.squeeze(1))
+    return tuple(out)
+
+
+def shared_lstm(en, sd, prefix="", d_hid=512, style_dim=128):
+    """reference models.py:449: nn.LSTM(d_hid+style_dim, d_hid//2, bidirectional, batch_first)."""
+    lstm = torch.nn.LSTM(d_hid + style_dim, d_hid // 2, 1, batch_first=True, bidirectional=True)
+    lsd = {k[len(prefix) + 7:]: _t(sd, k) for k in sd if k.startswith(prefix + "shared.")}
+    lstm.load_state_dict(lsd)
+    with torch.no_grad():
+        x, _ = lstm(en.transpose(-1, -2))
+    return x.transpose(-1, -2)
+
+
+def f0ntrain(en, s, sd, prefix=""):
+    """reference models.py:448-461 (ProsodyPredictor.F0Ntrain)."""
+    xl = shared_lstm(en, sd, prefix)
+    return f0n_convstacks(xl, s, sd, prefix)
+
+
+def _down_half(x):
+    """reference models.py:58-61 (DownSample 'half')."""
+    if x.shape[-1] % 2 != 0:
+        x = torch.cat([x, x[..., -1].unsqueeze(-1)], dim=-1)
+    return F.avg_pool2d(x, 2)
+
+
+def resblk2d(x, sd, p, learned_sc):
+    """reference models.py:82-123 (ResBlk, normalize=False, downsample='half')."""
+    sc = x
+    if learned_sc:
+        sc = F.conv2d(sc, _t(sd, p + ".conv1x1.weight"), None)
+    sc = _down_half(sc)
+    r = F.leaky_relu(x, 0.2)
+    r = F.conv2d(r, _t(sd, p + ".conv1.weight"), _t(sd, p + ".conv1.bias"), 1, 1)
+    C = r.shape[1]
+    r = F.conv2d(r, _t(sd, p + ".downsample_res.conv.weight"), _t(sd, p + ".downsample_res.conv.bias"),
+                 2, 1, 1, C)
+    r = F.leaky_relu(r, 0.2)
+    r = F.conv2d(r, _t(sd, p + ".conv2.weight"), _t(sd, p + ".conv2.bias"), 1, 1)
+    return (sc + r) / SQRT2
+
+
+def style_encoder(mel, sd, prefix="", taps=None):
+    """reference models.py:125-150 (StyleEncoder.forward). mel [B,1,80,F] -> [B,style_dim]."""
+    h = F.conv2d(mel, _t(sd, prefix + "shared.0.weight"), _t(sd, prefix + "shared.0.bias"), 1, 1)
+    for i in range(1, 5):
+        p = f"{prefix}shared.{i}"
+        h = resblk2d(h, sd, p, (p + ".conv1x1.weight") in sd)
+        if taps is not None:
+            taps[f"blk{i}"] = h
+    h = F.leaky_relu(h, 0.2)
+    h = F.conv2d(h, _t(sd, prefix + "shared.6.weight"), _t(sd, prefix + "shared.6.bias"))
+    h = F.adaptive_avg_pool2d(h, 1)
+    h = F.leaky_relu(h, 0.2)
+    h = h.view(h.size(0), -1)
+    return F.linear(h, _t(sd, prefix + "unshared.weight"), _t(sd, prefix + "unshared.bias"))

@@ -1,0 +1,53 @@
+"""Shared test helpers: formula weights for the drop-in modules, golden loading."""
+import json
+import os
+
+import numpy as np
+import torch
+
+from stts2_mi355x import synth
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+HIFI_CFG = dict(resblock_kernel_sizes=[3, 7, 11], upsample_rates=[10, 5, 3, 2], upsample_initial_channel=512,
+                resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], upsample_kernel_sizes=[20, 10, 6, 4])
+ISTFT_CFG = dict(resblock_kernel_sizes=[3, 7, 11], upsample_rates=[10, 6], upsample_initial_channel=512,
+                 resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], upsample_kernel_sizes=[20, 12],
+                 gen_istft_n_fft=20, gen_istft_hop_size=5)
+
+
+def golden(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+def meta():
+    with open(os.path.join(GOLDEN, "meta.json")) as f:
+        return json.load(f)
+
+
+def fill_module(module, prefix=""):
+    """Load formula weights (stts2_mi355x.synth) into a module by state-dict key."""
+    sd = module.state_dict()
+    new = {}
+    for k, v in sd.items():
+        if synth.is_fixed_buffer(k):
+            new[k] = v
+        else:
+            new[k] = torch.from_numpy(synth.synth_param(prefix + k, tuple(v.shape)))
+    module.load_state_dict(new, strict=True)
+    return module
+
+
+def make_decoder(kind):
+    if kind == "hifigan":
+        from stts2_mi355x.hifigan import Decoder
+        return fill_module(Decoder(dim_in=512, style_dim=128, dim_out=80, **HIFI_CFG)).eval(), HIFI_CFG
+    from stts2_mi355x.istftnet import Decoder
+    return fill_module(Decoder(dim_in=512, style_dim=128, dim_out=80, **ISTFT_CFG)).eval(), ISTFT_CFG
+
+
+def decoder_case(B, T, utt0=0):
+    asr, f0, n, s = synth.decoder_inputs(B, T, utt0=utt0)
+    noise = synth.source_noise(B, 600 * T, utt0=utt0)
+    return [torch.from_numpy(a) for a in (asr, f0, n, s, noise)]
