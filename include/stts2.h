@@ -1,0 +1,110 @@
+/*
+ * stts2.h — C-ABI of the MI355X-native StyleTTS2-lite synthesis path (libstts2.so).
+ *
+ * The library replaces the compute under these reference interfaces (thewh1teagle/StyleTTS2-lite
+ * @ 2025-06-14), keeping their argument meaning:
+ *
+ *   stts_decoder_fwd  <- Modules/hifigan.py:446  Decoder.forward(asr, F0_curve, N, s)
+ *                        Modules/istftnet.py:692 Decoder.forward(asr, F0_curve, N, s)
+ *   stts_f0n_fwd      <- models.py:448           ProsodyPredictor.F0Ntrain(x, s)  (conv stacks
+ *                        after the shared BiLSTM, models.py:451-461)
+ *   stts_style_fwd    <- models.py:145           StyleEncoder.forward(x)
+ *   stts_model_create / stts_param_* / stts_set_param / stts_pack
+ *                     <- the module constructors + load_state_dict (inference.py:93-124, 150-174)
+ *
+ * Conventions: every tensor argument is a raw DEVICE pointer (HIP, gfx950) to contiguous
+ * float32 data in the reference's own layout; sizes are plain ints; `stream` is a hipStream_t
+ * (0 = default stream).  The caller owns all memory: parameters (the state-dict tensors,
+ * float32, contiguous), the packed-weight buffer and the workspace.  Nothing is allocated or
+ * freed on the device by the library; calls are asynchronous on `stream` and re-entrant per
+ * (model, workspace).  Return value: 0 on success, >0 a hipError_t, <0 an STTS_E* code below.
+ */
+#ifndef STTS2_H
+#define STTS2_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct stts_model stts_model;
+
+/* model kinds */
+#define STTS_KIND_HIFIGAN 0  /* Modules/hifigan.py Decoder   */
+#define STTS_KIND_ISTFTNET 1 /* Modules/istftnet.py Decoder  */
+#define STTS_KIND_F0N 2      /* models.py ProsodyPredictor F0/N conv stacks */
+#define STTS_KIND_STYLE 3    /* models.py StyleEncoder       */
+
+/* compute / activation dtypes */
+#define STTS_FP32 0 /* fp32 storage, exact-fp32 MFMA (parity mode)          */
+#define STTS_BF16 1 /* bf16 storage, bf16 MFMA with fp32 accumulation      */
+
+/* error codes (negative) */
+#define STTS_EINVAL (-1)
+#define STTS_EDTYPE (-2)
+#define STTS_EPARAMS (-3)
+#define STTS_EWORKSPACE (-4)
+#define STTS_ENOTPACKED (-5)
+
+/*
+ * cfg (ints) per kind:
+ *   HIFIGAN : dim_in, style_dim, upsample_initial_channel, n_up, rates[n_up], kernels[n_up],
+ *             n_rb, rb_kernels[n_rb], rb_dilations[n_rb*3]
+ *             (reference Decoder(dim_in, style_dim, resblock_kernel_sizes, upsample_rates,
+ *              upsample_initial_channel, resblock_dilation_sizes, upsample_kernel_sizes))
+ *   ISTFTNET: as HIFIGAN, then gen_istft_n_fft, gen_istft_hop_size
+ *   F0N     : d_hid, style_dim                     (ProsodyPredictor(style_dim, d_hid, ...))
+ *   STYLE   : dim_in, style_dim, max_conv_dim      (StyleEncoder(dim_in, style_dim, max_conv_dim))
+ */
+int stts_model_create(int kind, const int* cfg, int ncfg, stts_model** out);
+void stts_model_destroy(stts_model* m);
+
+/* Parameters the model reads, named exactly as the reference state-dict keys. */
+int stts_param_count(const stts_model* m);
+const char* stts_param_name(const stts_model* m, int i);
+long long stts_param_numel(const stts_model* m, int i);
+int stts_set_param(stts_model* m, int i, const float* dev_ptr);
+
+/* Weight-norm folding + MFMA packing into a caller buffer (once per dtype after load). */
+long long stts_packed_bytes(const stts_model* m, int dtype);
+int stts_pack(stts_model* m, int dtype, void* packed, long long bytes, void* stream);
+
+/* Workspace for one forward of B utterances of T frames (decoder: T = asr frames;
+ * F0N: T = text-aligned frames; STYLE: T = mel frames). */
+long long stts_workspace_bytes(const stts_model* m, int dtype, int B, int T);
+
+/* Decoder: asr [B][dim_in][T], F0_curve [B][2T], N [B][2T], s [B][style_dim] -> out [B][1][600T].
+ * noise: [B][600T][9] = the SineGen randn_like draw (hifigan.py:213), or NULL to draw it on the
+ * device from a counter RNG keyed by (seed, utt_offset + b, sample, harmonic). */
+int stts_decoder_fwd(stts_model* m, int dtype, const float* asr, const float* f0_curve, const float* n,
+                     const float* s, const float* noise, unsigned long long seed, long long utt_offset, int B,
+                     int T, float* out, void* workspace, long long ws_bytes, void* stream);
+
+/* F0/N conv stacks: x = shared-BiLSTM output [B][T][d_hid] (batch_first, as nn.LSTM returns it),
+ * s [B][style_dim] -> F0 [B][2T], N [B][2T]. */
+int stts_f0n_fwd(stts_model* m, int dtype, const float* x, const float* s, int B, int T, float* F0, float* N,
+                 void* workspace, long long ws_bytes, void* stream);
+
+/* Style encoder: mel [B][1][80][T] -> style [B][style_dim]. */
+int stts_style_fwd(stts_model* m, int dtype, const float* mel, int B, int T, float* out, void* workspace,
+                   long long ws_bytes, void* stream);
+
+const char* stts_error_string(int code);
+
+/* Optional per-kernel timing of the dominant kernel class (conv1d_igemm) with hipEvents recorded
+ * on `stream` around each launch: enable, run, then read totals (ms, launches). */
+int stts_profile_enable(int on);
+int stts_profile_read(double* total_ms, long long* launches, double* alg_flops, double* alg_bytes);
+
+/* ---- testing hook (not a product path): one conv1d_igemm launch on fp32 frames.
+ * x [B][Lin][Cin] frames; w in nn.Conv1d [Cout][Cin][K] / nn.ConvTranspose1d [Cin][Cout][K] layout;
+ * pro_mode bitmask 1 = AdaIN (instance stats of x, gamma_beta [B][2*Cin]), 2 = Snake (alpha [Cin]),
+ * 4 = LeakyReLU(slope); y = (conv + bias + res) * out_scale, [B][Lout][Cout]; stats_out [B][Cout][2]. */
+int stts_test_conv1d(int dtype, const float* x, int B, int Lin, int Cin, const float* w, const float* bias, int Cout,
+                     int K, int transposed, int stride, int dil, int pad, int out_pad, int pro_mode,
+                     const float* gamma_beta, const float* alpha, float slope, const float* res, float out_scale,
+                     float* y, int Lout, double* stats_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STTS2_H */

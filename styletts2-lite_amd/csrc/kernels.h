@@ -1,0 +1,110 @@
+// Internal launcher interface (host side) for the gfx950 kernels.  Not part of the
+// public C-ABI (include/stts2.h); the plan code in plan.cpp strings these together.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+// ---------------------------------------------------------------- conv1d_igemm
+struct ConvParams {
+  // input frames [B][Lin][x_ld] (dtype of the run); channels [0, Cin) used
+  const void* x;
+  long long x_bs;
+  int x_ld, Lin, Cin;
+  // geometry: input row of output frame q, tap t = q*stride + t*dil - pad
+  int B, Lq, KS, dil, stride, pad;
+  // GEMM columns and packed weights ([chunk][tap][Np][32] bf16 / [chunk][tap][32][Np] fp32)
+  int N;
+  const void* w;
+  int nchunks;
+  const float* bias;  // [Cout], column n uses bias[n % Cout]
+  int Cout;
+  Prologue pro;
+  // epilogue: column n -> (phase n / Cout, channel n % Cout); output row o = q*up + phase - opad
+  int up, opad, Lout;
+  void* y;
+  long long y_bs;
+  int y_ld, y_row_off, y_f32;
+  const void* res;  // residual, row (o + y_row_off) >> res_shift
+  long long res_bs;
+  int res_ld, res_shift;
+  float out_scale;
+  const void* accb;  // running sum buffer (resblock average)
+  long long acc_bs;
+  int acc_ld;
+  float acc_div;
+  int epi_tanh, reflect_front;
+  double* stats;  // [B][stats_ld][2] accumulated statistics of the stored output
+  int stats_ld;
+  // 2-D taps on a zero-padded, row-flattened image (style encoder): tap t reads input row
+  // q*stride + (t / kw) * row_off + (t % kw) * dil - pad.  1-D convs: kw = KS, row_off = 0.
+  int kw, row_off;
+  // zero columns: output rows o with (o % zc_period) >= zc_valid are written as 0 and excluded
+  // from the statistics (keeps the padded image borders zero); zc_period = 0 disables.
+  int zc_period, zc_valid;
+  int tg;  // set by the launcher
+};
+
+int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);
+
+// ---------------------------------------------------------------- misc kernels
+// src [B][C][L] fp32 (torch NCL) -> dst frames [B][L][ld] at channel offset c0; optional stats.
+int st_ncl_to_frames(const float* src, int B, int C, int L, void* dst, int ld, int c0, long long dst_bs,
+                     double* stats, int stats_ld, int dtype, hipStream_t s);
+// frames fp32 [B][L][ld_in] -> frames (dtype) [B][L][ld_out]; optional stats
+int st_frames_convert(const float* src, int B, int L, int C, int ld_in, void* dst, int ld_out, double* stats,
+                      int stats_ld, int dtype, hipStream_t s);
+// single-input-channel conv (F0_conv / N_conv / HiFi-GAN noise_convs): in fp32 [B][in_bs]
+// out[b][t][c0+c] = bias[c] + sum_k w[c][k] * in[b][t*stride - pad + k]; up to 3 destinations.
+struct SmallConvDst {
+  void* y;
+  long long y_bs;
+  int y_ld, c0;
+  double* stats;
+  int stats_ld;
+};
+int st_conv_cin1(const float* in, long long in_bs, int Lin, int B, const float* w, const float* bias, int C,
+                 int K, int stride, int pad, int Lout, const SmallConvDst* dst, int ndst, int dtype,
+                 hipStream_t s);
+// SineGen phase: ph[b][h][j] = ((cumsum_f64(rad)[j] * 2) * pi) * scale  (fp32)
+int st_sine_phase(const float* f0, int B, int n, int scale, float* ph, hipStream_t s);
+// SineGen + SourceModuleHnNSF: har[b][t] (fp32), t < n*scale
+int st_sine_source(const float* f0, const float* ph, int B, int n, int scale, const float* lw, const float* lb,
+                   const float* noise, unsigned long long seed, long long utt_offset, float* har, hipStream_t s);
+// depthwise ConvTranspose1d(C, C, 3, stride 2, pad 1, out_pad 1, groups=C) with prologue
+int st_pool_dw(const void* x, long long x_bs, int x_ld, int B, int Lin, int C, const float* w, const float* bias,
+               const Prologue& pro, void* y, long long y_bs, int y_ld, int dtype, hipStream_t s);
+// H[b][n] = bias[n] + sum_k s[b][k] * W[n][k]
+int st_linear(const float* s, int B, int K, const float* W, const float* bias, int N, float* H, hipStream_t st);
+// column statistics of frames (dtype) [B][L][ld] channels [c0, c0+C) into stats[b][c0+c]
+int st_frames_stats(const void* x, long long x_bs, int x_ld, int B, int L, int c0, int C, double* stats,
+                    int stats_ld, int dtype, hipStream_t s);
+// CustomSTFT.transform: wave fp32 [B][L] -> frames [B][F][ld] with mag (0..nb-1), phase (nb..2nb-1)
+int st_stft(const float* wave, int B, int L, int n_fft, int hop, const float* wr, const float* wi, void* y,
+            int ld, int dtype, hipStream_t s);
+// exp/sin head + CustomSTFT.inverse: post frames [B][F][ld] -> wave fp32 [B][L]
+int st_istft(const void* post, int B, int F, int ld, int n_fft, int hop, const float* br, const float* bi,
+             float* out, int L, int dtype, hipStream_t s);
+// weight-norm fold: wout[i] = v[i] * (g[row]/||v[row]||), rows = d0 of v ([d0][inner]); g may be null (copy)
+int st_wn_fold(const float* v, const float* g, int d0, int inner, float* wout, hipStream_t s);
+// pack a folded conv weight for conv1d_igemm.
+//   transposed == 0: w [Cout][Cin][K]   (nn.Conv1d),           N = Cout,   taps = K
+//   transposed == 1: w [Cin][Cout][K]   (nn.ConvTranspose1d),  N = u*Cout, taps = ceil(K/u)
+int st_pack_conv(const float* w, int Cin, int Cout, int K, int transposed, int u, void* out, int dtype,
+                 hipStream_t s);
+size_t st_packed_conv_elems(int Cin, int Cout, int K, int transposed, int u);
+// frames (dtype) [B][L][ld] -> fp32 frames [B][L][C]
+int st_frames_to_f32(const void* src, int B, int L, int C, int ld, float* dst, int dtype, hipStream_t s);
+// ---------------------------------------------------------------- style encoder (2-D, padded NHWC)
+// An image [H][W] is stored zero-padded as rows (H+2)*(W+2) of ld channels ("padded frames").
+// mel fp32 [B][1][H][W] -> padded frames (channel 0), ld = 8
+int st_mel_to_padded(const float* mel, int B, int H, int W, void* dst, int dtype, hipStream_t s);
+// depthwise Conv2d(C, C, 3, stride 2, pad 1, groups=C) + bias: padded [H][W] -> padded [H/2][ceil(W/2)]
+int st_dw_s2(const void* x, int B, int H, int W, int C, const float* w, const float* bias, void* y, int dtype,
+             hipStream_t s);
+// DownSample('half'): replicate-pad odd W, avg_pool2d(2): padded [H][W] -> padded [H/2][ceil(W/2)]
+int st_avgpool_half(const void* x, int B, int H, int W, int C, void* y, int dtype, hipStream_t s);
+// AdaptiveAvgPool2d(1) over Wv valid rows of z [B][rows][C] -> LeakyReLU(0.2) -> Linear(C, N)
+int st_gap_linear(const void* z, int B, int rows, int Wv, int C, const float* w, const float* bias, int N,
+                  float* out, int dtype, hipStream_t s);

@@ -1,0 +1,651 @@
+// Memory-bound / small kernels of the synthesis path (gfx950):
+//   layout conversion + InstanceNorm statistics, the single-channel convs (F0_conv,
+//   N_conv, HiFi-GAN noise_convs), the harmonic-plus-noise source (SineGen +
+//   SourceModuleHnNSF), the depthwise x2 ConvTranspose "pool", the AdaIN style
+//   projections, the iSTFTNet CustomSTFT transform / inverse, and weight-norm
+//   folding + MFMA weight packing.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+
+
+#define DISPATCH_DTYPE(dtype, T, ...)              \
+  do {                                             \
+    if ((dtype) == ST_FP32) {                      \
+      using T = float;                             \
+      __VA_ARGS__;                                 \
+    } else if ((dtype) == ST_BF16) {               \
+      using T = bf16_t;                            \
+      __VA_ARGS__;                                 \
+    } else {                                       \
+      return ST_EDTYPE;                            \
+    }                                              \
+  } while (0)
+
+__device__ __forceinline__ void atomic_stats(double* st, double a, double q) {
+  atomicAdd(st, a);
+  atomicAdd(st + 1, q);
+}
+
+// ------------------------------------------------------------------ NCL -> frames
+template <typename T>
+__global__ void __launch_bounds__(256) k_ncl_to_frames(const float* __restrict__ src, int C, int L, T* dst, int ld,
+                                                       int c0, long long dst_bs, double* stats, int stats_ld) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z, ct = blockIdx.y * 64, lt = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  const float* sb = src + (size_t)b * C * L;
+  for (int i = ty; i < 64; i += 4) {
+    const int c = ct + i, l = lt + tx;
+    tile[i][tx] = (c < C && l < L) ? sb[(size_t)c * L + l] : 0.f;
+  }
+  __syncthreads();
+  T* db = dst + (size_t)b * dst_bs;
+  for (int i = ty; i < 64; i += 4) {
+    const int l = lt + i, c = ct + tx;
+    if (l < L && c < C) db[(size_t)l * ld + c0 + c] = from_f32<T>(tile[tx][i]);
+  }
+  if (stats && threadIdx.x < 64) {
+    const int c = ct + threadIdx.x;
+    if (c < C) {
+      double a = 0, q = 0;
+      for (int j = 0; j < 64; ++j) {
+        if (lt + j < L) {
+          const float v = to_f32(from_f32<T>(tile[threadIdx.x][j]));
+          a += v;
+          q += (double)v * v;
+        }
+      }
+      atomic_stats(stats + ((size_t)b * stats_ld + c0 + c) * 2, a, q);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fp32 frames -> frames
+template <typename T>
+__global__ void __launch_bounds__(256) k_frames_convert(const float* __restrict__ src, int L, int C, int ld_in,
+                                                        T* dst, int ld_out, double* stats, int stats_ld) {
+  const int b = blockIdx.y;
+  const int c = threadIdx.x + blockIdx.z * 256;
+  if (c >= C) return;
+  const int rows = 64, r0 = blockIdx.x * rows;
+  double a = 0, q = 0;
+  for (int r = r0; r < min(r0 + rows, L); ++r) {
+    const float v = src[((size_t)b * L + r) * ld_in + c];
+    const T t = from_f32<T>(v);
+    dst[((size_t)b * L + r) * ld_out + c] = t;
+    const float w = to_f32(t);
+    a += w;
+    q += (double)w * w;
+  }
+  if (stats) atomic_stats(stats + ((size_t)b * stats_ld + c) * 2, a, q);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_frames_to_f32(const T* __restrict__ src, int L, int C, int ld, float* dst) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= (size_t)L * C) return;
+  const size_t r = i / C, c = i % C;
+  dst[((size_t)b * L + r) * C + c] = to_f32(src[((size_t)b * L + r) * ld + c]);
+}
+
+// ------------------------------------------------------------------ Cin = 1 conv
+// out[b][t][c] = bias[c] + sum_k w[c][k] * in[b][t*stride - pad + k]   (zero padded)
+constexpr int C1_TT = 128;
+template <typename T>
+__global__ void __launch_bounds__(256) k_conv_cin1(const float* __restrict__ in, long long in_bs, int Lin,
+                                                   const float* __restrict__ w, const float* __restrict__ bias,
+                                                   int C, int K, int stride, int pad, int Lout, SmallConvDst d0,
+                                                   SmallConvDst d1, SmallConvDst d2, int ndst) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* win = reinterpret_cast<float*>(smem);
+  const int b = blockIdx.y, t0 = blockIdx.x * C1_TT;
+  const int nwin = (C1_TT - 1) * stride + K;
+  const float* ib = in + (size_t)b * in_bs;
+  for (int i = threadIdx.x; i < nwin; i += 256) {
+    const int g = t0 * stride - pad + i;
+    win[i] = (g >= 0 && g < Lin) ? ib[g] : 0.f;
+  }
+  __syncthreads();
+  const int cstr = C < 256 ? C : 256;
+  const int tsplit = 256 / cstr;
+  const int cl = threadIdx.x % cstr, ts = threadIdx.x / cstr;
+  double* red = reinterpret_cast<double*>(win + ((nwin + 3) & ~3));
+  for (int cb = 0; cb < C; cb += cstr) {
+    const int c = cb + cl;
+    double a = 0, q = 0;
+    if (ts < tsplit) {
+      const float* wc = w + (size_t)c * K;
+      const float bc = bias ? bias[c] : 0.f;
+      for (int tl = ts; tl < C1_TT; tl += tsplit) {
+        const int t = t0 + tl;
+        if (t >= Lout) break;
+        float acc = 0.f;
+        const float* xw = win + tl * stride;
+        for (int k = 0; k < K; ++k) acc = fmaf(wc[k], xw[k], acc);
+        const float v = acc + bc;
+        const SmallConvDst* ds[3] = {&d0, &d1, &d2};
+        float vs = v;
+        for (int di = 0; di < ndst; ++di) {
+          const SmallConvDst& D = *ds[di];
+          const T tv = from_f32<T>(v);
+          reinterpret_cast<T*>(D.y)[(size_t)b * D.y_bs + (size_t)t * D.y_ld + D.c0 + c] = tv;
+          vs = to_f32(tv);
+        }
+        a += vs;
+        q += (double)vs * vs;
+      }
+    }
+    // reduce over ts
+    __syncthreads();
+    if (ts < tsplit) {
+      red[(ts * cstr + cl) * 2] = a;
+      red[(ts * cstr + cl) * 2 + 1] = q;
+    }
+    __syncthreads();
+    if (threadIdx.x < cstr) {
+      double A = 0, Q = 0;
+      for (int s = 0; s < tsplit; ++s) {
+        A += red[(s * cstr + threadIdx.x) * 2];
+        Q += red[(s * cstr + threadIdx.x) * 2 + 1];
+      }
+      const SmallConvDst* ds[3] = {&d0, &d1, &d2};
+      for (int di = 0; di < ndst; ++di)
+        if (ds[di]->stats) atomic_stats(ds[di]->stats + ((size_t)b * ds[di]->stats_ld + ds[di]->c0 + cb + threadIdx.x) * 2, A, Q);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ SineGen
+// reference hifigan.py:117-157: rad = (f0*h/sr) % 1; linear /scale downsample reads two
+// equal samples of the nearest-upsampled curve (src = scale*j + (scale-1)/2), so the
+// downsampled value is rad(f0[j]) exactly; cumsum accumulates in fp64 and rounds per
+// element (PyTorch-CPU semantics); phase = (cum*2)*pi, then *scale.
+__global__ void k_sine_phase(const float* __restrict__ f0, int B, int n, int scale, float* ph) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * 9) return;
+  const int b = i / 9, h = i % 9;
+  const float hm = (float)(h + 1);
+  const float pi_f = (float)3.14159265358979323846;
+  const float sc = (float)scale;
+  double cum = 0.0;
+  for (int j = 0; j < n; ++j) {
+    const float fn = f0[(size_t)b * n + j] * hm;
+    float r = fn / 24000.0f;
+    r = r - floorf(r);
+    cum += (double)r;
+    const float c = (float)cum;
+    ph[((size_t)b * 9 + h) * n + j] = ((c * 2.0f) * pi_f) * sc;
+  }
+}
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+// counter RNG: N(0,1) keyed by (seed, global utterance, sample, harmonic) -> shard invariant
+__device__ __forceinline__ float rng_normal(unsigned long long seed, long long utt, int t, int h) {
+  const unsigned long long key = splitmix64(seed ^ splitmix64((unsigned long long)utt * 0x632BE59BD9B4E019ULL));
+  const unsigned long long z = splitmix64(key + (unsigned long long)t * 9ULL + (unsigned long long)h);
+  const float u1 = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+  const float u2 = (float)((z >> 16) & 0xFFFFFF) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
+
+// reference hifigan.py:155-157 (x scale linear upsample + sin), :189-218 (uv, noise),
+// :254-264 (tanh(Linear 9->1)).  Upsample arithmetic follows PyTorch-CPU bit for bit:
+// src = fma(1/scale, t+0.5, -0.5), out = fma(l0, x0, l1*x1).
+__global__ void __launch_bounds__(256) k_sine_source(const float* __restrict__ f0, const float* __restrict__ ph,
+                                                     int n, int scale, const float* __restrict__ lw,
+                                                     const float* __restrict__ lb, const float* __restrict__ noise,
+                                                     unsigned long long seed, long long utt_offset, float* har) {
+  const int b = blockIdx.y;
+  const int L = n * scale;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L) return;
+  const float inv_sc = (float)(1.0 / (double)scale);
+  int fi = (int)floorf((float)t * inv_sc);
+  if (fi > n - 1) fi = n - 1;
+  const float f0v = f0[(size_t)b * n + fi];
+  const float uv = f0v > 10.0f ? 1.0f : 0.0f;
+  float src = fmaf(inv_sc, (float)t + 0.5f, -0.5f);
+  if (src < 0.f) src = 0.f;
+  const int i0 = (int)src;
+  const int i1 = i0 < n - 1 ? i0 + 1 : i0;
+  const float l1 = src - (float)i0;
+  const float l0 = 1.0f - l1;
+  const float namp = uv * 0.003f + ((1.0f - uv) * 0.1f) / 3.0f;
+  float acc = 0.f;
+  const float* pb = ph + (size_t)b * 9 * n;
+#pragma unroll
+  for (int h = 0; h < 9; ++h) {
+    const float x0 = pb[h * n + i0], x1 = pb[h * n + i1];
+    const float phase = fmaf(l0, x0, l1 * x1);
+    const float sine = sinf(phase) * 0.1f;
+    const float z = noise ? noise[((size_t)b * L + t) * 9 + h] : rng_normal(seed, utt_offset + b, t, h);
+    const float sw = sine * uv + namp * z;
+    acc = fmaf(lw[h], sw, acc);
+  }
+  har[(size_t)b * L + t] = tanhf(acc + lb[0]);
+}
+
+// ------------------------------------------------------------------ depthwise x2 ConvTranspose
+// reference hifigan.py:373 (pool = ConvTranspose1d(C, C, 3, stride 2, groups=C, padding 1,
+// output_padding 1)) applied after AdaIN(norm1) + LReLU(0.2) (hifigan.py:391-393).
+template <typename T>
+__global__ void __launch_bounds__(256) k_pool_dw(const T* __restrict__ x, long long x_bs, int x_ld, int Lin, int C,
+                                                 const float* __restrict__ w, const float* __restrict__ bias,
+                                                 Prologue pro, T* y, long long y_bs, int y_ld) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.z * 256 + threadIdx.x;
+  if (c >= C) return;
+  float m = 0.f, a = 1.f, be = 0.f;
+  if (pro.mode & PRO_AFFINE) adain_coeffs(pro, b, c, m, a, be);
+  auto f = [&](int i) -> float {
+    float v = to_f32(x[(size_t)b * x_bs + (size_t)i * x_ld + c]);
+    if (pro.mode & PRO_AFFINE) v = (v - m) * a + be;
+    if (pro.mode & PRO_LRELU) v = v > 0.f ? v : v * pro.slope;
+    return v;
+  };
+  const float w0 = w[c * 3 + 0], w1 = w[c * 3 + 1], w2 = w[c * 3 + 2], bc = bias[c];
+  const int rows = 16, i0 = blockIdx.x * rows;
+  for (int i = i0; i < min(i0 + rows, Lin); ++i) {
+    const float xi = f(i);
+    // o = 2i:   k=1 from x[i]
+    // o = 2i+1: k=0 from x[i+1] (if any) + k=2 from x[i]
+    const float ve = xi * w1 + bc;
+    float vo = xi * w2;
+    if (i + 1 < Lin) vo = f(i + 1) * w0 + vo;
+    vo = vo + bc;
+    y[(size_t)b * y_bs + (size_t)(2 * i) * y_ld + c] = from_f32<T>(ve);
+    y[(size_t)b * y_bs + (size_t)(2 * i + 1) * y_ld + c] = from_f32<T>(vo);
+  }
+}
+
+// ------------------------------------------------------------------ style projections
+// H[b][n] = bias[n] + sum_k s[b][k] * Wt[k][n]   (Wt packed [K][N] at load)
+__global__ void __launch_bounds__(256) k_linear(const float* __restrict__ s, int B, int K,
+                                                const float* __restrict__ Wt, const float* __restrict__ bias, int N,
+                                                float* H) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int b0 = blockIdx.y * 16;
+  if (n >= N) return;
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float wv = Wt[(size_t)k * N + n];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (b0 + i < B) acc[i] = fmaf(s[(size_t)(b0 + i) * K + k], wv, acc[i]);
+  }
+  const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (b0 + i < B) H[(size_t)(b0 + i) * N + n] = acc[i] + bv;
+}
+
+// ------------------------------------------------------------------ column statistics
+template <typename T>
+__global__ void __launch_bounds__(256) k_frames_stats(const T* __restrict__ x, long long x_bs, int x_ld, int L, int c0,
+                                                      int C, double* stats, int stats_ld) {
+  const int b = blockIdx.y, c = blockIdx.z * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int rows = 256, r0 = blockIdx.x * rows;
+  double a = 0, q = 0;
+  for (int r = r0; r < min(r0 + rows, L); ++r) {
+    const float v = to_f32(x[(size_t)b * x_bs + (size_t)r * x_ld + c0 + c]);
+    a += v;
+    q += (double)v * v;
+  }
+  atomic_stats(stats + ((size_t)b * stats_ld + c0 + c) * 2, a, q);
+}
+
+// ------------------------------------------------------------------ CustomSTFT
+// reference istftnet.py:207-243: replicate pad n_fft/2, DFT-as-conv stride hop,
+// mag = sqrt(re^2 + im^2 + 1e-14), phase = atan2(im, re) with (im==0 & re<0) -> pi.
+template <typename T>
+__global__ void __launch_bounds__(256) k_stft(const float* __restrict__ wave, int L, int n_fft, int hop,
+                                              const float* __restrict__ wr, const float* __restrict__ wi, int F, T* y,
+                                              int ld) {
+  const int nb = n_fft / 2 + 1;
+  const int b = blockIdx.y;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= F * nb) return;
+  const int f = idx / nb, k = idx % nb;
+  const int pad = n_fft / 2;
+  const float* wb = wave + (size_t)b * L;
+  float re = 0.f, im = 0.f;
+  for (int n = 0; n < n_fft; ++n) {
+    int g = f * hop + n - pad;
+    g = g < 0 ? 0 : (g >= L ? L - 1 : g);
+    const float xv = wb[g];
+    re = fmaf(xv, wr[k * n_fft + n], re);
+    im = fmaf(xv, wi[k * n_fft + n], im);
+  }
+  const float mag = sqrtf(re * re + im * im + 1e-14f);
+  float phase = atan2f(im, re);
+  if (im == 0.f && re < 0.f) phase = 3.14159265358979323846f;
+  T* yr = y + ((size_t)b * F + f) * ld;
+  yr[k] = from_f32<T>(mag);
+  yr[nb + k] = from_f32<T>(phase);
+}
+
+// reference istftnet.py:571-573 + 246-293: spec = exp(x[:nb]), phase = sin(x[nb:]);
+// re = spec*cos(phase), im = spec*sin(phase); wave = convT(re, Br) - convT(im, Bi), trim n_fft/2.
+template <typename T>
+__global__ void __launch_bounds__(256) k_istft(const T* __restrict__ post, int F, int ld, int n_fft, int hop,
+                                               const float* __restrict__ br, const float* __restrict__ bi, float* out,
+                                               int L) {
+  const int nb = n_fft / 2 + 1;
+  const int b = blockIdx.y;
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= L) return;
+  const int pos = m + n_fft / 2;
+  int flo = pos - n_fft + 1;
+  flo = flo <= 0 ? 0 : (flo + hop - 1) / hop;
+  int fhi = pos / hop;
+  if (fhi > F - 1) fhi = F - 1;
+  float rr = 0.f, ii = 0.f;
+  for (int f = flo; f <= fhi; ++f) {
+    const int kk = pos - f * hop;
+    const T* xr = post + ((size_t)b * F + f) * ld;
+    for (int k = 0; k < nb; ++k) {
+      const float sp = expf(to_f32(xr[k]));
+      const float phs = sinf(to_f32(xr[nb + k]));
+      rr = fmaf(sp * cosf(phs), br[k * n_fft + kk], rr);
+      ii = fmaf(sp * sinf(phs), bi[k * n_fft + kk], ii);
+    }
+  }
+  out[(size_t)b * L + m] = rr - ii;
+}
+
+// ------------------------------------------------------------------ weight prep
+__global__ void __launch_bounds__(256) k_wn_fold(const float* __restrict__ v, const float* __restrict__ g, int inner,
+                                                 float* wout) {
+  __shared__ double red[256];
+  const int row = blockIdx.x;
+  const float* vr = v + (size_t)row * inner;
+  double a = 0;
+  for (int i = threadIdx.x; i < inner; i += 256) a += (double)vr[i] * vr[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const float factor = g ? g[row] / (float)sqrt(red[0]) : 1.0f;
+  for (int i = threadIdx.x; i < inner; i += 256) wout[(size_t)row * inner + i] = vr[i] * factor;
+}
+
+template <typename MT>
+__global__ void __launch_bounds__(256) k_pack_conv(const float* __restrict__ w, int Cin, int Cout, int K,
+                                                   int transposed, int u, int taps, int nchunks, int N, int Np,
+                                                   MT* out) {
+  const size_t total = (size_t)nchunks * taps * 32 * Np;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  int c, tap, n, kl;
+  if (std::is_same<MT, bf16_t>::value) {  // [chunk][tap][Np][32]
+    kl = (int)(i % 32);
+    size_t r = i / 32;
+    n = (int)(r % Np);
+    r /= Np;
+    tap = (int)(r % taps);
+    c = (int)(r / taps);
+  } else {  // [chunk][tap][32][Np]
+    n = (int)(i % Np);
+    size_t r = i / Np;
+    kl = (int)(r % 32);
+    r /= 32;
+    tap = (int)(r % taps);
+    c = (int)(r / taps);
+  }
+  const int ci = c * 32 + kl;
+  float val = 0.f;
+  if (ci < Cin && n < N) {
+    if (!transposed) {
+      val = w[((size_t)n * Cin + ci) * K + tap];
+    } else {
+      const int p = n / Cout, co = n % Cout;
+      const int k = p + (taps - 1 - tap) * u;
+      if (k < K) val = w[((size_t)ci * Cout + co) * K + k];
+    }
+  }
+  out[i] = (MT)val;
+}
+
+
+// ------------------------------------------------------------------ style encoder (models.py:13-150)
+__device__ __forceinline__ size_t prow(int h, int w, int W) { return (size_t)h * (W + 2) + w; }
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_mel_to_padded(const float* __restrict__ mel, int H, int W, T* dst) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= H * W) return;
+  const int h = i / W, w = i % W;
+  dst[((size_t)b * (H + 2) * (W + 2) + prow(h + 1, w + 1, W)) * 8] = from_f32<T>(mel[(size_t)b * H * W + i]);
+}
+
+// reference models.py:23 LearnedDownSample('half'): depthwise Conv2d k3 s2 p1 (+bias)
+template <typename T>
+__global__ void __launch_bounds__(256) k_dw_s2(const T* __restrict__ x, int H, int W, int C,
+                                               const float* __restrict__ w, const float* __restrict__ bias, T* y) {
+  const int b = blockIdx.z;
+  const int Ho = H / 2, Wo = (W + 1) / 2;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)Ho * Wo * C) return;
+  const int c = (int)(i % C);
+  const size_t pix = i / C;
+  const int oi = (int)(pix / Wo), oj = (int)(pix % Wo);
+  const T* xb = x + (size_t)b * (H + 2) * (W + 2) * C;
+  float acc = 0.f;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+      acc = fmaf(w[c * 9 + dy * 3 + dx], to_f32(xb[prow(2 * oi + dy, 2 * oj + dx, W) * C + c]), acc);
+  y[((size_t)b * (Ho + 2) * (Wo + 2) + prow(oi + 1, oj + 1, Wo)) * C + c] = from_f32<T>(acc + bias[c]);
+}
+
+// reference models.py:58-61 DownSample('half'): odd width -> repeat last column; avg_pool2d(2)
+template <typename T>
+__global__ void __launch_bounds__(256) k_avgpool_half(const T* __restrict__ x, int H, int W, int C, T* y) {
+  const int b = blockIdx.z;
+  const int Ho = H / 2, Wo = (W + 1) / 2;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)Ho * Wo * C) return;
+  const int c = (int)(i % C);
+  const size_t pix = i / C;
+  const int oi = (int)(pix / Wo), oj = (int)(pix % Wo);
+  const T* xb = x + (size_t)b * (H + 2) * (W + 2) * C;
+  const int c0 = 2 * oj, c1 = (2 * oj + 1 < W) ? 2 * oj + 1 : W - 1;  // unpadded columns
+  const float a00 = to_f32(xb[prow(2 * oi + 1, c0 + 1, W) * C + c]);
+  const float a01 = to_f32(xb[prow(2 * oi + 1, c1 + 1, W) * C + c]);
+  const float a10 = to_f32(xb[prow(2 * oi + 2, c0 + 1, W) * C + c]);
+  const float a11 = to_f32(xb[prow(2 * oi + 2, c1 + 1, W) * C + c]);
+  y[((size_t)b * (Ho + 2) * (Wo + 2) + prow(oi + 1, oj + 1, Wo)) * C + c] = from_f32<T>((((a00 + a01) + a10) + a11) / 4.0f);
+}
+
+// reference models.py:139-148: AdaptiveAvgPool2d(1) -> LeakyReLU(0.2) -> view -> Linear
+template <typename T>
+__global__ void __launch_bounds__(256) k_gap_linear(const T* __restrict__ z, int rows, int Wv, int C,
+                                                    const float* __restrict__ w, const float* __restrict__ bias, int N,
+                                                    float* out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* h = reinterpret_cast<float*>(smem);
+  const int b = blockIdx.x;
+  const T* zb = z + (size_t)b * rows * C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f;
+    for (int r = 0; r < Wv; ++r) a += to_f32(zb[(size_t)r * C + c]);
+    a = a / (float)Wv;
+    h[c] = a > 0.f ? a : 0.2f * a;
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < N; n += 256) {
+    float a = 0.f;
+    for (int c = 0; c < C; ++c) a = fmaf(w[(size_t)n * C + c], h[c], a);
+    out[(size_t)b * N + n] = a + bias[n];
+  }
+}
+
+}  // namespace
+
+// ================================================================== launchers
+int st_ncl_to_frames(const float* src, int B, int C, int L, void* dst, int ld, int c0, long long dst_bs,
+                     double* stats, int stats_ld, int dtype, hipStream_t s) {
+  dim3 grid((L + 63) / 64, (C + 63) / 64, B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_ncl_to_frames<T>, grid, dim3(256), 0, s, src, C, L,
+                                              reinterpret_cast<T*>(dst), ld, c0, dst_bs, stats, stats_ld));
+  return (int)hipGetLastError();
+}
+
+int st_frames_convert(const float* src, int B, int L, int C, int ld_in, void* dst, int ld_out, double* stats,
+                      int stats_ld, int dtype, hipStream_t s) {
+  dim3 grid((L + 63) / 64, B, (C + 255) / 256);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_frames_convert<T>, grid, dim3(256), 0, s, src, L, C, ld_in,
+                                              reinterpret_cast<T*>(dst), ld_out, stats, stats_ld));
+  return (int)hipGetLastError();
+}
+
+int st_frames_to_f32(const void* src, int B, int L, int C, int ld, float* dst, int dtype, hipStream_t s) {
+  dim3 grid((unsigned)(((size_t)L * C + 255) / 256), B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_frames_to_f32<T>, grid, dim3(256), 0, s,
+                                              reinterpret_cast<const T*>(src), L, C, ld, dst));
+  return (int)hipGetLastError();
+}
+
+int st_conv_cin1(const float* in, long long in_bs, int Lin, int B, const float* w, const float* bias, int C, int K,
+                 int stride, int pad, int Lout, const SmallConvDst* dst, int ndst, int dtype, hipStream_t s) {
+  if (ndst < 1 || ndst > 3 || C <= 0) return ST_EINVAL;
+  SmallConvDst d[3] = {dst[0], ndst > 1 ? dst[1] : dst[0], ndst > 2 ? dst[2] : dst[0]};
+  const int nwin = (C1_TT - 1) * stride + K;
+  const size_t lds = ((nwin + 3) & ~3) * sizeof(float) + 256 * 2 * sizeof(double);
+  dim3 grid((Lout + C1_TT - 1) / C1_TT, B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cin1<T>, grid, dim3(256), lds, s, in, in_bs, Lin, w, bias, C, K,
+                                              stride, pad, Lout, d[0], d[1], d[2], ndst));
+  return (int)hipGetLastError();
+}
+
+int st_sine_phase(const float* f0, int B, int n, int scale, float* ph, hipStream_t s) {
+  hipLaunchKernelGGL(k_sine_phase, dim3((B * 9 + 63) / 64), dim3(64), 0, s, f0, B, n, scale, ph);
+  return (int)hipGetLastError();
+}
+
+int st_sine_source(const float* f0, const float* ph, int B, int n, int scale, const float* lw, const float* lb,
+                   const float* noise, unsigned long long seed, long long utt_offset, float* har, hipStream_t s) {
+  const int L = n * scale;
+  hipLaunchKernelGGL(k_sine_source, dim3((L + 255) / 256, B), dim3(256), 0, s, f0, ph, n, scale, lw, lb, noise, seed,
+                     utt_offset, har);
+  return (int)hipGetLastError();
+}
+
+int st_pool_dw(const void* x, long long x_bs, int x_ld, int B, int Lin, int C, const float* w, const float* bias,
+               const Prologue& pro, void* y, long long y_bs, int y_ld, int dtype, hipStream_t s) {
+  dim3 grid((Lin + 15) / 16, B, (C + 255) / 256);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_pool_dw<T>, grid, dim3(256), 0, s, reinterpret_cast<const T*>(x),
+                                              x_bs, x_ld, Lin, C, w, bias, pro, reinterpret_cast<T*>(y), y_bs, y_ld));
+  return (int)hipGetLastError();
+}
+
+int st_linear(const float* s, int B, int K, const float* Wt, const float* bias, int N, float* H, hipStream_t st) {
+  hipLaunchKernelGGL(k_linear, dim3((N + 255) / 256, (B + 15) / 16), dim3(256), 0, st, s, B, K, Wt, bias, N, H);
+  return (int)hipGetLastError();
+}
+
+int st_frames_stats(const void* x, long long x_bs, int x_ld, int B, int L, int c0, int C, double* stats, int stats_ld,
+                    int dtype, hipStream_t s) {
+  dim3 grid((L + 255) / 256, B, (C + 255) / 256);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_frames_stats<T>, grid, dim3(256), 0, s,
+                                              reinterpret_cast<const T*>(x), x_bs, x_ld, L, c0, C, stats, stats_ld));
+  return (int)hipGetLastError();
+}
+
+int st_stft(const float* wave, int B, int L, int n_fft, int hop, const float* wr, const float* wi, void* y, int ld,
+            int dtype, hipStream_t s) {
+  const int F = L / hop + 1;
+  const int nb = n_fft / 2 + 1;
+  dim3 grid((F * nb + 255) / 256, B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_stft<T>, grid, dim3(256), 0, s, wave, L, n_fft, hop, wr, wi, F,
+                                              reinterpret_cast<T*>(y), ld));
+  return (int)hipGetLastError();
+}
+
+int st_istft(const void* post, int B, int F, int ld, int n_fft, int hop, const float* br, const float* bi, float* out,
+             int L, int dtype, hipStream_t s) {
+  dim3 grid((L + 255) / 256, B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_istft<T>, grid, dim3(256), 0, s, reinterpret_cast<const T*>(post), F,
+                                              ld, n_fft, hop, br, bi, out, L));
+  return (int)hipGetLastError();
+}
+
+int st_wn_fold(const float* v, const float* g, int d0, int inner, float* wout, hipStream_t s) {
+  hipLaunchKernelGGL(k_wn_fold, dim3(d0), dim3(256), 0, s, v, g, inner, wout);
+  return (int)hipGetLastError();
+}
+
+size_t st_packed_conv_elems(int Cin, int Cout, int K, int transposed, int u) {
+  const int taps = transposed ? (K + u - 1) / u : K;
+  const int N = transposed ? u * Cout : Cout;
+  const int Np = (N + 31) & ~31;
+  const int nchunks = (Cin + 31) / 32;
+  return (size_t)nchunks * taps * 32 * Np;
+}
+
+int st_pack_conv(const float* w, int Cin, int Cout, int K, int transposed, int u, void* out, int dtype,
+                 hipStream_t s) {
+  const int taps = transposed ? (K + u - 1) / u : K;
+  const int N = transposed ? u * Cout : Cout;
+  const int Np = (N + 31) & ~31;
+  const int nchunks = (Cin + 31) / 32;
+  const size_t total = st_packed_conv_elems(Cin, Cout, K, transposed, u);
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (dtype == ST_FP32)
+    hipLaunchKernelGGL(k_pack_conv<float>, grid, dim3(256), 0, s, w, Cin, Cout, K, transposed, u, taps, nchunks, N, Np,
+                       reinterpret_cast<float*>(out));
+  else if (dtype == ST_BF16)
+    hipLaunchKernelGGL(k_pack_conv<bf16_t>, grid, dim3(256), 0, s, w, Cin, Cout, K, transposed, u, taps, nchunks, N,
+                       Np, reinterpret_cast<bf16_t*>(out));
+  else
+    return ST_EDTYPE;
+  return (int)hipGetLastError();
+}
+
+int st_mel_to_padded(const float* mel, int B, int H, int W, void* dst, int dtype, hipStream_t s) {
+  dim3 grid((H * W + 255) / 256, B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mel_to_padded<T>, grid, dim3(256), 0, s, mel, H, W,
+                                              reinterpret_cast<T*>(dst)));
+  return (int)hipGetLastError();
+}
+
+int st_dw_s2(const void* x, int B, int H, int W, int C, const float* w, const float* bias, void* y, int dtype,
+             hipStream_t s) {
+  const size_t n = (size_t)(H / 2) * ((W + 1) / 2) * C;
+  dim3 grid((unsigned)((n + 255) / 256), 1, B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_dw_s2<T>, grid, dim3(256), 0, s, reinterpret_cast<const T*>(x), H, W,
+                                              C, w, bias, reinterpret_cast<T*>(y)));
+  return (int)hipGetLastError();
+}
+
+int st_avgpool_half(const void* x, int B, int H, int W, int C, void* y, int dtype, hipStream_t s) {
+  const size_t n = (size_t)(H / 2) * ((W + 1) / 2) * C;
+  dim3 grid((unsigned)((n + 255) / 256), 1, B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_avgpool_half<T>, grid, dim3(256), 0, s,
+                                              reinterpret_cast<const T*>(x), H, W, C, reinterpret_cast<T*>(y)));
+  return (int)hipGetLastError();
+}
+
+int st_gap_linear(const void* z, int B, int rows, int Wv, int C, const float* w, const float* bias, int N, float* out,
+                  int dtype, hipStream_t s) {
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_gap_linear<T>, dim3(B), dim3(256), C * sizeof(float), s,
+                                              reinterpret_cast<const T*>(z), rows, Wv, C, w, bias, N, out));
+  return (int)hipGetLastError();
+}

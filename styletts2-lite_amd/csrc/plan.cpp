@@ -1,0 +1,1171 @@
+// Model plans (HiFi-GAN / iSTFTNet decoders, F0/N conv stacks, style encoder) and the
+// C-ABI declared in include/stts2.h.  A plan is built from the constructor arguments of the
+// reference module, names every parameter exactly like the reference state dict, packs the
+// weights (weight-norm fold + MFMA layout) into a caller buffer, and strings the gfx950
+// kernels together for one forward.  All launches go to the caller's stream; the workspace
+// is carved by a bump allocator whose dry run gives stts_workspace_bytes().
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/stts2.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr size_t ALIGN = 256;
+inline size_t rup(size_t x, size_t a) { return (x + a - 1) / a * a; }
+inline int rup8(int x) { return (x + 7) & ~7; }
+
+// ----------------------------------------------------------------------- profiling
+struct Prof {
+  bool on = false;
+  std::vector<hipEvent_t> ev;  // pairs
+  size_t used = 0;
+  long long launches = 0;
+  double flops = 0, bytes = 0;
+} g_prof;
+
+// ----------------------------------------------------------------------- parameters
+struct Params {
+  std::vector<std::string> names;
+  std::vector<long long> numel;
+  std::vector<const float*> ptr;
+  int add(const std::string& n, long long k) {
+    names.push_back(n);
+    numel.push_back(k);
+    ptr.push_back(nullptr);
+    return (int)names.size() - 1;
+  }
+  const float* operator[](int i) const { return i < 0 ? nullptr : ptr[i]; }
+};
+
+// A convolution whose weights are packed for conv1d_igemm.
+struct WConv {
+  int v = -1, g = -1, bias = -1;
+  int Cin = 0, Cout = 0, K = 0, transposed = 0, u = 1;
+  size_t off[2] = {0, 0};
+  int taps() const { return transposed ? (K + u - 1) / u : K; }
+  int N() const { return transposed ? u * Cout : Cout; }
+};
+
+struct WAdaIN {
+  int w = -1, b = -1, C = 0, hoff = 0;
+};
+
+struct ResBlock1 {  // AdaINResBlock1 (hifigan.py:26-80)
+  int C = 0, K = 0, dil[3] = {1, 3, 5};
+  WConv c1[3], c2[3];
+  WAdaIN a1[3], a2[3];
+  int al1[3], al2[3];
+};
+
+struct AdainBlk {  // AdainResBlk1d (hifigan.py:359-403)
+  int cin = 0, cout = 0;
+  bool up = false, learned = false;
+  WConv conv1, conv2, sc;
+  WAdaIN n1, n2;
+  int pool_v = -1, pool_g = -1, pool_b = -1;
+  size_t pool_off = 0;  // folded fp32 [cin][3] in the aux area
+};
+
+struct Small {  // weight-norm conv folded to fp32 for a VALU kernel
+  int v = -1, g = -1, bias = -1;
+  long long rows = 0, inner = 0;
+  size_t off = 0;
+};
+
+}  // namespace
+
+struct stts_model {
+  int kind = 0;
+  Params P;
+  // -------- decoder config
+  int dim_in = 512, style_dim = 128, init_ch = 512, n_fft = 0, hop = 0;
+  std::vector<int> rates, kernels, rbk;
+  std::vector<std::vector<int>> rbd;
+  // -------- decoder layers
+  AdainBlk encode, decode[4];
+  Small F0_conv, N_conv;
+  WConv asr_res;
+  int l_lin_w = -1, l_lin_b = -1;
+  std::vector<int> nc_w, nc_b;      // hifigan noise_convs (Cin=1): raw [C][K]
+  std::vector<WConv> nc_conv;       // istftnet noise_convs (Cin=n_fft+2): igemm
+  std::vector<WConv> ups;
+  std::vector<ResBlock1> noise_res, resblocks;
+  std::vector<int> alphas;
+  WConv conv_post;
+  int stft_fr = -1, stft_fi = -1, stft_br = -1, stft_bi = -1;
+  // -------- F0N
+  int d_hid = 512;
+  AdainBlk f0blk[3], nblk[3];
+  WConv f0_proj, n_proj;
+  // -------- style encoder (models.py:125-150)
+  struct SEBlk {
+    int cin = 0, cout = 0;
+    bool learned = false;
+    WConv conv1, conv2, sc;
+    int dw_w = -1, dw_b = -1;
+  } se_blk[4];
+  WConv se_conv0, se_last;
+  int se_lin_w = -1, se_lin_b = -1, se_dim = 0;
+  // -------- AdaIN projections (all AdaIN layers share one GEMV: H = s @ Wt + b)
+  std::vector<WAdaIN*> adains;
+  int Htot = 0;
+  size_t wt_off = 0, bcat_off = 0;  // fp32 Wt [style_dim][Htot], bias [Htot] in the aux area
+  // -------- packing
+  std::vector<WConv*> convs;
+  std::vector<Small*> smalls;
+  std::vector<AdainBlk*> pools;
+  size_t conv_bytes[2] = {0, 0};
+  size_t aux_off[2] = {0, 0}, aux_bytes = 0, scratch_off[2] = {0, 0}, scratch_bytes = 0;
+  size_t total_bytes[2] = {0, 0};
+  const char* packed[2] = {nullptr, nullptr};
+};
+
+namespace {
+
+using Model = stts_model;
+
+// ----------------------------------------------------------------------- builders
+void add_wconv(Model& m, WConv& c, const std::string& p, int cin, int cout, int k, bool wn, bool bias,
+               int transposed = 0, int u = 1, int groups = 1) {
+  c.Cin = cin;
+  c.Cout = cout;
+  c.K = k;
+  c.transposed = transposed;
+  c.u = u;
+  if (bias) c.bias = m.P.add(p + ".bias", cout);
+  if (wn) {
+    c.g = m.P.add(p + ".weight_g", transposed ? cin : cout);
+    c.v = m.P.add(p + ".weight_v", (long long)cin * cout / groups * k);
+  } else {
+    c.v = m.P.add(p + ".weight", (long long)cin * cout / groups * k);
+  }
+  m.convs.push_back(&c);
+}
+
+void add_adain(Model& m, WAdaIN& a, const std::string& p, int C) {
+  a.C = C;
+  a.w = m.P.add(p + ".fc.weight", (long long)2 * C * m.style_dim);
+  a.b = m.P.add(p + ".fc.bias", 2 * C);
+  m.adains.push_back(&a);
+}
+
+void add_resblock1(Model& m, ResBlock1& r, const std::string& p, int C, int K, const int* dil) {
+  r.C = C;
+  r.K = K;
+  for (int j = 0; j < 3; ++j) r.dil[j] = dil[j];
+  for (int j = 0; j < 3; ++j) add_wconv(m, r.c1[j], p + ".convs1." + std::to_string(j), C, C, K, true, true);
+  for (int j = 0; j < 3; ++j) add_wconv(m, r.c2[j], p + ".convs2." + std::to_string(j), C, C, K, true, true);
+  for (int j = 0; j < 3; ++j) add_adain(m, r.a1[j], p + ".adain1." + std::to_string(j), C);
+  for (int j = 0; j < 3; ++j) add_adain(m, r.a2[j], p + ".adain2." + std::to_string(j), C);
+  for (int j = 0; j < 3; ++j) r.al1[j] = m.P.add(p + ".alpha1." + std::to_string(j), C);
+  for (int j = 0; j < 3; ++j) r.al2[j] = m.P.add(p + ".alpha2." + std::to_string(j), C);
+}
+
+void add_adainblk(Model& m, AdainBlk& b, const std::string& p, int cin, int cout, bool up) {
+  b.cin = cin;
+  b.cout = cout;
+  b.up = up;
+  b.learned = cin != cout;
+  add_wconv(m, b.conv1, p + ".conv1", cin, cout, 3, true, true);
+  add_wconv(m, b.conv2, p + ".conv2", cout, cout, 3, true, true);
+  add_adain(m, b.n1, p + ".norm1", cin);
+  add_adain(m, b.n2, p + ".norm2", cout);
+  if (b.learned) add_wconv(m, b.sc, p + ".conv1x1", cin, cout, 1, true, false);
+  if (up) {
+    b.pool_b = m.P.add(p + ".pool.bias", cin);
+    b.pool_g = m.P.add(p + ".pool.weight_g", cin);
+    b.pool_v = m.P.add(p + ".pool.weight_v", (long long)cin * 3);
+    m.pools.push_back(&b);
+  }
+}
+
+void add_small_wn(Model& m, Small& s, const std::string& p, long long rows, long long inner) {
+  s.rows = rows;
+  s.inner = inner;
+  s.bias = m.P.add(p + ".bias", rows);
+  s.g = m.P.add(p + ".weight_g", rows);
+  s.v = m.P.add(p + ".weight_v", rows * inner);
+  m.smalls.push_back(&s);
+}
+
+int build_decoder(Model& m, const int* cfg, int n) {
+  int i = 0;
+  auto take = [&](int& dst) -> bool {
+    if (i >= n) return false;
+    dst = cfg[i++];
+    return true;
+  };
+  int nup = 0, nrb = 0;
+  if (!take(m.dim_in) || !take(m.style_dim) || !take(m.init_ch) || !take(nup) || nup <= 0 || nup > 8) return ST_EINVAL;
+  m.rates.resize(nup);
+  m.kernels.resize(nup);
+  for (auto& r : m.rates)
+    if (!take(r) || r <= 0) return ST_EINVAL;
+  for (auto& k : m.kernels)
+    if (!take(k) || k <= 0) return ST_EINVAL;
+  if (!take(nrb) || nrb <= 0 || nrb > 8) return ST_EINVAL;
+  m.rbk.resize(nrb);
+  m.rbd.assign(nrb, std::vector<int>(3));
+  for (auto& k : m.rbk)
+    if (!take(k) || k <= 0 || k % 2 == 0) return ST_EINVAL;
+  for (auto& d : m.rbd)
+    for (auto& x : d)
+      if (!take(x) || x <= 0) return ST_EINVAL;
+  if (m.kind == STTS_KIND_ISTFTNET) {
+    if (!take(m.n_fft) || !take(m.hop) || m.n_fft <= 0 || m.hop <= 0) return ST_EINVAL;
+  }
+  if (i != n) return ST_EINVAL;
+  if (m.init_ch != 512) return ST_EINVAL;  // decode.3 emits 512 channels (hifigan.py:432)
+  const bool ist = m.kind == STTS_KIND_ISTFTNET;
+  // front-end (hifigan.py:427-440)
+  add_adainblk(m, m.encode, "encode", m.dim_in + 2, 1024, false);
+  for (int k = 0; k < 4; ++k)
+    add_adainblk(m, m.decode[k], "decode." + std::to_string(k), 1024 + 2 + 64, k == 3 ? 512 : 1024, k == 3);
+  add_small_wn(m, m.F0_conv, "F0_conv", 1, 3);
+  add_small_wn(m, m.N_conv, "N_conv", 1, 3);
+  add_wconv(m, m.asr_res, "asr_res.0", m.dim_in, 64, 1, true, true);
+  // generator (hifigan.py:272-319 / istftnet.py:494-540)
+  m.l_lin_w = m.P.add("generator.m_source.l_linear.weight", 9);
+  m.l_lin_b = m.P.add("generator.m_source.l_linear.bias", 1);
+  m.ups.resize(nup);
+  m.noise_res.resize(nup);
+  m.resblocks.resize((size_t)nup * nrb);
+  if (ist) m.nc_conv.resize(nup);
+  static const int d135[3] = {1, 3, 5};
+  for (int s = 0; s < nup; ++s) {
+    const int u = m.rates[s], k = m.kernels[s];
+    const int cin = m.init_ch >> s, c = m.init_ch >> (s + 1);
+    const std::string gp = "generator.";
+    add_wconv(m, m.ups[s], gp + "ups." + std::to_string(s), cin, c, k, true, true, 1, u);
+    int sf = 1;
+    for (int j = s + 1; j < nup; ++j) sf *= m.rates[j];
+    const bool last = s + 1 == nup;
+    const int nk = last ? 1 : 2 * sf;
+    if (ist) {
+      add_wconv(m, m.nc_conv[s], gp + "noise_convs." + std::to_string(s), m.n_fft + 2, c, nk, false, true);
+    } else {
+      m.nc_w.push_back(m.P.add(gp + "noise_convs." + std::to_string(s) + ".weight", (long long)c * nk));
+      m.nc_b.push_back(m.P.add(gp + "noise_convs." + std::to_string(s) + ".bias", c));
+    }
+    add_resblock1(m, m.noise_res[s], gp + "noise_res." + std::to_string(s), c, last ? 11 : 7, d135);
+  }
+  if (!ist) m.alphas.push_back(m.P.add("generator.alphas.0", m.init_ch));
+  for (int s = 0; s < nup; ++s) {
+    const int c = m.init_ch >> (s + 1);
+    if (!ist) m.alphas.push_back(m.P.add("generator.alphas." + std::to_string(s + 1), c));
+    for (int j = 0; j < nrb; ++j)
+      add_resblock1(m, m.resblocks[(size_t)s * nrb + j], "generator.resblocks." + std::to_string(s * nrb + j), c,
+                    m.rbk[j], m.rbd[j].data());
+  }
+  const int clast = m.init_ch >> nup;
+  add_wconv(m, m.conv_post, "generator.conv_post", clast, ist ? m.n_fft + 2 : 1, 7, true, true);
+  if (ist) {
+    const int nb = m.n_fft / 2 + 1;
+    m.P.add("generator.stft.window", m.n_fft);
+    m.stft_fr = m.P.add("generator.stft.weight_forward_real", (long long)nb * m.n_fft);
+    m.stft_fi = m.P.add("generator.stft.weight_forward_imag", (long long)nb * m.n_fft);
+    m.stft_br = m.P.add("generator.stft.weight_backward_real", (long long)nb * m.n_fft);
+    m.stft_bi = m.P.add("generator.stft.weight_backward_imag", (long long)nb * m.n_fft);
+  }
+  return ST_OK;
+}
+
+int build_f0n(Model& m, const int* cfg, int n) {
+  if (n != 2 || cfg[0] <= 0 || cfg[0] % 2 || cfg[1] <= 0) return ST_EINVAL;
+  m.d_hid = cfg[0];
+  m.style_dim = cfg[1];
+  const int d = m.d_hid;
+  const char* br[2] = {"F0", "N"};
+  AdainBlk* blks[2] = {m.f0blk, m.nblk};
+  for (int b = 0; b < 2; ++b) {
+    const std::string p = br[b];
+    add_adainblk(m, blks[b][0], p + ".0", d, d, false);
+    add_adainblk(m, blks[b][1], p + ".1", d, d / 2, true);
+    add_adainblk(m, blks[b][2], p + ".2", d / 2, d / 2, false);
+  }
+  add_wconv(m, m.f0_proj, "F0_proj", d / 2, 1, 1, false, true);
+  add_wconv(m, m.n_proj, "N_proj", d / 2, 1, 1, false, true);
+  return ST_OK;
+}
+
+int build_style(Model& m, const int* cfg, int n) {
+  if (n != 3 || cfg[0] <= 0 || cfg[1] <= 0 || cfg[2] <= 0) return ST_EINVAL;
+  int d = cfg[0];
+  m.style_dim = cfg[1];
+  add_wconv(m, m.se_conv0, "shared.0", 1, d, 9, false, true);
+  for (int i = 0; i < 4; ++i) {
+    auto& b = m.se_blk[i];
+    const int dout = std::min(d * 2, cfg[2]);
+    const std::string p = "shared." + std::to_string(i + 1);
+    b.cin = d;
+    b.cout = dout;
+    b.learned = d != dout;
+    add_wconv(m, b.conv1, p + ".conv1", d, d, 9, false, true);
+    add_wconv(m, b.conv2, p + ".conv2", d, dout, 9, false, true);
+    if (b.learned) add_wconv(m, b.sc, p + ".conv1x1", d, dout, 1, false, false);
+    b.dw_w = m.P.add(p + ".downsample_res.conv.weight", (long long)d * 9);
+    b.dw_b = m.P.add(p + ".downsample_res.conv.bias", d);
+    d = dout;
+  }
+  add_wconv(m, m.se_last, "shared.6", d, d, 25, false, true);
+  m.se_lin_w = m.P.add("unshared.weight", (long long)m.style_dim * d);
+  m.se_lin_b = m.P.add("unshared.bias", m.style_dim);
+  m.se_dim = d;
+  return ST_OK;
+}
+
+void finalize_layout(Model& m) {
+  m.Htot = 0;
+  for (auto* a : m.adains) {
+    a->hoff = m.Htot;
+    m.Htot += 2 * a->C;
+  }
+  for (int dt = 0; dt < 2; ++dt) {
+    const size_t esz = dt == ST_FP32 ? 4 : 2;
+    size_t off = 0;
+    for (auto* c : m.convs) {
+      c->off[dt] = off;
+      off += rup(st_packed_conv_elems(c->Cin, c->Cout, c->K, c->transposed, c->u) * esz, ALIGN);
+    }
+    m.conv_bytes[dt] = off;
+  }
+  // aux fp32 area: AdaIN Wt + bias, folded small convs, pools (dtype independent)
+  size_t a = 0;
+  m.wt_off = a;
+  a += rup((size_t)m.style_dim * m.Htot * 4, ALIGN);
+  m.bcat_off = a;
+  a += rup((size_t)m.Htot * 4, ALIGN);
+  for (auto* s : m.smalls) {
+    s->off = a;
+    a += rup((size_t)s->rows * s->inner * 4, ALIGN);
+  }
+  for (auto* p : m.pools) {
+    p->pool_off = a;
+    a += rup((size_t)p->cin * 3 * 4, ALIGN);
+  }
+  m.aux_bytes = a;
+  size_t sc = 0;
+  for (auto* c : m.convs)
+    if (c->g >= 0) sc = std::max(sc, (size_t)c->Cin * c->Cout * c->K * 4);
+  m.scratch_bytes = rup(sc, ALIGN);
+  for (int dt = 0; dt < 2; ++dt) {
+    m.aux_off[dt] = m.conv_bytes[dt];
+    m.scratch_off[dt] = m.aux_off[dt] + m.aux_bytes;
+    m.total_bytes[dt] = m.scratch_off[dt] + m.scratch_bytes;
+  }
+}
+
+// ----------------------------------------------------------------------- forward context
+struct Buf {
+  char* p = nullptr;
+  long long bs = 0;  // batch stride (elements)
+  int ld = 0, L = 0;
+  void* at(int c0, size_t esz) const { return p + (size_t)c0 * esz; }
+};
+
+struct Ctx {
+  Model* m;
+  int dtype;
+  size_t esz;
+  int B;
+  hipStream_t s;
+  bool dry;
+  char* ws;
+  size_t off = 0;
+  size_t stats_begin = 0, stats_off = 0;
+  float* H = nullptr;
+  const char* packed;
+  char* aux;
+
+  char* alloc(size_t bytes) {
+    char* p = dry ? nullptr : ws + off;
+    off += rup(bytes, ALIGN);
+    return p;
+  }
+  Buf frames(int L, int ld) {
+    Buf b;
+    b.L = L;
+    b.ld = ld;
+    b.bs = (long long)L * ld;
+    b.p = alloc((size_t)B * L * ld * esz);
+    return b;
+  }
+  double* stat(int C) {
+    double* p = dry ? nullptr : reinterpret_cast<double*>(ws + stats_off);
+    stats_off += rup((size_t)B * C * 2 * sizeof(double), ALIGN);
+    return p;
+  }
+  const void* wpk(const WConv& c) const { return packed + c.off[dtype]; }
+  const float* aux_f(size_t o) const { return reinterpret_cast<const float*>(aux + o); }
+  const float* P(int i) const { return m->P[i]; }
+};
+
+#define RUN(expr)                \
+  do {                           \
+    if (!c.dry) {                \
+      int _r = (expr);           \
+      if (_r != 0) return _r;    \
+    }                            \
+  } while (0)
+
+Prologue pro_none() {
+  Prologue p;
+  memset(&p, 0, sizeof(p));
+  return p;
+}
+
+Prologue pro_adain(Ctx& c, const WAdaIN& a, const double* stats, int stats_ld, int L, int extra, int alpha,
+                   float slope) {
+  Prologue p = pro_none();
+  p.mode = PRO_AFFINE | extra;
+  p.stats = stats;
+  p.stats_ld = stats_ld;
+  p.inv_n = 1.0 / (double)L;
+  p.gamma = c.H ? c.H + a.hoff : nullptr;
+  p.gb_ld = c.m->Htot;
+  p.gb_C = a.C;
+  p.alpha = alpha >= 0 ? c.P(alpha) : nullptr;
+  p.slope = slope;
+  return p;
+}
+
+ConvParams conv_base(Ctx& c, const WConv& w, const Buf& x, int c0) {
+  ConvParams p;
+  memset(&p, 0, sizeof(p));
+  p.x = x.at(c0, c.esz);
+  p.x_bs = x.bs;
+  p.x_ld = x.ld;
+  p.Lin = x.L;
+  p.Cin = w.Cin;
+  p.B = c.B;
+  p.KS = w.taps();
+  p.dil = 1;
+  p.stride = 1;
+  p.pad = 0;
+  p.N = w.N();
+  p.w = c.wpk(w);
+  p.nchunks = (w.Cin + 31) / 32;
+  p.bias = c.P(w.bias);
+  p.Cout = w.Cout;
+  p.pro = pro_none();
+  p.up = 1;
+  p.out_scale = 1.0f;
+  return p;
+}
+
+void conv_out(ConvParams& p, Ctx& c, const Buf& y, int c0, int Lout) {
+  p.y = y.at(c0, c.esz);
+  p.y_bs = y.bs;
+  p.y_ld = y.ld;
+  p.Lout = Lout;
+}
+
+int conv_run(Ctx& c, ConvParams& p) {
+  if (c.dry) return 0;
+  const bool prof = g_prof.on;
+  if (prof) {
+    while (g_prof.ev.size() < g_prof.used + 2) {
+      hipEvent_t e;
+      ST_CHECK_HIP(hipEventCreate(&e));
+      g_prof.ev.push_back(e);
+    }
+    ST_CHECK_HIP(hipEventRecord(g_prof.ev[g_prof.used], c.s));
+  }
+  int r = st_conv1d(p, c.dtype, c.s);
+  if (r) return r;
+  if (prof) {
+    ST_CHECK_HIP(hipEventRecord(g_prof.ev[g_prof.used + 1], c.s));
+    g_prof.used += 2;
+    g_prof.launches++;
+    // algorithmic work: a (transposed) conv is 2 * rows * N * Cin * taps flops on its GEMM view
+    g_prof.flops += 2.0 * p.B * (double)p.Lq * p.N * p.Cin * p.KS;
+    double elems = (double)p.B * ((double)p.Lin * p.Cin + (double)p.Lout * p.Cout * (1 + (p.res ? 1 : 0) +
+                                                                                     (p.accb ? 1 : 0)));
+    g_prof.bytes += elems * c.esz + (p.y_f32 ? (double)p.B * p.Lout * p.Cout * (4.0 - c.esz) : 0.0);
+  }
+  return 0;
+}
+
+// AdainResBlk1d forward (hifigan.py:390-403).  x frames (ld, L); output into y at channel c0.
+int adain_blk(Ctx& c, const AdainBlk& k, const Buf& x, int xc0, const double* st_x, int st_x_ld, const Buf& y,
+              int yc0, double* st_y, int st_y_ld, Buf& H1, Buf& SC, Buf& POOL) {
+  const int L = x.L, Lr = k.up ? 2 * L : L;
+  const float slope = 0.2f;
+  // shortcut: conv1x1 at the input rate (nearest x2 commutes with a 1x1 conv)
+  if (k.learned) {
+    ConvParams p = conv_base(c, k.sc, x, xc0);
+    p.Lq = L;
+    Buf sc = SC;
+    sc.ld = k.cout;
+    sc.L = L;
+    sc.bs = (long long)L * k.cout;
+    conv_out(p, c, sc, 0, L);
+    RUN(conv_run(c, p));
+  }
+  // residual: norm1 -> lrelu -> [pool] -> conv1
+  Buf h1 = H1;
+  h1.ld = k.cout;
+  h1.L = Lr;
+  h1.bs = (long long)Lr * k.cout;
+  double* st_h1 = c.stat(k.cout);
+  {
+    ConvParams p;
+    if (k.up) {
+      Buf pool = POOL;
+      pool.ld = rup8(k.cin);
+      pool.L = Lr;
+      pool.bs = (long long)Lr * pool.ld;
+      Prologue pr = pro_adain(c, k.n1, st_x, st_x_ld, L, PRO_LRELU, -1, slope);
+      RUN(st_pool_dw(x.at(xc0, c.esz), x.bs, x.ld, c.B, L, k.cin, c.aux_f(k.pool_off), c.P(k.pool_b), pr, pool.p,
+                     pool.bs, pool.ld, c.dtype, c.s));
+      p = conv_base(c, k.conv1, pool, 0);
+    } else {
+      p = conv_base(c, k.conv1, x, xc0);
+      p.pro = pro_adain(c, k.n1, st_x, st_x_ld, L, PRO_LRELU, -1, slope);
+    }
+    p.pad = 1;
+    p.Lq = Lr;
+    conv_out(p, c, h1, 0, Lr);
+    p.stats = st_h1;
+    p.stats_ld = k.cout;
+    RUN(conv_run(c, p));
+  }
+  // norm2 -> lrelu -> conv2, + shortcut, / sqrt(2)
+  {
+    ConvParams p = conv_base(c, k.conv2, h1, 0);
+    p.pro = pro_adain(c, k.n2, st_h1, k.cout, Lr, PRO_LRELU, -1, slope);
+    p.pad = 1;
+    p.Lq = Lr;
+    conv_out(p, c, y, yc0, Lr);
+    if (k.learned) {
+      p.res = SC.p;
+      p.res_bs = (long long)L * k.cout;
+      p.res_ld = k.cout;
+    } else {
+      p.res = x.at(xc0, c.esz);
+      p.res_bs = x.bs;
+      p.res_ld = x.ld;
+    }
+    p.res_shift = k.up ? 1 : 0;
+    p.out_scale = (float)(1.0 / sqrt(2.0));
+    p.stats = st_y;
+    p.stats_ld = st_y_ld;
+    RUN(conv_run(c, p));
+  }
+  return 0;
+}
+
+enum ResOut { RO_PLAIN = 0, RO_ACC_FIRST, RO_ACC_MID, RO_ACC_LAST };
+
+// AdaINResBlock1 forward (hifigan.py:65-74).  Input X (stats st_x); temps R, XT; the final
+// iteration writes R (RO_PLAIN) or accumulates into ACC (resblock average, hifigan.py:336-342).
+int resblock1(Ctx& c, const ResBlock1& rb, const Buf& X, const double* st_x, Buf& R, Buf& XT, int ro, Buf* ACC,
+              int nk) {
+  const int L = X.L, C = rb.C;
+  const Buf* xc = &X;
+  const double* st_c = st_x;
+  for (int d = 0; d < 3; ++d) {
+    double* st_xt = c.stat(C);
+    {
+      ConvParams p = conv_base(c, rb.c1[d], *xc, 0);
+      p.pro = pro_adain(c, rb.a1[d], st_c, C, L, PRO_SNAKE, rb.al1[d], 0.f);
+      p.dil = rb.dil[d];
+      p.pad = rb.dil[d] * (rb.K - 1) / 2;
+      p.Lq = L;
+      conv_out(p, c, XT, 0, L);
+      p.stats = st_xt;
+      p.stats_ld = C;
+      RUN(conv_run(c, p));
+    }
+    {
+      ConvParams p = conv_base(c, rb.c2[d], XT, 0);
+      p.pro = pro_adain(c, rb.a2[d], st_xt, C, L, PRO_SNAKE, rb.al2[d], 0.f);
+      p.pad = (rb.K - 1) / 2;
+      p.Lq = L;
+      p.res = xc->p;
+      p.res_bs = xc->bs;
+      p.res_ld = xc->ld;
+      const bool final = d == 2;
+      if (final && ro != RO_PLAIN) {
+        conv_out(p, c, *ACC, 0, L);
+        if (ro != RO_ACC_FIRST) {
+          p.accb = ACC->p;
+          p.acc_bs = ACC->bs;
+          p.acc_ld = ACC->ld;
+          if (ro == RO_ACC_LAST) p.acc_div = (float)nk;
+        }
+      } else {
+        conv_out(p, c, R, 0, L);
+        if (!final) {
+          double* st_r = c.stat(C);
+          p.stats = st_r;
+          p.stats_ld = C;
+          st_c = st_r;
+        }
+      }
+      RUN(conv_run(c, p));
+    }
+    xc = &R;
+  }
+  return 0;
+}
+
+// --------------------------------------------------------------------- decoder forward
+struct DecIO {
+  const float *asr, *f0, *n, *s, *noise;
+  unsigned long long seed;
+  long long utt;
+  int T;
+  float* out;
+};
+
+int decoder_forward(Ctx& c, const DecIO& io) {
+  Model& m = *c.m;
+  const int B = c.B, T = io.T;
+  const bool ist = m.kind == STTS_KIND_ISTFTNET;
+  const int nup = (int)m.rates.size(), nrb = (int)m.rbk.size();
+  const int ld_enc = rup8(m.dim_in + 2), ld_cat = rup8(1024 + 2 + 64);
+  const size_t esz = c.esz;
+  // ---------------- allocations (identical in dry and real runs)
+  Buf ENC = c.frames(T, ld_enc);
+  Buf CAT[2] = {c.frames(T, ld_cat), c.frames(T, ld_cat)};
+  Buf H1 = c.frames(2 * T, 1024);
+  Buf SC = c.frames(T, 1024);
+  Buf POOL = c.frames(2 * T, ld_cat);
+  Buf X0 = c.frames(2 * T, 512);
+  c.H = reinterpret_cast<float*>(c.alloc((size_t)B * m.Htot * 4));
+  const int n = 2 * T;
+  int scale = 1;
+  for (int r : m.rates) scale *= r;
+  if (ist) scale *= m.hop;
+  const int L = n * scale;
+  float* PH = reinterpret_cast<float*>(c.alloc((size_t)B * 9 * n * 4));
+  float* HAR = reinterpret_cast<float*>(c.alloc((size_t)B * L * 4));
+  // generator stage geometry
+  std::vector<int> Ls(nup), Cs(nup);
+  long long smax = 0;
+  {
+    int Lc = 2 * T;
+    for (int s = 0; s < nup; ++s) {
+      Lc *= m.rates[s];
+      Ls[s] = Lc + ((ist && s == nup - 1) ? 1 : 0);
+      Cs[s] = m.init_ch >> (s + 1);
+      smax = std::max(smax, (long long)Ls[s] * Cs[s]);
+    }
+  }
+  Buf G[6];
+  for (int i = 0; i < 6; ++i) {
+    G[i].p = c.alloc((size_t)B * smax * esz);
+    G[i].bs = smax;
+  }
+  const int F = ist ? L / m.hop + 1 : 0;
+  const int ld_h = ist ? rup8(m.n_fft + 2) : 0;
+  Buf HARF, POST;
+  if (ist) {
+    HARF = c.frames(F, ld_h);
+    POST = c.frames(F, ld_h);
+  }
+  c.stats_begin = c.stats_off = c.off;  // stats region follows; its size is known after the dry run
+  // ---------------- style projections for every AdaIN layer
+  RUN(st_linear(io.s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
+  // ---------------- front-end (hifigan.py:458-472)
+  double* S_enc = c.stat(ld_enc);
+  RUN(st_ncl_to_frames(io.asr, B, m.dim_in, T, ENC.p, ld_enc, 0, ENC.bs, S_enc, ld_enc, c.dtype, c.s));
+  double* S_cat[4];
+  for (int k = 0; k < 4; ++k) S_cat[k] = c.stat(ld_cat);
+  for (int w = 0; w < 2; ++w) {
+    const Small& sm = w == 0 ? m.F0_conv : m.N_conv;
+    const float* src = w == 0 ? io.f0 : io.n;
+    SmallConvDst d[3];
+    d[0] = {ENC.p, ENC.bs, ld_enc, m.dim_in + w, S_enc, ld_enc};
+    d[1] = {CAT[0].p, CAT[0].bs, ld_cat, 1024 + 64 + w, S_cat[0], ld_cat};
+    d[2] = {CAT[1].p, CAT[1].bs, ld_cat, 1024 + 64 + w, nullptr, 0};
+    RUN(st_conv_cin1(src, n, n, B, c.aux_f(sm.off), c.P(sm.bias), 1, 3, 2, 1, T, d, 3, c.dtype, c.s));
+  }
+  for (int w = 0; w < 2; ++w) {  // asr_res (hifigan.py:438-440, 464) into both concat buffers
+    ConvParams p = conv_base(c, m.asr_res, ENC, 0);
+    p.Lq = T;
+    conv_out(p, c, CAT[w], 1024, T);
+    if (w == 0) {
+      p.stats = S_cat[0] + 1024 * 2;
+      p.stats_ld = ld_cat;
+    }
+    RUN(conv_run(c, p));
+  }
+  if (!c.dry) {  // the constant concat channels share their statistics across the 4 blocks
+    for (int k = 1; k < 4; ++k)
+      ST_CHECK_HIP(hipMemcpy2DAsync(S_cat[k] + 1024 * 2, (size_t)ld_cat * 16, S_cat[0] + 1024 * 2,
+                                    (size_t)ld_cat * 16, 66 * 16, B, hipMemcpyDeviceToDevice, c.s));
+  }
+  ST_CHECK(adain_blk(c, m.encode, ENC, 0, S_enc, ld_enc, CAT[0], 0, S_cat[0], ld_cat, H1, SC, POOL));
+  ST_CHECK(adain_blk(c, m.decode[0], CAT[0], 0, S_cat[0], ld_cat, CAT[1], 0, S_cat[1], ld_cat, H1, SC, POOL));
+  ST_CHECK(adain_blk(c, m.decode[1], CAT[1], 0, S_cat[1], ld_cat, CAT[0], 0, S_cat[2], ld_cat, H1, SC, POOL));
+  ST_CHECK(adain_blk(c, m.decode[2], CAT[0], 0, S_cat[2], ld_cat, CAT[1], 0, S_cat[3], ld_cat, H1, SC, POOL));
+  ST_CHECK(adain_blk(c, m.decode[3], CAT[1], 0, S_cat[3], ld_cat, X0, 0, nullptr, 0, H1, SC, POOL));
+  // ---------------- harmonic source (hifigan.py:323-326 / istftnet.py:544-550)
+  RUN(st_sine_phase(io.f0, B, n, scale, PH, c.s));
+  RUN(st_sine_source(io.f0, PH, B, n, scale, c.P(m.l_lin_w), c.P(m.l_lin_b), io.noise, io.seed, io.utt, HAR, c.s));
+  if (ist) {
+    RUN(st_stft(HAR, B, L, m.n_fft, m.hop, c.P(m.stft_fr), c.P(m.stft_fi), HARF.p, ld_h, c.dtype, c.s));
+  }
+  // ---------------- generator stages
+  Buf xin = X0;
+  int Lcur = 2 * T, Ccur = 512;
+  int accsel = 4;
+  for (int s = 0; s < nup; ++s) {
+    const int u = m.rates[s], C = Cs[s], Ls_ = Ls[s];
+    const bool last = s + 1 == nup;
+    auto view = [&](Buf g) {
+      g.ld = C;
+      g.L = Ls_;
+      g.bs = (long long)Ls_ * C;
+      return g;
+    };
+    Buf NS = view(G[0]), R = view(G[1]), XT = view(G[2]), X = view(G[3]), ACC = view(G[accsel]);
+    // noise branch: noise_convs -> noise_res (hifigan.py:330-331)
+    double* S_ns = c.stat(C);
+    int sf = 1;
+    for (int j = s + 1; j < nup; ++j) sf *= m.rates[j];
+    if (!ist) {
+      SmallConvDst d = {NS.p, NS.bs, C, 0, S_ns, C};
+      const int K = last ? 1 : 2 * sf, st = last ? 1 : sf, pd = last ? 0 : (sf + 1) / 2;
+      RUN(st_conv_cin1(HAR, L, L, B, c.P(m.nc_w[s]), c.P(m.nc_b[s]), C, K, st, pd, Ls_, &d, 1, c.dtype, c.s));
+    } else {
+      Buf hf = HARF;
+      ConvParams p = conv_base(c, m.nc_conv[s], hf, 0);
+      if (!last) {
+        p.stride = sf;
+        p.pad = (sf + 1) / 2;
+      }
+      p.Lq = Ls_;
+      conv_out(p, c, NS, 0, Ls_);
+      p.stats = S_ns;
+      p.stats_ld = C;
+      RUN(conv_run(c, p));
+    }
+    ST_CHECK(resblock1(c, m.noise_res[s], NS, S_ns, R, XT, RO_PLAIN, nullptr, 0));
+    // ups (+ x_source): Snake(alpha_s) / LReLU(0.1) prologue, polyphase ConvTranspose1d
+    double* S_x = c.stat(C);
+    {
+      const WConv& w = m.ups[s];
+      ConvParams p = conv_base(c, w, xin, 0);
+      p.Cin = Ccur;
+      if (!ist) {
+        p.pro.mode = PRO_SNAKE;
+        p.pro.alpha = c.P(m.alphas[s]);
+      } else {
+        p.pro.mode = PRO_LRELU;
+        p.pro.slope = 0.1f;
+      }
+      const int taps = w.taps();
+      const int padT = ist ? (w.K - u) / 2 : u / 2 + u % 2;
+      const int Lout = Lcur * u;
+      p.pad = taps - 1;
+      p.Lq = (Lout - 1 + padT) / u + 1;
+      p.up = u;
+      p.opad = padT;
+      conv_out(p, c, X, 0, Lout);
+      if (ist && last) {
+        p.y_row_off = 1;
+        p.reflect_front = 1;
+      }
+      p.res = R.p;
+      p.res_bs = R.bs;
+      p.res_ld = R.ld;
+      p.stats = S_x;
+      p.stats_ld = C;
+      RUN(conv_run(c, p));
+    }
+    for (int j = 0; j < nrb; ++j) {
+      const int ro = nrb == 1 ? RO_ACC_FIRST : (j == 0 ? RO_ACC_FIRST : (j == nrb - 1 ? RO_ACC_LAST : RO_ACC_MID));
+      ST_CHECK(resblock1(c, m.resblocks[(size_t)s * nrb + j], X, S_x, R, XT, ro, &ACC, nrb));
+    }
+    xin = ACC;
+    Lcur = Ls_;
+    Ccur = C;
+    accsel = accsel == 4 ? 5 : 4;
+  }
+  // ---------------- output head
+  if (!ist) {  // Snake(alpha_last) -> conv_post -> tanh  (hifigan.py:343-345)
+    ConvParams p = conv_base(c, m.conv_post, xin, 0);
+    p.pro.mode = PRO_SNAKE;
+    p.pro.alpha = c.P(m.alphas[nup]);
+    p.pad = 3;
+    p.Lq = Lcur;
+    p.y = io.out;
+    p.y_bs = Lcur;
+    p.y_ld = 1;
+    p.y_f32 = 1;
+    p.Lout = Lcur;
+    p.epi_tanh = 1;
+    RUN(conv_run(c, p));
+  } else {  // LReLU(0.01) -> conv_post -> exp/sin -> CustomSTFT.inverse (istftnet.py:569-573)
+    ConvParams p = conv_base(c, m.conv_post, xin, 0);
+    p.pro.mode = PRO_LRELU;
+    p.pro.slope = 0.01f;
+    p.pad = 3;
+    p.Lq = Lcur;
+    conv_out(p, c, POST, 0, Lcur);
+    RUN(conv_run(c, p));
+    RUN(st_istft(POST.p, B, F, ld_h, m.n_fft, m.hop, c.P(m.stft_br), c.P(m.stft_bi), io.out, L, c.dtype, c.s));
+  }
+  (void)esz;
+  return 0;
+}
+
+// --------------------------------------------------------------------- F0/N forward
+int f0n_forward(Ctx& c, const float* x, const float* s, int T, float* F0, float* Nout) {
+  Model& m = *c.m;
+  const int B = c.B, d = m.d_hid;
+  Buf XL = c.frames(T, d);
+  Buf Y0 = c.frames(T, d), Y1 = c.frames(2 * T, d / 2), Y2 = c.frames(2 * T, d / 2);
+  Buf H1 = c.frames(2 * T, d), SC = c.frames(T, d), POOL = c.frames(2 * T, rup8(d));
+  c.H = reinterpret_cast<float*>(c.alloc((size_t)B * m.Htot * 4));
+  c.stats_begin = c.stats_off = c.off;
+  RUN(st_linear(s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
+  double* S0 = c.stat(d);
+  RUN(st_frames_convert(x, B, T, d, d, XL.p, d, S0, d, c.dtype, c.s));
+  for (int br = 0; br < 2; ++br) {
+    AdainBlk* blk = br == 0 ? m.f0blk : m.nblk;
+    double* S1 = c.stat(d);
+    double* S2 = c.stat(d / 2);
+    ST_CHECK(adain_blk(c, blk[0], XL, 0, S0, d, Y0, 0, S1, d, H1, SC, POOL));
+    ST_CHECK(adain_blk(c, blk[1], Y0, 0, S1, d, Y1, 0, S2, d / 2, H1, SC, POOL));
+    ST_CHECK(adain_blk(c, blk[2], Y1, 0, S2, d / 2, Y2, 0, nullptr, 0, H1, SC, POOL));
+    ConvParams p = conv_base(c, br == 0 ? m.f0_proj : m.n_proj, Y2, 0);
+    p.Lq = 2 * T;
+    p.y = br == 0 ? F0 : Nout;
+    p.y_bs = 2 * T;
+    p.y_ld = 1;
+    p.y_f32 = 1;
+    p.Lout = 2 * T;
+    RUN(conv_run(c, p));
+  }
+  return 0;
+}
+
+// --------------------------------------------------------------------- style forward
+// An image [H][W] is kept zero-padded and row-flattened: row (h+1)*(W+2) + (w+1) holds pixel
+// (h, w).  A 3x3 / pad-1 conv is then the 1-D implicit GEMM with 2-level taps
+// (row_off = W+2, dil = 1) over output rows q = h*(W+2) + w, written at offset W+3, with the
+// two wrap-around columns per image row forced to 0 (they are the next image's padding).
+struct Img {
+  Buf b;
+  int H = 0, W = 0, C = 0;
+};
+
+Img img_alloc(Ctx& c, int H, int W, int C) {
+  Img im;
+  im.H = H;
+  im.W = W;
+  im.C = C;
+  im.b = c.frames((H + 2) * (W + 2), C);
+  return im;
+}
+
+int conv3x3(Ctx& c, const WConv& w, const Img& x, const Img& y, int pro_lrelu, const Img* res) {
+  ConvParams p = conv_base(c, w, x.b, 0);
+  p.KS = 9;
+  p.kw = 3;
+  p.row_off = x.W + 2;
+  p.Lq = x.H * (x.W + 2);
+  p.zc_period = x.W + 2;
+  p.zc_valid = x.W;
+  if (pro_lrelu) {
+    p.pro.mode = PRO_LRELU;
+    p.pro.slope = 0.2f;
+  }
+  p.y = y.b.p ? y.b.p + (size_t)(x.W + 3) * y.C * c.esz : nullptr;
+  p.y_bs = y.b.bs;
+  p.y_ld = y.C;
+  p.Lout = p.Lq;
+  if (res) {
+    p.res = res->b.p ? res->b.p + (size_t)(x.W + 3) * res->C * c.esz : nullptr;
+    p.res_bs = res->b.bs;
+    p.res_ld = res->C;
+    p.out_scale = (float)(1.0 / sqrt(2.0));
+  }
+  return conv_run(c, p);
+}
+
+int style_forward(Ctx& c, const float* mel, int T, float* out) {
+  Model& m = *c.m;
+  const int B = c.B;
+  int H = 80, W = T;
+  Img M = img_alloc(c, H, W, 8);
+  Img A = img_alloc(c, H, W, m.se_conv0.Cout);
+  struct BI {
+    Img t1, d, scf, scp, y;
+  } bi[4];
+  {
+    int h = H, w = W;
+    for (int i = 0; i < 4; ++i) {
+      const auto& k = m.se_blk[i];
+      const int ho = h / 2, wo = (w + 1) / 2;
+      bi[i].t1 = img_alloc(c, h, w, k.cin);
+      bi[i].d = img_alloc(c, ho, wo, k.cin);
+      if (k.learned) bi[i].scf = img_alloc(c, h, w, k.cout);
+      bi[i].scp = img_alloc(c, ho, wo, k.cout);
+      bi[i].y = img_alloc(c, ho, wo, k.cout);
+      h = ho;
+      w = wo;
+    }
+    if (h < 5 || w < 5) return ST_EINVAL;  // conv 5x5 'valid' needs a 5 x 5 map (T >= 65)
+  }
+  const Img& X4 = bi[3].y;
+  const int Wz = X4.W + 2;
+  Buf Z = c.frames(Wz, m.se_dim);
+  const size_t style_end = c.off;
+  c.stats_begin = c.stats_off = c.off;
+  if (!c.dry) ST_CHECK_HIP(hipMemsetAsync(c.ws, 0, style_end, c.s));  // zero image borders
+  RUN(st_mel_to_padded(mel, B, H, W, M.b.p, c.dtype, c.s));
+  RUN(conv3x3(c, m.se_conv0, M, A, 0, nullptr));
+  const Img* x = &A;
+  for (int i = 0; i < 4; ++i) {
+    const auto& k = m.se_blk[i];
+    BI& t = bi[i];
+    if (k.learned) {  // shortcut: conv1x1 over every padded row (borders stay 0: no bias)
+      ConvParams p = conv_base(c, k.sc, x->b, 0);
+      p.Lq = (x->H + 2) * (x->W + 2);
+      conv_out(p, c, t.scf.b, 0, p.Lq);
+      RUN(conv_run(c, p));
+      RUN(st_avgpool_half(t.scf.b.p, B, x->H, x->W, k.cout, t.scp.b.p, c.dtype, c.s));
+    } else {
+      RUN(st_avgpool_half(x->b.p, B, x->H, x->W, k.cin, t.scp.b.p, c.dtype, c.s));
+    }
+    RUN(conv3x3(c, k.conv1, *x, t.t1, 1, nullptr));                                     // lrelu -> conv1
+    RUN(st_dw_s2(t.t1.b.p, B, x->H, x->W, k.cin, c.P(k.dw_w), c.P(k.dw_b), t.d.b.p, c.dtype, c.s));  // dw s2
+    RUN(conv3x3(c, k.conv2, t.d, t.y, 1, &t.scp));                                       // lrelu -> conv2, +sc, /sqrt2
+    x = &t.y;
+  }
+  {  // LeakyReLU -> Conv2d(C, C, 5, 1, 0) over the 5 x W4 map (models.py:137-138)
+    ConvParams p = conv_base(c, m.se_last, X4.b, 0);
+    p.x = X4.b.p ? X4.b.p + (size_t)(X4.W + 3) * X4.C * c.esz : nullptr;
+    p.Lin = (X4.H + 2) * (X4.W + 2) - (X4.W + 3);
+    p.KS = 25;
+    p.kw = 5;
+    p.row_off = X4.W + 2;
+    p.Lq = Wz;
+    p.zc_period = Wz;
+    p.zc_valid = X4.W - 4;
+    p.pro.mode = PRO_LRELU;
+    p.pro.slope = 0.2f;
+    conv_out(p, c, Z, 0, Wz);
+    RUN(conv_run(c, p));
+  }
+  RUN(st_gap_linear(Z.p, B, Wz, X4.W - 4, m.se_dim, c.P(m.se_lin_w), c.P(m.se_lin_b), m.style_dim, out, c.dtype,
+                    c.s));
+  return 0;
+}
+
+// --------------------------------------------------------------------- packing
+int pack_model(Model& m, int dt, char* base, hipStream_t s) {
+  char* aux = base + m.aux_off[dt];
+  float* scratch = reinterpret_cast<float*>(base + m.scratch_off[dt]);
+  for (auto* c : m.convs) {
+    const float* v = m.P[c->v];
+    const float* src = v;
+    if (c->g >= 0) {
+      const int rows = c->transposed ? c->Cin : c->Cout;
+      const long long inner = (long long)c->Cin * c->Cout * c->K / rows;
+      ST_CHECK(st_wn_fold(v, m.P[c->g], rows, (int)inner, scratch, s));
+      src = scratch;
+    }
+    ST_CHECK(st_pack_conv(src, c->Cin, c->Cout, c->K, c->transposed, c->u, base + c->off[dt], dt, s));
+  }
+  // AdaIN projections: Wt[k][hoff + n] = fc.weight[n][k]; bias concat
+  float* Wt = reinterpret_cast<float*>(aux + m.wt_off);
+  float* bc = reinterpret_cast<float*>(aux + m.bcat_off);
+  for (auto* a : m.adains) {
+    ST_CHECK(st_ncl_to_frames(m.P[a->w], 1, 2 * a->C, m.style_dim, Wt, m.Htot, a->hoff, 0, nullptr, 0, ST_FP32, s));
+    ST_CHECK_HIP(hipMemcpyAsync(bc + a->hoff, m.P[a->b], (size_t)2 * a->C * 4, hipMemcpyDeviceToDevice, s));
+  }
+  for (auto* sm : m.smalls)
+    ST_CHECK(st_wn_fold(m.P[sm->v], m.P[sm->g], (int)sm->rows, (int)sm->inner,
+                        reinterpret_cast<float*>(aux + sm->off), s));
+  for (auto* p : m.pools)
+    ST_CHECK(st_wn_fold(m.P[p->pool_v], m.P[p->pool_g], p->cin, 3, reinterpret_cast<float*>(aux + p->pool_off), s));
+  return 0;
+}
+
+int check_params(const Model& m) {
+  for (size_t i = 0; i < m.P.ptr.size(); ++i)
+    if (!m.P.ptr[i]) return ST_EPARAMS;
+  return 0;
+}
+
+template <typename F>
+int with_ctx(Model* m, int dtype, int B, void* ws, long long ws_bytes, void* stream, F&& body, size_t* need) {
+  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  Ctx c{m, dtype, (size_t)(dtype == ST_FP32 ? 4 : 2), B, (hipStream_t)stream, true, nullptr};
+  c.packed = m->packed[dtype];
+  c.aux = m->packed[dtype] ? const_cast<char*>(m->packed[dtype]) + m->aux_off[dtype] : nullptr;
+  ST_CHECK(body(c));  // dry run: layout
+  const size_t total = c.stats_off;
+  if (need) {
+    *need = total;
+    return 0;
+  }
+  if (!m->packed[dtype]) return ST_ENOTPACKED;
+  if ((long long)total > ws_bytes || !ws) return ST_EWORKSPACE;
+  const size_t stats_begin = c.stats_begin;
+  Ctx r{m, dtype, c.esz, B, (hipStream_t)stream, false, reinterpret_cast<char*>(ws)};
+  r.packed = c.packed;
+  r.aux = c.aux;
+  if (total > stats_begin) ST_CHECK_HIP(hipMemsetAsync(r.ws + stats_begin, 0, total - stats_begin, r.s));
+  return body(r);
+}
+
+}  // namespace
+
+// ======================================================================= C-ABI
+extern "C" {
+
+int stts_model_create(int kind, const int* cfg, int ncfg, stts_model** out) {
+  if (!out || (ncfg > 0 && !cfg)) return ST_EINVAL;
+  *out = nullptr;
+  Model* m = new Model();
+  m->kind = kind;
+  int r = ST_EINVAL;
+  if (kind == STTS_KIND_HIFIGAN || kind == STTS_KIND_ISTFTNET)
+    r = build_decoder(*m, cfg, ncfg);
+  else if (kind == STTS_KIND_F0N)
+    r = build_f0n(*m, cfg, ncfg);
+  else if (kind == STTS_KIND_STYLE)
+    r = build_style(*m, cfg, ncfg);
+  if (r != 0) {
+    delete m;
+    return r;
+  }
+  finalize_layout(*m);
+  *out = m;
+  return 0;
+}
+
+void stts_model_destroy(stts_model* m) { delete m; }
+
+int stts_param_count(const stts_model* m) { return m ? (int)m->P.names.size() : ST_EINVAL; }
+
+const char* stts_param_name(const stts_model* m, int i) {
+  if (!m || i < 0 || i >= (int)m->P.names.size()) return nullptr;
+  return m->P.names[i].c_str();
+}
+
+long long stts_param_numel(const stts_model* m, int i) {
+  if (!m || i < 0 || i >= (int)m->P.names.size()) return ST_EINVAL;
+  return m->P.numel[i];
+}
+
+int stts_set_param(stts_model* m, int i, const float* p) {
+  if (!m || i < 0 || i >= (int)m->P.names.size()) return ST_EINVAL;
+  m->P.ptr[i] = p;
+  m->packed[0] = m->packed[1] = nullptr;  // weights changed: repack required
+  return 0;
+}
+
+long long stts_packed_bytes(const stts_model* m, int dtype) {
+  if (!m) return ST_EINVAL;
+  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  return (long long)m->total_bytes[dtype];
+}
+
+int stts_pack(stts_model* m, int dtype, void* packed, long long bytes, void* stream) {
+  if (!m || !packed) return ST_EINVAL;
+  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  if (bytes < (long long)m->total_bytes[dtype]) return ST_EWORKSPACE;
+  ST_CHECK(check_params(*m));
+  ST_CHECK(pack_model(*m, dtype, reinterpret_cast<char*>(packed), (hipStream_t)stream));
+  m->packed[dtype] = reinterpret_cast<const char*>(packed);
+  return 0;
+}
+
+long long stts_workspace_bytes(const stts_model* mc, int dtype, int B, int T) {
+  if (!mc || B <= 0 || T <= 0) return ST_EINVAL;
+  Model* m = const_cast<Model*>(mc);
+  size_t need = 0;
+  int r;
+  if (m->kind == STTS_KIND_HIFIGAN || m->kind == STTS_KIND_ISTFTNET) {
+    DecIO io{};
+    io.T = T;
+    r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return decoder_forward(c, io); }, &need);
+  } else if (m->kind == STTS_KIND_F0N) {
+    r = with_ctx(m, dtype, B, nullptr, 0, nullptr,
+                 [&](Ctx& c) { return f0n_forward(c, nullptr, nullptr, T, nullptr, nullptr); }, &need);
+  } else {
+    r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return style_forward(c, nullptr, T, nullptr); },
+                 &need);
+  }
+  return r ? r : (long long)need;
+}
+
+int stts_decoder_fwd(stts_model* m, int dtype, const float* asr, const float* f0, const float* n, const float* s,
+                     const float* noise, unsigned long long seed, long long utt_offset, int B, int T, float* out,
+                     void* ws, long long ws_bytes, void* stream) {
+  if (!m || (m->kind != STTS_KIND_HIFIGAN && m->kind != STTS_KIND_ISTFTNET)) return ST_EINVAL;
+  if (B <= 0 || T <= 0 || !asr || !f0 || !n || !s || !out) return ST_EINVAL;
+  ST_CHECK(check_params(*m));
+  DecIO io{asr, f0, n, s, noise, seed, utt_offset, T, out};
+  return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return decoder_forward(c, io); }, nullptr);
+}
+
+int stts_f0n_fwd(stts_model* m, int dtype, const float* x, const float* s, int B, int T, float* F0, float* N,
+                 void* ws, long long ws_bytes, void* stream) {
+  if (!m || m->kind != STTS_KIND_F0N) return ST_EINVAL;
+  if (B <= 0 || T <= 0 || !x || !s || !F0 || !N) return ST_EINVAL;
+  ST_CHECK(check_params(*m));
+  return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return f0n_forward(c, x, s, T, F0, N); },
+                  nullptr);
+}
+
+int stts_style_fwd(stts_model* m, int dtype, const float* mel, int B, int T, float* out, void* ws, long long ws_bytes,
+                   void* stream) {
+  if (!m || m->kind != STTS_KIND_STYLE) return ST_EINVAL;
+  if (B <= 0 || T <= 0 || !mel || !out) return ST_EINVAL;
+  ST_CHECK(check_params(*m));
+  return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return style_forward(c, mel, T, out); }, nullptr);
+}
+
+const char* stts_error_string(int code) {
+  switch (code) {
+    case 0: return "ok";
+    case ST_EINVAL: return "invalid argument or shape";
+    case ST_EDTYPE: return "unsupported dtype";
+    case ST_EPARAMS: return "parameter table incomplete";
+    case ST_EWORKSPACE: return "workspace / buffer too small";
+    case ST_ENOTPACKED: return "weights not packed for this dtype";
+    default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
+  }
+}
+
+int stts_profile_enable(int on) {
+  g_prof.on = on != 0;
+  g_prof.used = 0;
+  g_prof.launches = 0;
+  g_prof.flops = g_prof.bytes = 0;
+  return 0;
+}
+
+int stts_profile_read(double* total_ms, long long* launches, double* alg_flops, double* alg_bytes) {
+  double t = 0;
+  for (size_t i = 0; i + 1 < g_prof.used; i += 2) {
+    float ms = 0;
+    ST_CHECK_HIP(hipEventSynchronize(g_prof.ev[i + 1]));
+    ST_CHECK_HIP(hipEventElapsedTime(&ms, g_prof.ev[i], g_prof.ev[i + 1]));
+    t += ms;
+  }
+  if (total_ms) *total_ms = t;
+  if (launches) *launches = g_prof.launches;
+  if (alg_flops) *alg_flops = g_prof.flops;
+  if (alg_bytes) *alg_bytes = g_prof.bytes;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,278 @@
+"""ctypes binding of libstts2.so (include/stts2.h) and the per-module engines.
+
+PyTorch is used only as the device-memory / stream container: parameters are the
+module's own state-dict tensors on the HIP device, the packed-weight buffer and the
+workspace are torch uint8 tensors, and every kernel is launched by the C library on
+`torch.cuda.current_stream()`.  There is no compute fallback: without the library or
+a HIP device every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+KIND_HIFIGAN, KIND_ISTFTNET, KIND_F0N, KIND_STYLE = 0, 1, 2, 3
+DTYPES = {"fp32": 0, "bf16": 1}
+
+_LIB = None
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libstts2.so")
+
+c_int, c_ll, c_ull, c_vp, c_fp = ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_void_p, ctypes.c_void_p
+
+
+def lib():
+    """Load libstts2.so (after torch, so both share torch's HIP runtime)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} missing: build it with `python -m stts2_mi355x.build` "
+                           "(__graft_entry__.build()); there is no non-HIP fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    L.stts_model_create.argtypes = [c_int, ctypes.POINTER(c_int), c_int, ctypes.POINTER(c_vp)]
+    L.stts_model_create.restype = c_int
+    L.stts_model_destroy.argtypes = [c_vp]
+    L.stts_model_destroy.restype = None
+    L.stts_param_count.argtypes = [c_vp]
+    L.stts_param_count.restype = c_int
+    L.stts_param_name.argtypes = [c_vp, c_int]
+    L.stts_param_name.restype = ctypes.c_char_p
+    L.stts_param_numel.argtypes = [c_vp, c_int]
+    L.stts_param_numel.restype = c_ll
+    L.stts_set_param.argtypes = [c_vp, c_int, c_vp]
+    L.stts_set_param.restype = c_int
+    L.stts_packed_bytes.argtypes = [c_vp, c_int]
+    L.stts_packed_bytes.restype = c_ll
+    L.stts_pack.argtypes = [c_vp, c_int, c_vp, c_ll, c_vp]
+    L.stts_pack.restype = c_int
+    L.stts_workspace_bytes.argtypes = [c_vp, c_int, c_int, c_int]
+    L.stts_workspace_bytes.restype = c_ll
+    L.stts_decoder_fwd.argtypes = [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_ull, c_ll, c_int, c_int, c_vp, c_vp,
+                                   c_ll, c_vp]
+    L.stts_decoder_fwd.restype = c_int
+    L.stts_f0n_fwd.argtypes = [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_ll, c_vp]
+    L.stts_f0n_fwd.restype = c_int
+    L.stts_style_fwd.argtypes = [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_ll, c_vp]
+    L.stts_style_fwd.restype = c_int
+    L.stts_error_string.argtypes = [c_int]
+    L.stts_error_string.restype = ctypes.c_char_p
+    L.stts_profile_enable.argtypes = [c_int]
+    L.stts_profile_enable.restype = c_int
+    L.stts_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_ll),
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    L.stts_profile_read.restype = c_int
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str = "stts"):
+    if rc != 0:
+        msg = lib().stts_error_string(rc).decode()
+        raise RuntimeError(f"{what} failed: {msg} (code {rc})")
+
+
+def _require_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("stts2_mi355x needs a HIP device (MI355X / gfx950); no CPU fallback exists")
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _dev_f32(t, device):
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(np.asarray(t))
+    return t.detach().to(device=device, dtype=torch.float32).contiguous()
+
+
+class NativeModel:
+    """One stts_model handle: parameters bound by reference state-dict name, packed per dtype."""
+
+    def __init__(self, kind: int, cfg, module: torch.nn.Module):
+        _require_device()
+        L = lib()
+        self.kind = kind
+        arr = (c_int * len(cfg))(*[int(v) for v in cfg])
+        h = c_vp()
+        check(L.stts_model_create(kind, arr, len(cfg), ctypes.byref(h)), "stts_model_create")
+        self.h = h
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        sd = module.state_dict()
+        n = L.stts_param_count(h)
+        self.names, self._keep = [], []
+        for i in range(n):
+            name = L.stts_param_name(h, i).decode()
+            if name not in sd:
+                raise KeyError(f"parameter {name} expected by the native plan is not in the module state dict")
+            t = _dev_f32(sd[name], self.device)
+            if t.numel() != L.stts_param_numel(h, i):
+                raise ValueError(f"{name}: numel {t.numel()} != plan {L.stts_param_numel(h, i)}")
+            self._keep.append(t)
+            self.names.append(name)
+            check(L.stts_set_param(h, i, _ptr(t)), "stts_set_param")
+        self._packed = {}
+        self._ws = {}
+
+    def pack(self, dtype: str):
+        if dtype not in self._packed:
+            L = lib()
+            dt = DTYPES[dtype]
+            nb = L.stts_packed_bytes(self.h, dt)
+            if nb < 0:
+                check(int(nb), "stts_packed_bytes")
+            buf = torch.empty(max(int(nb), 1), dtype=torch.uint8, device=self.device)
+            check(L.stts_pack(self.h, dt, _ptr(buf), int(nb), _stream()), "stts_pack")
+            self._packed[dtype] = buf
+        return self._packed[dtype]
+
+    def workspace(self, dtype: str, B: int, T: int):
+        L = lib()
+        nb = L.stts_workspace_bytes(self.h, DTYPES[dtype], int(B), int(T))
+        if nb < 0:
+            check(int(nb), "stts_workspace_bytes")
+        cur = self._ws.get(dtype)
+        if cur is None or cur.numel() < nb:
+            self._ws[dtype] = cur = torch.empty(max(int(nb), 1), dtype=torch.uint8, device=self.device)
+        return cur, int(nb)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _LIB is not None:
+                _LIB.stts_model_destroy(self.h)
+        except Exception:
+            pass
+
+
+def _watch(module, engine_attr="_engine"):
+    """Drop a module's cached engine whenever new weights are loaded."""
+    if getattr(module, "_stts_hooked", False):
+        return
+
+    def hook(mod, incompatible):
+        setattr(mod, engine_attr, None)
+    module.register_load_state_dict_post_hook(hook)
+    module._stts_hooked = True
+
+
+class _Engine:
+    def __init__(self, module, dtype):
+        if dtype not in DTYPES:
+            raise ValueError(f"dtype must be one of {list(DTYPES)}")
+        self.dtype = dtype
+        _watch(module)
+
+    def stale(self, module):
+        return False
+
+
+class DecoderEngine(_Engine):
+    """HIP forward of Modules/hifigan.py / istftnet.py Decoder (reference :446 / :692)."""
+
+    def __init__(self, module, dtype="fp32"):
+        super().__init__(module, dtype)
+        g = module.generator
+        kind = KIND_ISTFTNET if module.decoder_type == "istftnet" else KIND_HIFIGAN
+        cfg = [module.dim_in, module.style_dim, g.upsample_initial_channel, len(g.upsample_rates),
+               *g.upsample_rates, *g.upsample_kernel_sizes, len(g.resblock_kernel_sizes),
+               *g.resblock_kernel_sizes, *[d for ds in g.resblock_dilation_sizes for d in ds]]
+        if kind == KIND_ISTFTNET:
+            cfg += [g.gen_istft_n_fft, g.gen_istft_hop_size]
+        self.kind = kind
+        self.scale = g.upsample_scale
+        self.dim_in, self.style_dim = module.dim_in, module.style_dim
+        self.model = NativeModel(kind, cfg, module)
+        self.model.pack(dtype)
+
+    def forward(self, asr, F0_curve, N, s, noise=None, seed=0, utt_offset=0, out=None):
+        dev = self.model.device
+        in_dev = asr.device if isinstance(asr, torch.Tensor) else torch.device("cpu")
+        asr, F0_curve, N, s = (_dev_f32(t, dev) for t in (asr, F0_curve, N, s))
+        B, C, T = asr.shape
+        if C != self.dim_in or tuple(F0_curve.shape) != (B, 2 * T) or tuple(N.shape) != (B, 2 * T) \
+                or tuple(s.shape) != (B, self.style_dim):
+            raise ValueError(f"decoder inputs: asr {tuple(asr.shape)}, F0 {tuple(F0_curve.shape)}, "
+                             f"N {tuple(N.shape)}, s {tuple(s.shape)}")
+        Lw = 2 * T * self.scale
+        if noise is not None:
+            noise = _dev_f32(noise, dev)
+            if tuple(noise.shape) != (B, Lw, 9):
+                raise ValueError(f"noise must be [B, {Lw}, 9], got {tuple(noise.shape)}")
+        if out is None:
+            out = torch.empty(B, 1, Lw, dtype=torch.float32, device=dev)
+        ws, nb = self.model.workspace(self.dtype, B, T)
+        rc = lib().stts_decoder_fwd(self.model.h, DTYPES[self.dtype], _ptr(asr), _ptr(F0_curve), _ptr(N), _ptr(s),
+                                    _ptr(noise), int(seed) & (2 ** 64 - 1), int(utt_offset), B, T, _ptr(out),
+                                    _ptr(ws), nb, _stream())
+        check(rc, "stts_decoder_fwd")
+        return out if in_dev.type == "cuda" else out.to(in_dev)
+
+
+class F0NEngine(_Engine):
+    """HIP forward of ProsodyPredictor.F0Ntrain's conv stacks (reference models.py:451-461)."""
+
+    def __init__(self, module, dtype="fp32"):
+        super().__init__(module, dtype)
+        self.d_hid, self.style_dim = module.d_hid, module.style_dim
+        self.model = NativeModel(KIND_F0N, [module.d_hid, module.style_dim], module)
+        self.model.pack(dtype)
+
+    def forward_nlc(self, x, s):
+        """x: shared-LSTM output [B, T, d_hid] (batch_first); s [B, style_dim] -> (F0, N) [B, 2T]."""
+        dev = self.model.device
+        in_dev = x.device
+        x, s = _dev_f32(x, dev), _dev_f32(s, dev)
+        B, T, D = x.shape
+        if D != self.d_hid or tuple(s.shape) != (B, self.style_dim):
+            raise ValueError(f"F0Ntrain inputs: x {tuple(x.shape)}, s {tuple(s.shape)}")
+        F0 = torch.empty(B, 2 * T, dtype=torch.float32, device=dev)
+        Nn = torch.empty(B, 2 * T, dtype=torch.float32, device=dev)
+        ws, nb = self.model.workspace(self.dtype, B, T)
+        check(lib().stts_f0n_fwd(self.model.h, DTYPES[self.dtype], _ptr(x), _ptr(s), B, T, _ptr(F0), _ptr(Nn),
+                                 _ptr(ws), nb, _stream()), "stts_f0n_fwd")
+        if in_dev.type != "cuda":
+            return F0.to(in_dev), Nn.to(in_dev)
+        return F0, Nn
+
+
+class StyleEngine(_Engine):
+    """HIP forward of models.py StyleEncoder (reference models.py:145-150)."""
+
+    def __init__(self, module, dtype="fp32"):
+        super().__init__(module, dtype)
+        d_in = module.shared[0].cout
+        self.style_dim = module.style_dim
+        max_conv = max(d for _, d in module.dims)
+        self.model = NativeModel(KIND_STYLE, [d_in, module.style_dim, max_conv], module)
+        self.model.pack(dtype)
+
+    def forward(self, mel):
+        dev = self.model.device
+        in_dev = mel.device
+        mel = _dev_f32(mel, dev)
+        B, one, M, T = mel.shape
+        if one != 1 or M != 80:
+            raise ValueError(f"mel must be [B, 1, 80, T], got {tuple(mel.shape)}")
+        out = torch.empty(B, self.style_dim, dtype=torch.float32, device=dev)
+        ws, nb = self.model.workspace(self.dtype, B, T)
+        check(lib().stts_style_fwd(self.model.h, DTYPES[self.dtype], _ptr(mel), B, T, _ptr(out), _ptr(ws), nb,
+                                   _stream()), "stts_style_fwd")
+        return out if in_dev.type == "cuda" else out.to(in_dev)
+
+
+def profile_enable(on: bool = True):
+    check(lib().stts_profile_enable(1 if on else 0))
+
+
+def profile_read():
+    t, n, f, b = ctypes.c_double(), c_ll(), ctypes.c_double(), ctypes.c_double()
+    check(lib().stts_profile_read(ctypes.byref(t), ctypes.byref(n), ctypes.byref(f), ctypes.byref(b)))
+    return {"ms": t.value, "launches": n.value, "flops": f.value, "bytes": b.value}

@@ -1,0 +1,87 @@
+"""GPU: the conv1d_igemm engine (one launch through the stts_test_conv1d hook) against
+torch.nn.functional fp32 on the CPU: dilation, stride, polyphase ConvTranspose1d,
+AdaIN/Snake/LReLU prologues, residual + scale epilogue and the InstanceNorm statistics."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from stts2_mi355x import engine as E
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # name, Cin, Cout, K, transposed, stride(u), dil, pad, out_pad, L, pro
+    ("rb32_k11_d5", 32, 32, 11, 0, 1, 5, 25, 0, 700, 3),
+    ("rb64_k7_d3", 64, 64, 7, 0, 1, 3, 9, 0, 333, 3),
+    ("rb128_k3_d1", 128, 128, 3, 0, 1, 1, 1, 0, 257, 3),
+    ("rb256_k11_d1", 256, 256, 11, 0, 1, 1, 5, 0, 130, 3),
+    ("front_1090_1024", 1090, 1024, 3, 0, 1, 1, 1, 0, 40, 5),
+    ("sc_1x1", 514, 1024, 1, 0, 1, 1, 0, 0, 37, 0),
+    ("istft_noise_s6", 22, 256, 12, 0, 6, 1, 3, 0, 481, 0),
+    ("post_32_1", 32, 1, 7, 0, 1, 1, 3, 0, 999, 2),
+    ("ups0_u10", 512, 256, 20, 1, 10, 1, 5, 0, 23, 2),
+    ("ups1_u5", 256, 128, 10, 1, 5, 1, 3, 1, 31, 2),
+    ("ups2_u3", 128, 64, 6, 1, 3, 1, 2, 1, 40, 4),
+    ("ups3_u2", 64, 32, 4, 1, 2, 1, 1, 0, 77, 2),
+    ("istft_ups1_u6", 256, 128, 12, 1, 6, 1, 3, 0, 50, 4),
+]
+
+
+def reference(x, w, b, gb, alpha, slope, res, scale, c):
+    name, Cin, Cout, K, tr, st, dil, pad, op, L, pro = c
+    v = x.transpose(1, 2)  # [B, Cin, L]
+    if pro & 1:
+        n = F.instance_norm(v, eps=1e-5)
+        g, be = gb[:, :Cin, None], gb[:, Cin:, None]
+        v = (1 + g) * n + be
+    if pro & 2:
+        a = alpha[None, :, None]
+        v = v + (1 / a) * torch.sin(a * v) ** 2
+    if pro & 4:
+        v = F.leaky_relu(v, slope)
+    if tr:
+        y = F.conv_transpose1d(v, w, b, st, pad, op)
+    else:
+        y = F.conv1d(v, w, b, st, pad, dil)
+    y = y.transpose(1, 2)
+    if res is not None:
+        y = y + res
+    return y * scale
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_conv_engine(case, dtype):
+    name, Cin, Cout, K, tr, st, dil, pad, op, L, pro = case
+    g = torch.Generator().manual_seed(hash(name) % 1000)
+    B = 2
+    x = torch.randn(B, L, Cin, generator=g) * 1.5 + 0.3
+    w = torch.randn(*((Cin, Cout, K) if tr else (Cout, Cin, K)), generator=g) / np.sqrt(Cin * K / (st if tr else 1))
+    b = torch.randn(Cout, generator=g) * 0.1
+    gb = torch.randn(B, 2 * Cin, generator=g) * 0.3
+    alpha = torch.rand(Cin, generator=g) + 0.5
+    slope = 0.2
+    Lout = (L - 1) * st - 2 * pad + K + op if tr else (L + 2 * pad - dil * (K - 1) - 1) // st + 1
+    res = torch.randn(B, Lout, Cout, generator=g) if not tr else None
+    scale = 0.70710677 if res is not None else 1.0
+    ref = reference(x, w, b, gb, alpha, slope, res, scale, case)
+    dev = "cuda"
+    xd, wd, bd, gbd, ad = (t.to(dev).contiguous() for t in (x, w, b, gb, alpha))
+    rd = res.to(dev).contiguous() if res is not None else None
+    y = torch.empty(B, Lout, Cout, device=dev)
+    st_out = torch.zeros(B, Cout, 2, dtype=torch.float64, device=dev)
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)  # noqa: E731
+    rc = E.lib().stts_test_conv1d(E.DTYPES[dtype], P(xd), B, L, Cin, P(wd), P(bd), Cout, K, tr, st, dil, pad, op,
+                                  pro, P(gbd), P(ad), ctypes.c_float(slope), P(rd), ctypes.c_float(scale), P(y), Lout,
+                                  P(st_out))
+    E.check(rc)
+    y = y.cpu()
+    err = (y - ref).abs().max().item()
+    tol = 2e-4 if dtype == "fp32" else 0.03 * max(1.0, ref.abs().max().item() / 4)
+    assert err < tol, f"{name} {dtype}: max err {err}"
+    s = st_out.cpu()
+    np.testing.assert_allclose(s[..., 0].numpy(), y.double().sum(1).numpy(), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[..., 1].numpy(), (y.double() ** 2).sum(1).numpy(), rtol=1e-5, atol=1e-3)

@@ -1,0 +1,117 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/stts2.h declares,
+and its model plans name exactly the reference state-dict keys (no GPU compute here)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from helpers import HIFI_CFG, ISTFT_CFG
+from stts2_mi355x import engine as E
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "stts2.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(stts_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_all_declared_symbols():
+    L = E.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(L, s), f"libstts2.so does not export {s}"
+
+
+def _plan(kind, cfg):
+    L = E.lib()
+    arr = (ctypes.c_int * len(cfg))(*cfg)
+    h = ctypes.c_void_p()
+    rc = L.stts_model_create(kind, arr, len(cfg), ctypes.byref(h))
+    return rc, h
+
+
+def _dec_cfg(module, ist):
+    g = module.generator
+    cfg = [module.dim_in, module.style_dim, g.upsample_initial_channel, len(g.upsample_rates), *g.upsample_rates,
+           *g.upsample_kernel_sizes, len(g.resblock_kernel_sizes), *g.resblock_kernel_sizes,
+           *[d for ds in g.resblock_dilation_sizes for d in ds]]
+    return cfg + ([g.gen_istft_n_fft, g.gen_istft_hop_size] if ist else [])
+
+
+@pytest.mark.parametrize("kind", ["hifigan", "istftnet"])
+def test_decoder_plan_names_match_state_dict(kind):
+    from stts2_mi355x.hifigan import Decoder as H
+    from stts2_mi355x.istftnet import Decoder as I
+    ist = kind == "istftnet"
+    mod = (I if ist else H)(dim_in=512, style_dim=128, dim_out=80, **(ISTFT_CFG if ist else HIFI_CFG))
+    rc, h = _plan(1 if ist else 0, _dec_cfg(mod, ist))
+    assert rc == 0
+    L = E.lib()
+    sd = mod.state_dict()
+    names = [L.stts_param_name(h, i).decode() for i in range(L.stts_param_count(h))]
+    assert sorted(names) == sorted(sd.keys())
+    for i, n in enumerate(names):
+        assert L.stts_param_numel(h, i) == sd[n].numel(), n
+    assert L.stts_packed_bytes(h, 1) > 0 and L.stts_packed_bytes(h, 0) > L.stts_packed_bytes(h, 1)
+    ws = L.stts_workspace_bytes(h, 1, 32, 400)
+    assert 0 < ws < 8 << 30  # B=32 x 10 s in bf16 fits a few GB of the 288 GB HBM
+    # forward without packed weights / params must fail loudly, not compute
+    rc = L.stts_decoder_fwd(h, 0, None, None, None, None, None, 0, 0, 1, 4, None, None, 0, None)
+    assert rc < 0
+    L.stts_model_destroy(h)
+
+
+def test_f0n_plan_names_match_state_dict():
+    from stts2_mi355x.models import ProsodyPredictor
+    pp = ProsodyPredictor(style_dim=128, d_hid=512, nlayers=3, max_dur=50, dropout=0.2)
+    rc, h = _plan(2, [512, 128])
+    assert rc == 0
+    L = E.lib()
+    sd = pp.state_dict()
+    names = [L.stts_param_name(h, i).decode() for i in range(L.stts_param_count(h))]
+    assert set(names) <= set(sd.keys())
+    assert {n for n in sd if n.startswith(("F0.", "N.", "F0_proj", "N_proj"))} == set(names)
+    L.stts_model_destroy(h)
+
+
+def test_bad_configs_rejected():
+    assert _plan(0, [512, 128, 512, 4, 10, 5, 3])[0] < 0       # truncated
+    assert _plan(0, [512, 128, 256, 1, 2, 4, 1, 3, 1, 3, 5])[0] < 0  # init channel must be 512
+    assert _plan(7, [1])[0] < 0                                 # unknown kind
+    assert _plan(2, [511, 128])[0] < 0                          # odd d_hid
+
+
+def test_error_strings():
+    L = E.lib()
+    for code in (0, -1, -2, -3, -4, -5):
+        assert L.stts_error_string(code)
+
+
+def test_product_path_refuses_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from helpers import make_decoder
+    dec, _ = make_decoder("hifigan")
+    with pytest.raises(RuntimeError):
+        dec(torch.zeros(1, 512, 4), torch.zeros(1, 8), torch.zeros(1, 8), torch.zeros(1, 128))
+
+
+def test_style_plan_names_match_state_dict():
+    from stts2_mi355x.models import StyleEncoder
+    se = StyleEncoder(dim_in=64, style_dim=128, max_conv_dim=512)
+    rc, h = _plan(3, [64, 128, 512])
+    assert rc == 0
+    L = E.lib()
+    sd = se.state_dict()
+    names = [L.stts_param_name(h, i).decode() for i in range(L.stts_param_count(h))]
+    assert sorted(names) == sorted(sd.keys())
+    for i, n in enumerate(names):
+        assert L.stts_param_numel(h, i) == sd[n].numel(), n
+    assert L.stts_workspace_bytes(h, 0, 1, 241) > 0
+    assert L.stts_workspace_bytes(h, 0, 1, 48) < 0  # 5x5 valid conv needs T >= 65 (reference raises too)
+    L.stts_model_destroy(h)
