@@ -59,7 +59,8 @@ def cpu_baseline(kind, dec, cfg, T, budget_s=12.0):
     one utterance at a time until `budget_s` of CPU work: samples/s."""
     from oracle import stts_oracle as orc
     from stts2_mi355x import synth
-    torch.set_num_threads(os.cpu_count() or 1)
+    # the GPU box exports OMP_NUM_THREADS = this job's CPU share (nproc reports the whole host)
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1)
     sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
     fn = orc.decoder_hifigan if kind == "hifigan" else orc.decoder_istft
     done, t0 = 0, time.perf_counter()

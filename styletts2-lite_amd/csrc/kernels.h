@@ -43,7 +43,8 @@ struct ConvParams {
   // zero columns: output rows o with (o % zc_period) >= zc_valid are written as 0 and excluded
   // from the statistics (keeps the padded image borders zero); zc_period = 0 disables.
   int zc_period, zc_valid;
-  int tg;  // set by the launcher
+  int tg;          // taps per staged weight group (set by the launcher)
+  int w_resident;  // weights of the column tile stay in LDS across tiles (set by the launcher)
 };
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);

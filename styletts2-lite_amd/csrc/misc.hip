@@ -94,14 +94,18 @@ __global__ void __launch_bounds__(256) k_frames_to_f32(const T* __restrict__ src
 
 // ------------------------------------------------------------------ Cin = 1 conv
 // out[b][t][c] = bias[c] + sum_k w[c][k] * in[b][t*stride - pad + k]   (zero padded)
-constexpr int C1_TT = 128;
-template <typename T>
+// reference hifigan.py:296-302 (noise_convs), :434-436 (F0_conv / N_conv).
+// Each thread owns one channel (weights in registers); the input window is staged in LDS
+// and read as a wave-wide broadcast; stores are channel-contiguous.
+constexpr int C1_TT = 512;
+template <typename T, int KC>
 __global__ void __launch_bounds__(256) k_conv_cin1(const float* __restrict__ in, long long in_bs, int Lin,
                                                    const float* __restrict__ w, const float* __restrict__ bias,
-                                                   int C, int K, int stride, int pad, int Lout, SmallConvDst d0,
+                                                   int C, int Kr, int stride, int pad, int Lout, SmallConvDst d0,
                                                    SmallConvDst d1, SmallConvDst d2, int ndst) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* win = reinterpret_cast<float*>(smem);
+  const int K = KC > 0 ? KC : Kr;
   const int b = blockIdx.y, t0 = blockIdx.x * C1_TT;
   const int nwin = (C1_TT - 1) * stride + K;
   const float* ib = in + (size_t)b * in_bs;
@@ -109,52 +113,62 @@ __global__ void __launch_bounds__(256) k_conv_cin1(const float* __restrict__ in,
     const int g = t0 * stride - pad + i;
     win[i] = (g >= 0 && g < Lin) ? ib[g] : 0.f;
   }
+  float* wl = win + ((nwin + 3) & ~3);  // generic-K weights [C][K] (KC == 0 only)
+  double* red = reinterpret_cast<double*>(wl + (KC > 0 ? 0 : ((C * K + 3) & ~3)));
+  if (KC == 0)
+    for (int i = threadIdx.x; i < C * K; i += 256) wl[i] = w[i];
   __syncthreads();
   const int cstr = C < 256 ? C : 256;
   const int tsplit = 256 / cstr;
   const int cl = threadIdx.x % cstr, ts = threadIdx.x / cstr;
-  double* red = reinterpret_cast<double*>(win + ((nwin + 3) & ~3));
+  const SmallConvDst* ds[3] = {&d0, &d1, &d2};
   for (int cb = 0; cb < C; cb += cstr) {
     const int c = cb + cl;
     double a = 0, q = 0;
-    if (ts < tsplit) {
-      const float* wc = w + (size_t)c * K;
+    if (ts < tsplit && c < C) {
+      float wr[KC > 0 ? KC : 1];
+      if constexpr (KC > 0) {
+#pragma unroll
+        for (int k = 0; k < KC; ++k) wr[k] = w[(size_t)c * KC + k];
+      }
       const float bc = bias ? bias[c] : 0.f;
+      float fa = 0.f, fq = 0.f;
       for (int tl = ts; tl < C1_TT; tl += tsplit) {
         const int t = t0 + tl;
         if (t >= Lout) break;
-        float acc = 0.f;
         const float* xw = win + tl * stride;
-        for (int k = 0; k < K; ++k) acc = fmaf(wc[k], xw[k], acc);
-        const float v = acc + bc;
-        const SmallConvDst* ds[3] = {&d0, &d1, &d2};
-        float vs = v;
-        for (int di = 0; di < ndst; ++di) {
-          const SmallConvDst& D = *ds[di];
-          const T tv = from_f32<T>(v);
-          reinterpret_cast<T*>(D.y)[(size_t)b * D.y_bs + (size_t)t * D.y_ld + D.c0 + c] = tv;
-          vs = to_f32(tv);
+        float acc = 0.f;
+        if constexpr (KC > 0) {
+#pragma unroll
+          for (int k = 0; k < KC; ++k) acc = fmaf(wr[k], xw[k], acc);
+        } else {
+          for (int k = 0; k < K; ++k) acc = fmaf(wl[c * K + k], xw[k], acc);
         }
-        a += vs;
-        q += (double)vs * vs;
+        const float v = acc + bc;
+        const T tv = from_f32<T>(v);
+        for (int di = 0; di < ndst; ++di)
+          reinterpret_cast<T*>(ds[di]->y)[(size_t)b * ds[di]->y_bs + (size_t)t * ds[di]->y_ld + ds[di]->c0 + c] = tv;
+        const float vs = to_f32(tv);
+        fa += vs;
+        fq += vs * vs;
       }
+      a = fa;
+      q = fq;
     }
-    // reduce over ts
+    if (d0.stats == nullptr && d1.stats == nullptr) continue;
     __syncthreads();
-    if (ts < tsplit) {
-      red[(ts * cstr + cl) * 2] = a;
-      red[(ts * cstr + cl) * 2 + 1] = q;
-    }
+    red[(ts * cstr + cl) * 2] = a;
+    red[(ts * cstr + cl) * 2 + 1] = q;
     __syncthreads();
-    if (threadIdx.x < cstr) {
+    if (threadIdx.x < cstr && cb + threadIdx.x < C) {
       double A = 0, Q = 0;
-      for (int s = 0; s < tsplit; ++s) {
-        A += red[(s * cstr + threadIdx.x) * 2];
-        Q += red[(s * cstr + threadIdx.x) * 2 + 1];
+      for (int s2 = 0; s2 < tsplit; ++s2) {
+        A += red[(s2 * cstr + threadIdx.x) * 2];
+        Q += red[(s2 * cstr + threadIdx.x) * 2 + 1];
       }
-      const SmallConvDst* ds[3] = {&d0, &d1, &d2};
       for (int di = 0; di < ndst; ++di)
-        if (ds[di]->stats) atomic_stats(ds[di]->stats + ((size_t)b * ds[di]->stats_ld + ds[di]->c0 + cb + threadIdx.x) * 2, A, Q);
+        if (ds[di]->stats)
+          atomic_stats(ds[di]->stats + ((size_t)b * ds[di]->stats_ld + ds[di]->c0 + cb + threadIdx.x) * 2, A, Q);
     }
   }
 }
@@ -525,13 +539,33 @@ int st_frames_to_f32(const void* src, int B, int L, int C, int ld, float* dst, i
 
 int st_conv_cin1(const float* in, long long in_bs, int Lin, int B, const float* w, const float* bias, int C, int K,
                  int stride, int pad, int Lout, const SmallConvDst* dst, int ndst, int dtype, hipStream_t s) {
-  if (ndst < 1 || ndst > 3 || C <= 0) return ST_EINVAL;
+  if (ndst < 1 || ndst > 3 || C <= 0 || K <= 0) return ST_EINVAL;
   SmallConvDst d[3] = {dst[0], ndst > 1 ? dst[1] : dst[0], ndst > 2 ? dst[2] : dst[0]};
+  if (ndst < 3) d[2].stats = nullptr;
+  if (ndst < 2) d[1].stats = nullptr;
   const int nwin = (C1_TT - 1) * stride + K;
-  const size_t lds = ((nwin + 3) & ~3) * sizeof(float) + 256 * 2 * sizeof(double);
+  const bool generic = !(K == 1 || K == 3 || K == 4 || K == 12 || K == 60);
+  const size_t lds = ((nwin + 3) & ~3) * sizeof(float) + (generic ? ((C * K + 3) & ~3) * sizeof(float) : 0) +
+                     256 * 2 * sizeof(double);
+  if (lds > 160 * 1024) return ST_EINVAL;
   dim3 grid((Lout + C1_TT - 1) / C1_TT, B);
-  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cin1<T>, grid, dim3(256), lds, s, in, in_bs, Lin, w, bias, C, K,
-                                              stride, pad, Lout, d[0], d[1], d[2], ndst));
+#define CIN1(KC)                                                                                                 \
+  DISPATCH_DTYPE(dtype, T, {                                                                                     \
+    auto kern = k_conv_cin1<T, KC>;                                                                              \
+    if (lds > 64 * 1024)                                                                                         \
+      ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, in, in_bs, Lin, w, bias, C, K, stride, pad, Lout, d[0], d[1], \
+                       d[2], ndst);                                                                              \
+  })
+  switch (K) {
+    case 1: CIN1(1); break;
+    case 3: CIN1(3); break;
+    case 4: CIN1(4); break;
+    case 12: CIN1(12); break;
+    case 60: CIN1(60); break;
+    default: CIN1(0); break;
+  }
+#undef CIN1
   return (int)hipGetLastError();
 }
 

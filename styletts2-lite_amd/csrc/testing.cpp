@@ -88,10 +88,10 @@ extern "C" int stts_test_conv1d(int dtype, const float* x, int B, int Lin, int C
   ST_CHECK(st_conv1d(p, dtype, s));
   ST_CHECK(st_frames_to_f32(yd, B, Lout, Cout, Cout, y, dtype, s));
   ST_CHECK_HIP(hipDeviceSynchronize());
-  hipFree(xd);
-  hipFree(wd);
-  hipFree(yd);
-  hipFree(sx);
-  if (rd) hipFree(rd);
+  (void)hipFree(xd);
+  (void)hipFree(wd);
+  (void)hipFree(yd);
+  (void)hipFree(sx);
+  if (rd) (void)hipFree(rd);
   return 0;
 }
