@@ -77,6 +77,26 @@ __device__ __forceinline__ float snake_f(float v, float al, float inv_al) {
   return v + inv_al * (s * s);
 }
 
+// Branch-free loads through a buffer descriptor: out-of-range offsets (negative rows wrap to
+// huge unsigned values) return 0 from the hardware range check, so every prefetch is issued
+// unconditionally and hipcc keeps counted vmcnt waits (a per-lane `if (ok) load` makes it
+// branch around each load and drain vmcnt(0): cdna_hip_programming.md §5 trap (c)).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* pb = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr unsigned OOB = 0x80000000u;  // an offset beyond every descriptor used here
+__device__ __forceinline__ uint4 bload16(Rsrc r, unsigned off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  uint4 o;
+  __builtin_memcpy(&o, &v, 16);
+  return o;
+}
+
 template <typename T> struct RawT;
 template <> struct RawT<bf16_t> { using type = uint4; };
 struct F8 { float4 a, b; };
@@ -84,6 +104,16 @@ template <> struct RawT<float> { using type = F8; };
 __device__ __forceinline__ uint4 load_raw(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ F8 load_raw(const float* p) {
   return F8{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 4)};
+}
+// 8 elements at element offset `e` (OOB when e is out of range of the descriptor)
+__device__ __forceinline__ void bload_raw(Rsrc r, unsigned e, uint4& out, const bf16_t*) {
+  out = bload16(r, e >= OOB / 2 ? OOB : e * 2u);
+}
+__device__ __forceinline__ void bload_raw(Rsrc r, unsigned e, F8& out, const float*) {
+  const unsigned o = e >= OOB / 4 ? OOB : e * 4u;
+  const uint4 a = bload16(r, o), b = bload16(r, o + 16u);
+  __builtin_memcpy(&out.a, &a, 16);
+  __builtin_memcpy(&out.b, &b, 16);
 }
 __device__ __forceinline__ void raw_to_f32(const uint4& r, float (&v)[8]) {
   bf16x8 b;
@@ -93,6 +123,17 @@ __device__ __forceinline__ void raw_to_f32(const uint4& r, float (&v)[8]) {
 }
 __device__ __forceinline__ void raw_to_f32(const F8& r, float (&v)[8]) {
   v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w; v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+}
+template <typename R>
+__device__ __forceinline__ void raw16_to_f32(const R& r, float (&v)[16]) {
+  float a[8], b[8];
+  raw_to_f32(r.a, a);
+  raw_to_f32(r.b, b);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v[j] = a[j];
+    v[8 + j] = b[j];
+  }
 }
 __device__ __forceinline__ void ld8_lds(const float* p, float (&v)[8]) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
@@ -192,28 +233,23 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
     }
   };
 
+  const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)p.nchunks * p.KS * BK * Np * sizeof(MT)));
   auto stage_w = [&](int c, int tap0, int ntap, MT* dst, int n0) {
     if constexpr (C::BF) {  // packed bf16: [chunk][tap][Np][32]
       const int units = ntap * BN * 4;
       for (int u = tid; u < units; u += NT) {
         const int tl = u / (BN * 4), rem = u % (BN * 4), n = rem >> 2, g = rem & 3;
         const int gn = n0 + n;
-        uint4 val = make_uint4(0, 0, 0, 0);
-        if (gn < Np)
-          val = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.w) +
-                                                (((size_t)c * p.KS + tap0 + tl) * Np + gn) * BK + 8 * g);
-        *reinterpret_cast<uint4*>(dst + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = val;
+        const unsigned off = gn < Np ? (unsigned)(((((size_t)c * p.KS + tap0 + tl) * Np + gn) * BK + 8 * g) * 2) : OOB;
+        *reinterpret_cast<uint4*>(dst + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = bload16(rw, off);
       }
     } else {  // packed fp32: [chunk][tap][32][Np]
       const int units = ntap * BK * (BN / 4);
       for (int u = tid; u < units; u += NT) {
         const int tl = u / (BK * (BN / 4)), rem = u % (BK * (BN / 4)), k = rem / (BN / 4), g = rem % (BN / 4);
         const int gn = n0 + 4 * g;
-        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gn < Np)
-          val = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.w) +
-                                                 (((size_t)c * p.KS + tap0 + tl) * BK + k) * Np + gn);
-        *reinterpret_cast<float4*>(dst + (size_t)tl * W_TAP + k * WPITCH + 4 * g) = val;
+        const unsigned off = gn < Np ? (unsigned)(((((size_t)c * p.KS + tap0 + tl) * BK + k) * Np + gn) * 4) : OOB;
+        *reinterpret_cast<uint4*>(dst + (size_t)tl * W_TAP + k * WPITCH + 4 * g) = bload16(rw, off);
       }
     }
   };
@@ -223,23 +259,20 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
   // latency hides under step s's MFMAs and epilogue.
   constexpr int MAXU = 6;  // prefetched 8-channel units per thread; the rest load synchronously
   typename RawT<T>::type pre[MAXU];
-  unsigned pre_ok = 0;
   const int units = R * 4;
 
   auto issue = [&](int t, int c) {
     const int mt = t % ntm, b = (t / ntm) % p.B;
     const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * p.x_bs;
+    const Rsrc rx = make_rsrc(xb, (unsigned)((size_t)p.Lin * p.x_ld * sizeof(T)));
     const int gr0 = mt * BM * p.stride - p.pad, ci0 = c * BK;
-    pre_ok = 0;
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int u = tid + k * NT;
       const int r = u >> 2, g = u & 3;
       const int gr = gr0 + r, ch = ci0 + 8 * g;
-      if (u < units && gr >= 0 && gr < p.Lin && ch < p.Cin) {
-        pre[k] = load_raw(xb + (size_t)gr * p.x_ld + ch);
-        pre_ok |= 1u << k;
-      }
+      const unsigned e = (u < units) ? (unsigned)(gr * p.x_ld + ch) : OOB;  // gr < 0 wraps: OOB
+      bload_raw(rx, e, pre[k], (const T*)nullptr);
     }
   };
 
@@ -285,32 +318,39 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
 
   auto write_x = [&](int t, int c) {
     const int ci0 = c * BK;
+    const int gr0 = (t % ntm) * BM * p.stride - p.pad;
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int u = tid + k * NT;
-      if (u < units) {
-        float v[8];
-        const bool ok = (pre_ok >> k) & 1u;
-        if (ok) raw_to_f32(pre[k], v);
-        put(u, v, ok, ci0);
-      }
+      const int gr = gr0 + (u >> 2);
+      float v[8];
+      raw_to_f32(pre[k], v);
+      // conv zero padding applies to the post-prologue activation
+      if (u < units) put(u, v, gr >= 0 && gr < p.Lin, ci0);
     }
     if (units > MAXU * NT) {  // large windows (2-D style convs): synchronous remainder
       const int mt = t % ntm, b = (t / ntm) % p.B;
       const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * p.x_bs;
-      const int gr0 = mt * BM * p.stride - p.pad;
+      const Rsrc rx = make_rsrc(xb, (unsigned)((size_t)p.Lin * p.x_ld * sizeof(T)));
+      (void)mt;
       for (int u = tid + MAXU * NT; u < units; u += NT) {
         const int r = u >> 2, g = u & 3;
         const int gr = gr0 + r, ch = ci0 + 8 * g;
+        typename RawT<T>::type raw;
+        bload_raw(rx, (unsigned)(gr * p.x_ld + ch), raw, (const T*)nullptr);
         float v[8];
-        const bool ok = gr >= 0 && gr < p.Lin && ch < p.Cin;
-        if (ok) load8(xb + (size_t)gr * p.x_ld + ch, v);
-        put(u, v, ok, ci0);
+        raw_to_f32(raw, v);
+        put(u, v, gr >= 0 && gr < p.Lin, ci0);
       }
     }
   };
 
   f32x16 acc[WM][WN];
+  constexpr bool PREF = !NARROW && WM * WN <= 2;
+  struct Raw16 {
+    typename RawT<T>::type a, b;
+  };
+  Raw16 rres[PREF ? WM : 1][PREF ? WN : 1], racc[PREF ? WM : 1][PREF ? WN : 1];
   const int nsteps = (tend - tbeg) * p.nchunks;
   if (nsteps > 0) issue(tbeg, 0);
   for (int st = 0; st < nsteps; ++st) {
@@ -350,6 +390,33 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
           for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     }
 
+    // residual / running-sum rows of this tile's epilogue: issued before the MFMAs so their
+    // HBM latency hides under them (small-channel configs, where the epilogue dominates)
+    if constexpr (PREF) {
+      if (c == p.nchunks - 1) {
+        const Rsrc rr = make_rsrc(p.res ? reinterpret_cast<const T*>(p.res) + (size_t)b * p.res_bs : (const T*)p.y,
+                                  p.res ? (unsigned)(p.res_bs * sizeof(T)) : 0u);
+        const Rsrc ra = make_rsrc(p.accb ? reinterpret_cast<const T*>(p.accb) + (size_t)b * p.acc_bs : (const T*)p.y,
+                                  p.accb ? (unsigned)(p.acc_bs * sizeof(T)) : 0u);
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < WN; ++ni) {
+            const int q = q0 + (wm * WM + mi) * 32 + l32;
+            const int nb = n0 + (wn * WN + ni) * 32 + hi * 16;
+            const int ph = nb / p.Cout, co0 = nb - ph * p.Cout;
+            const int o = q * p.up + ph - p.opad;
+            const bool ok = q < p.Lq && nb < p.N && o >= 0 && o < p.Lout;
+            const int orow = o + p.y_row_off;
+            const unsigned er = ok ? (unsigned)((orow >> p.res_shift) * p.res_ld + co0) : OOB;
+            const unsigned ea = ok ? (unsigned)(orow * p.acc_ld + co0) : OOB;
+            bload_raw(rr, er, rres[mi][ni].a, (const T*)nullptr);
+            bload_raw(rr, er + 8u, rres[mi][ni].b, (const T*)nullptr);
+            bload_raw(ra, ea, racc[mi][ni].a, (const T*)nullptr);
+            bload_raw(ra, ea + 8u, racc[mi][ni].b, (const T*)nullptr);
+          }
+      }
+    }
     __syncthreads();  // previous readers of Xs (MFMA / epilogue scratch) are done; coef / W visible
     write_x(t, c);
     if (st + 1 < nsteps) issue(tbeg + (st + 1) / p.nchunks, (st + 1) % p.nchunks);
@@ -475,13 +542,15 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
                 }
                 if (resb) {
                   float r[16];
-                  load16(resb + (size_t)(orow >> p.res_shift) * p.res_ld + co0, r);
+                  if constexpr (PREF) raw16_to_f32(rres[PREF ? mi : 0][PREF ? ni : 0], r);
+                  else load16(resb + (size_t)(orow >> p.res_shift) * p.res_ld + co0, r);
 #pragma unroll
                   for (int j = 0; j < 16; ++j) v[j] = (v[j] + r[j]) * p.out_scale;
                 }
                 if (accb) {
                   float r[16];
-                  load16(accb + (size_t)orow * p.acc_ld + co0, r);
+                  if constexpr (PREF) raw16_to_f32(racc[PREF ? mi : 0][PREF ? ni : 0], r);
+                  else load16(accb + (size_t)orow * p.acc_ld + co0, r);
                   if (p.acc_div != 0.f) {
                     // the reference divides (xs / num_kernels); bf16 mode multiplies by the reciprocal
                     const float inv_div = 1.0f / p.acc_div;
