@@ -94,6 +94,9 @@ const char* stts_error_string(int code);
  * on `stream` around each launch: enable, run, then read totals (ms, launches). */
 int stts_profile_enable(int on);
 int stts_profile_read(double* total_ms, long long* launches, double* alg_flops, double* alg_bytes);
+/* Launch i of the timed region: shape = {B, rows, N, Cin, taps, dilation, Lout, res|acc<<1},
+ * ms_flops_bytes = {hipEvent ms, algorithmic flops, algorithmic bytes}. */
+int stts_profile_launch(long long i, int* shape, double* ms_flops_bytes);
 
 /* ---- testing hook (not a product path): one conv1d_igemm launch on fp32 frames.
  * x [B][Lin][Cin] frames; w in nn.Conv1d [Cout][Cin][K] / nn.ConvTranspose1d [Cin][Cout][K] layout;

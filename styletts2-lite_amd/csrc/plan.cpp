@@ -29,6 +29,8 @@ struct Prof {
   size_t used = 0;
   long long launches = 0;
   double flops = 0, bytes = 0;
+  struct Rec { int shape[8]; double flops, bytes; };
+  std::vector<Rec> rec;  // one per timed launch, in launch order
 } g_prof;
 
 // ----------------------------------------------------------------------- parameters
@@ -486,10 +488,13 @@ int conv_run(Ctx& c, ConvParams& p) {
     g_prof.used += 2;
     g_prof.launches++;
     // algorithmic work: a (transposed) conv is 2 * rows * N * Cin * taps flops on its GEMM view
-    g_prof.flops += 2.0 * p.B * (double)p.Lq * p.N * p.Cin * p.KS;
+    const double fl = 2.0 * p.B * (double)p.Lq * p.N * p.Cin * p.KS;
     double elems = (double)p.B * ((double)p.Lin * p.Cin + (double)p.Lout * p.Cout * (1 + (p.res ? 1 : 0) +
                                                                                      (p.accb ? 1 : 0)));
-    g_prof.bytes += elems * c.esz + (p.y_f32 ? (double)p.B * p.Lout * p.Cout * (4.0 - c.esz) : 0.0);
+    const double by = elems * c.esz + (p.y_f32 ? (double)p.B * p.Lout * p.Cout * (4.0 - c.esz) : 0.0);
+    g_prof.flops += fl;
+    g_prof.bytes += by;
+    g_prof.rec.push_back({{p.B, p.Lq, p.N, p.Cin, p.KS, p.dil, p.Lout, (p.res ? 1 : 0) | (p.accb ? 2 : 0)}, fl, by});
   }
   return 0;
 }
@@ -1150,6 +1155,23 @@ int stts_profile_enable(int on) {
   g_prof.used = 0;
   g_prof.launches = 0;
   g_prof.flops = g_prof.bytes = 0;
+  g_prof.rec.clear();
+  return 0;
+}
+
+int stts_profile_launch(long long i, int* shape, double* ms_flops_bytes) {
+  if (i < 0 || (size_t)i >= g_prof.rec.size() || 2 * (size_t)i + 1 >= g_prof.used) return ST_EINVAL;
+  float ms = 0;
+  ST_CHECK_HIP(hipEventSynchronize(g_prof.ev[2 * i + 1]));
+  ST_CHECK_HIP(hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
+  const auto& r = g_prof.rec[i];
+  if (shape)
+    for (int k = 0; k < 8; ++k) shape[k] = r.shape[k];
+  if (ms_flops_bytes) {
+    ms_flops_bytes[0] = ms;
+    ms_flops_bytes[1] = r.flops;
+    ms_flops_bytes[2] = r.bytes;
+  }
   return 0;
 }
 

@@ -65,6 +65,8 @@ def lib():
     L.stts_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_ll),
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
     L.stts_profile_read.restype = c_int
+    L.stts_profile_launch.argtypes = [c_ll, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double)]
+    L.stts_profile_launch.restype = c_int
     _LIB = L
     return L
 
@@ -276,3 +278,16 @@ def profile_read():
     t, n, f, b = ctypes.c_double(), c_ll(), ctypes.c_double(), ctypes.c_double()
     check(lib().stts_profile_read(ctypes.byref(t), ctypes.byref(n), ctypes.byref(f), ctypes.byref(b)))
     return {"ms": t.value, "launches": n.value, "flops": f.value, "bytes": b.value}
+
+
+def profile_launches():
+    """Per-launch records of the timed region: dicts with the GEMM shape, ms, flops, bytes."""
+    out = []
+    n = profile_read()["launches"]
+    shape, v = (ctypes.c_int * 8)(), (ctypes.c_double * 3)()
+    for i in range(n):
+        check(lib().stts_profile_launch(i, shape, v))
+        out.append({"B": shape[0], "rows": shape[1], "N": shape[2], "Cin": shape[3], "taps": shape[4],
+                    "dil": shape[5], "Lout": shape[6], "res_acc": shape[7], "ms": v[0], "flops": v[1],
+                    "bytes": v[2]})
+    return out
