@@ -23,15 +23,17 @@
 //     fuses bias, residual, 1/sqrt2, the resblock average, tanh, the iSTFTNet reflection pad
 //     and the InstanceNorm statistics; statistics are kept in registers across the tiles of
 //     one utterance and flushed with one fp64 atomic per (utterance, channel, workgroup).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
+#include "conv_common.h"
 #include "kernels.h"
 
 namespace {
 
 constexpr int BK = 32;
-constexpr int EP = 36;  // epilogue transpose pitch (floats): conflict-free b128 row reads
+constexpr int EP = 36;  // stats scratch pitch (floats): conflict-free b128 row writes
 
 template <typename MT> struct Layout;
 template <> struct Layout<bf16_t> {
@@ -56,128 +58,49 @@ struct ConvCfg {
   __host__ __device__ static int rows(const ConvParams& p) {
     return (BM - 1) * p.stride + ((p.KS - 1) / p.kw) * p.row_off + ((p.KS < p.kw ? p.KS : p.kw) - 1) * p.dil + 1;
   }
-  // LDS carve (bytes): [coef 4 x cinp f32][X window | epilogue scratch][W slices]
+  // LDS carve (bytes): [coef 4 x cinp f32 | bias BN f32 | stats scratch NW x 32 x EP f32][X window][W slices]
   __host__ __device__ static int cinp(const ConvParams& p) { return p.nchunks * BK; }
-  __host__ __device__ static size_t coef_bytes(const ConvParams& p) { return (size_t)4 * cinp(p) * 4; }
+  __host__ __device__ static size_t coef_bytes(const ConvParams& p) {
+    return ((size_t)4 * cinp(p) + BN + (size_t)NW * 32 * EP) * 4;
+  }
   __host__ __device__ static size_t xs_bytes(const ConvParams& p) {
-    size_t x = (((size_t)rows(p) * XP * sizeof(MT)) + 15) & ~(size_t)15;
-    const size_t ep = (size_t)NW * 32 * EP * 4;
-    const size_t red = (size_t)WAVES_M * BN * 2 * 4;
-    x = x > ep ? x : ep;
-    return x > red ? x : red;
+    return (((size_t)rows(p) * XP * sizeof(MT)) + 15) & ~(size_t)15;
   }
   static size_t lds_bytes(const ConvParams& p, int nwslices) {
     return coef_bytes(p) + xs_bytes(p) + (size_t)nwslices * W_TAP * sizeof(MT);
   }
 };
 
-template <bool FAST>
-__device__ __forceinline__ float snake_f(float v, float al, float inv_al) {
-  const float s = FAST ? __sinf(al * v) : sinf(al * v);
-  return v + inv_al * (s * s);
+typedef float f2v __attribute__((ext_vector_type(2)));
+// bf16: at least 2 waves per SIMD (<= 256 VGPRs); fp32 (parity mode) keeps its registers
+template <typename MT> constexpr int kMinWaves = std::is_same<MT, bf16_t>::value ? 2 : 1;
+
+// 16 values <-> 8 packed pairs
+__device__ __forceinline__ f2v pr(const float (&v)[16], int i) { return f2v{v[2 * i], v[2 * i + 1]}; }
+__device__ __forceinline__ void pw(float (&v)[16], int i, f2v x) {
+  v[2 * i] = x.x;
+  v[2 * i + 1] = x.y;
 }
 
-// Branch-free loads through a buffer descriptor: out-of-range offsets (negative rows wrap to
-// huge unsigned values) return 0 from the hardware range check, so every prefetch is issued
-// unconditionally and hipcc keeps counted vmcnt waits (a per-lane `if (ok) load` makes it
-// branch around each load and drain vmcnt(0): cdna_hip_programming.md §5 trap (c)).
-typedef __amdgpu_buffer_rsrc_t Rsrc;
-__device__ __forceinline__ Rsrc make_rsrc(const void* base, unsigned bytes) {
-  const unsigned long long a = (unsigned long long)base;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-  void* pb = (void*)(((unsigned long long)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-constexpr unsigned OOB = 0x80000000u;  // an offset beyond every descriptor used here
-__device__ __forceinline__ uint4 bload16(Rsrc r, unsigned off) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
-  uint4 o;
-  __builtin_memcpy(&o, &v, 16);
-  return o;
-}
-
-template <typename T> struct RawT;
-template <> struct RawT<bf16_t> { using type = uint4; };
-struct F8 { float4 a, b; };
-template <> struct RawT<float> { using type = F8; };
-__device__ __forceinline__ uint4 load_raw(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
-__device__ __forceinline__ F8 load_raw(const float* p) {
-  return F8{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 4)};
-}
-// 8 elements at element offset `e` (OOB when e is out of range of the descriptor)
-__device__ __forceinline__ void bload_raw(Rsrc r, unsigned e, uint4& out, const bf16_t*) {
-  out = bload16(r, e >= OOB / 2 ? OOB : e * 2u);
-}
-__device__ __forceinline__ void bload_raw(Rsrc r, unsigned e, F8& out, const float*) {
-  const unsigned o = e >= OOB / 4 ? OOB : e * 4u;
-  const uint4 a = bload16(r, o), b = bload16(r, o + 16u);
-  __builtin_memcpy(&out.a, &a, 16);
-  __builtin_memcpy(&out.b, &b, 16);
-}
-__device__ __forceinline__ void raw_to_f32(const uint4& r, float (&v)[8]) {
-  bf16x8 b;
-  __builtin_memcpy(&b, &r, 16);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (float)b[j];
-}
-__device__ __forceinline__ void raw_to_f32(const F8& r, float (&v)[8]) {
-  v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w; v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
-}
-template <typename R>
-__device__ __forceinline__ void raw16_to_f32(const R& r, float (&v)[16]) {
-  float a[8], b[8];
-  raw_to_f32(r.a, a);
-  raw_to_f32(r.b, b);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    v[j] = a[j];
-    v[8 + j] = b[j];
-  }
-}
-__device__ __forceinline__ void ld8_lds(const float* p, float (&v)[8]) {
-  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-
-template <typename T>
-__device__ __forceinline__ void load16(const T* p, float (&v)[16]) {
-  float a[8], b[8];
-  load8(p, a);
-  load8(p + 8, b);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    v[j] = a[j];
-    v[8 + j] = b[j];
-  }
-}
-
-__device__ __forceinline__ void store16(float* p, const float (&v)[16]) {
-#pragma unroll
-  for (int j = 0; j < 16; j += 4) *reinterpret_cast<float4*>(p + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
-}
-__device__ __forceinline__ void store16(bf16_t* p, const float (&v)[16]) {
-  bf16x8 a, b;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    a[j] = (bf16_t)v[j];
-    b[j] = (bf16_t)v[8 + j];
-  }
-  *reinterpret_cast<bf16x8*>(p) = a;
-  *reinterpret_cast<bf16x8*>(p + 8) = b;
-}
-
+// Accumulator orientation: the MFMA computes C^T = W^T X^T (A = weights, B = input window), so
+// a lane's 16 accumulator registers are ONE output frame (column = lane & 31) and, because
+// st_pack_conv permutes the packed rows inside each 32-block (row m holds channel
+// 16*((m>>2)&1) + (m&3) + 4*(m>>3)), 16 CONSECUTIVE channels 16*(lane>>5) + r.  The epilogue
+// therefore works straight from registers: no LDS transpose, 16-channel vector loads/stores,
+// and per-lane statistics accumulated across tiles (reduced across lanes once per utterance).
 template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW>
-__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(const ConvParams p) {
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
+    conv1d_igemm_kernel(const ConvParams p) {
   using C = ConvCfg<T, MT, WAVES_M, WAVES_N, WM, WN>;
   constexpr int BM = C::BM, BN = C::BN, XP = C::XP, WPITCH = C::WPITCH, W_TAP = C::W_TAP, NT = C::NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int R = C::rows(p);
   const int cinp = C::cinp(p);
-  float* coef = reinterpret_cast<float*>(smem);  // [4][cinp]: beta - mean*a, a, alpha, 1/alpha
+  float* coef = reinterpret_cast<float*>(smem);  // [4][cinp]: beta - mean*a, a, alpha (x 1/2pi in bf16), 1/alpha
+  float* bias_s = coef + 4 * cinp;               // [BN]: bias of the column tile's (phase, channel) columns
+  float* ws = bias_s + BN + (size_t)(threadIdx.x >> 6) * 32 * EP;  // this wave's stats scratch [frame][EP]
   MT* Xs = reinterpret_cast<MT*>(smem + C::coef_bytes(p));
-  float* scr = reinterpret_cast<float*>(Xs);     // epilogue scratch / stats reduction (aliases X)
   MT* Ws = reinterpret_cast<MT*>(smem + C::coef_bytes(p) + C::xs_bytes(p));
 
   const int ntn = (p.N + BN - 1) / BN;
@@ -194,42 +117,27 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
   const bool resident = p.w_resident != 0;
   constexpr bool FAST_SIN = C::BF;
 
-  // statistics partials: lane = one output column (l32 of tile ni), rows of its half (hi)
+  // statistics partials: lane = column l32 of tile ni, summed over the frames of its half (hi)
   float st_s[WN], st_q[WN];
 #pragma unroll
   for (int ni = 0; ni < WN; ++ni) st_s[ni] = st_q[ni] = 0.f;
 
   int cur_nt = -1, cur_b = -1;
 
-  // flush the register statistics of column tile `nt` / utterance `b` (block-uniform call)
+  // per-wave flush of the register statistics (no block barrier): the two frame halves
+  // combine across lanes l and l^32, then one fp64 atomic pair per (wave, column)
   auto flush_stats = [&](int nt, int b) {
-    __syncthreads();
-    // lanes l and l^32 hold the two row halves of the same column
 #pragma unroll
     for (int ni = 0; ni < WN; ++ni) {
       const float a = st_s[ni] + __shfl_xor(st_s[ni], 32);
       const float q = st_q[ni] + __shfl_xor(st_q[ni], 32);
-      if (hi == 0) {
-        const int nl = (wn * WN + ni) * 32 + l32;
-        scr[((size_t)wm * BN + nl) * 2 + 0] = a;
-        scr[((size_t)wm * BN + nl) * 2 + 1] = q;
+      const int n = nt * BN + (wn * WN + ni) * 32 + l32;
+      if (hi == 0 && n < p.N) {
+        const int co = n % p.Cout;
+        atomicAdd(p.stats + ((size_t)b * p.stats_ld + co) * 2 + 0, (double)a);
+        atomicAdd(p.stats + ((size_t)b * p.stats_ld + co) * 2 + 1, (double)q);
       }
       st_s[ni] = st_q[ni] = 0.f;
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      const int n = nt * BN + c;
-      if (n < p.N) {
-        double a = 0.0, q = 0.0;
-#pragma unroll
-        for (int w = 0; w < WAVES_M; ++w) {
-          a += scr[((size_t)w * BN + c) * 2 + 0];
-          q += scr[((size_t)w * BN + c) * 2 + 1];
-        }
-        const int co = n % p.Cout;
-        atomicAdd(p.stats + ((size_t)b * p.stats_ld + co) * 2 + 0, a);
-        atomicAdd(p.stats + ((size_t)b * p.stats_ld + co) * 2 + 1, q);
-      }
     }
   };
 
@@ -240,7 +148,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
       for (int u = tid; u < units; u += NT) {
         const int tl = u / (BN * 4), rem = u % (BN * 4), n = rem >> 2, g = rem & 3;
         const int gn = n0 + n;
-        const unsigned off = gn < Np ? (unsigned)(((((size_t)c * p.KS + tap0 + tl) * Np + gn) * BK + 8 * g) * 2) : OOB;
+        const int gp = g ^ ((gn >> 2) & 3);  // swizzled packed layout (st_pack_conv)
+        const unsigned off = gn < Np ? (unsigned)(((((size_t)c * p.KS + tap0 + tl) * Np + gn) * BK + 8 * gp) * 2) : OOB;
         *reinterpret_cast<uint4*>(dst + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = bload16(rw, off);
       }
     } else {  // packed fp32: [chunk][tap][32][Np]
@@ -254,12 +163,54 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
     }
   };
 
+  // ---- streamed weights (layers whose packed weights exceed the LDS budget): tap groups are
+  // software-pipelined through registers like the input window — group g+1's loads are issued
+  // right after group g is written to LDS, so the L2 latency hides under group g's MFMAs.
+  constexpr int MAXW = 4;  // 16-byte W units per thread per group (launch_cfg sizes tg to fit)
+  uint4 wpre[MAXW];
+  auto issue_w = [&](int t, int c, int tap0) {
+    const int n0 = (t / (ntm * p.B)) * BN;
+    const int ntap = min(p.tg, p.KS - tap0);
+#pragma unroll
+    for (int k = 0; k < MAXW; ++k) {
+      const int u = tid + k * NT;
+      unsigned off = OOB;
+      if constexpr (C::BF) {
+        const int tl = u / (BN * 4), rem = u % (BN * 4), n = rem >> 2, g = rem & 3;
+        const int gn = n0 + n;
+        if (tl < ntap && gn < Np)
+          off = (unsigned)(((((size_t)c * p.KS + tap0 + tl) * Np + gn) * BK + 8 * (g ^ ((gn >> 2) & 3))) * 2);
+      } else {
+        const int tl = u / (BK * (BN / 4)), rem = u % (BK * (BN / 4)), kq = rem / (BN / 4), g = rem % (BN / 4);
+        const int gn = n0 + 4 * g;
+        if (tl < ntap && gn < Np)
+          off = (unsigned)(((((size_t)c * p.KS + tap0 + tl) * BK + kq) * Np + gn) * 4);
+      }
+      wpre[k] = bload16(rw, off);
+    }
+  };
+  auto put_w = [&](int ntap) {
+#pragma unroll
+    for (int k = 0; k < MAXW; ++k) {
+      const int u = tid + k * NT;
+      if constexpr (C::BF) {
+        const int tl = u / (BN * 4), rem = u % (BN * 4), n = rem >> 2, g = rem & 3;
+        if (tl < ntap) *reinterpret_cast<uint4*>(Ws + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = wpre[k];
+      } else {
+        const int tl = u / (BK * (BN / 4)), rem = u % (BK * (BN / 4)), kq = rem / (BN / 4), g = rem % (BN / 4);
+        if (tl < ntap) *reinterpret_cast<uint4*>(Ws + (size_t)tl * W_TAP + kq * WPITCH + 4 * g) = wpre[k];
+      }
+    }
+  };
+
   // ---- input-window staging, software-pipelined over (tile, chunk) steps: the raw loads of
   // step s+1 are issued into registers right after step s's window is written to LDS, so HBM
   // latency hides under step s's MFMAs and epilogue.
   constexpr int MAXU = 6;  // prefetched 8-channel units per thread; the rest load synchronously
   typename RawT<T>::type pre[MAXU];
   const int units = R * 4;
+  // every unit of a thread is the same 8-channel group: u = tid + k*NT, NT % 4 == 0
+  const int g8 = tid & 3;
 
   auto issue = [&](int t, int c) {
     const int mt = t % ntm, b = (t / ntm) % p.B;
@@ -269,42 +220,80 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int u = tid + k * NT;
-      const int r = u >> 2, g = u & 3;
-      const int gr = gr0 + r, ch = ci0 + 8 * g;
+      const int r = u >> 2;
+      const int gr = gr0 + r, ch = ci0 + 8 * g8;
       const unsigned e = (u < units) ? (unsigned)(gr * p.x_ld + ch) : OOB;  // gr < 0 wraps: OOB
       bload_raw(rx, e, pre[k], (const T*)nullptr);
     }
   };
 
-  auto put = [&](int u, float (&v)[8], bool ok, int ci0) {
-    const int r = u >> 2, g = u & 3;
-    const int ch = ci0 + 8 * g;
-    if (ok) {
-      float cm[8], ca[8];
-      if (mode & PRO_AFFINE) {
-        ld8_lds(coef + ch, cm);
-        ld8_lds(coef + cinp + ch, ca);
+  // prologue coefficients of this thread's 8 channels, loaded once per step
+  struct Coef8 { f2v a[4], m[4], al[4], ia[4]; };
+  auto load_coef = [&](int ci0, Coef8& k) {
+    const int ch = ci0 + 8 * g8;
+    float t0[8], t1[8];
+    if (mode & PRO_AFFINE) {
+      ld8_lds(coef + ch, t0);
+      ld8_lds(coef + cinp + ch, t1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], ca[j], cm[j]);  // x*a + (beta - mean*a)
+      for (int i = 0; i < 4; ++i) {
+        k.m[i] = f2v{t0[2 * i], t0[2 * i + 1]};
+        k.a[i] = f2v{t1[2 * i], t1[2 * i + 1]};
+      }
+    }
+    if (mode & PRO_SNAKE) {
+      ld8_lds(coef + 2 * cinp + ch, t0);
+      ld8_lds(coef + 3 * cinp + ch, t1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        k.al[i] = f2v{t0[2 * i], t0[2 * i + 1]};
+        k.ia[i] = f2v{t1[2 * i], t1[2 * i + 1]};
+      }
+    }
+  };
+
+  auto put = [&](int u, float (&v)[8], bool ok, int ci0, const Coef8& k) {
+    const int r = u >> 2;
+    const int ch = ci0 + 8 * g8;
+    if (ok) {
+      f2v x[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = f2v{v[2 * i], v[2 * i + 1]};
+      if (mode & PRO_AFFINE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = __builtin_elementwise_fma(x[i], k.a[i], k.m[i]);  // x*a + (beta - mean*a)
       }
       if (mode & PRO_SNAKE) {
-        ld8_lds(coef + 2 * cinp + ch, cm);
-        ld8_lds(coef + 3 * cinp + ch, ca);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = snake_f<FAST_SIN>(v[j], cm[j], ca[j]);
+        for (int i = 0; i < 4; ++i) {
+          if constexpr (FAST_SIN) {  // v_sin_f32 takes revolutions: coef holds alpha / 2pi
+            const f2v t = x[i] * k.al[i];
+            const f2v sn = f2v{__builtin_amdgcn_sinf(t.x), __builtin_amdgcn_sinf(t.y)};
+            x[i] = __builtin_elementwise_fma(sn * sn, k.ia[i], x[i]);
+          } else {
+            x[i] = f2v{snake_f<false>(x[i].x, k.al[i].x, k.ia[i].x), snake_f<false>(x[i].y, k.al[i].y, k.ia[i].y)};
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] = x[i].x;
+        v[2 * i + 1] = x[i].y;
       }
       if (mode & PRO_LRELU) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * p.pro.slope;
       }
+      if (ch + 8 > p.Cin) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (ch + j >= p.Cin) v[j] = 0.f;
+        for (int j = 0; j < 8; ++j)
+          if (ch + j >= p.Cin) v[j] = 0.f;
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = 0.f;
     }
-    MT* dst = Xs + r * XP + 8 * g;
+    MT* dst = Xs + r * XP + 8 * g8;
     if constexpr (C::BF) {
       bf16x8 o;
 #pragma unroll
@@ -319,28 +308,29 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
   auto write_x = [&](int t, int c) {
     const int ci0 = c * BK;
     const int gr0 = (t % ntm) * BM * p.stride - p.pad;
+    Coef8 k;
+    load_coef(ci0, k);
 #pragma unroll
-    for (int k = 0; k < MAXU; ++k) {
-      const int u = tid + k * NT;
+    for (int kk = 0; kk < MAXU; ++kk) {
+      const int u = tid + kk * NT;
       const int gr = gr0 + (u >> 2);
       float v[8];
-      raw_to_f32(pre[k], v);
+      raw_to_f32(pre[kk], v);
       // conv zero padding applies to the post-prologue activation
-      if (u < units) put(u, v, gr >= 0 && gr < p.Lin, ci0);
+      if (u < units) put(u, v, gr >= 0 && gr < p.Lin, ci0, k);
     }
     if (units > MAXU * NT) {  // large windows (2-D style convs): synchronous remainder
-      const int mt = t % ntm, b = (t / ntm) % p.B;
+      const int b = (t / ntm) % p.B;
       const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * p.x_bs;
       const Rsrc rx = make_rsrc(xb, (unsigned)((size_t)p.Lin * p.x_ld * sizeof(T)));
-      (void)mt;
       for (int u = tid + MAXU * NT; u < units; u += NT) {
-        const int r = u >> 2, g = u & 3;
-        const int gr = gr0 + r, ch = ci0 + 8 * g;
+        const int r = u >> 2;
+        const int gr = gr0 + r, ch = ci0 + 8 * g8;
         typename RawT<T>::type raw;
         bload_raw(rx, (unsigned)(gr * p.x_ld + ch), raw, (const T*)nullptr);
         float v[8];
         raw_to_f32(raw, v);
-        put(u, v, gr >= 0 && gr < p.Lin, ci0);
+        put(u, v, gr >= 0 && gr < p.Lin, ci0, k);
       }
     }
   };
@@ -352,7 +342,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
   };
   Raw16 rres[PREF ? WM : 1][PREF ? WN : 1], racc[PREF ? WM : 1][PREF ? WN : 1];
   const int nsteps = (tend - tbeg) * p.nchunks;
-  if (nsteps > 0) issue(tbeg, 0);
+  if (nsteps > 0) {
+    issue(tbeg, 0);
+    if (!resident) issue_w(tbeg, 0, 0);
+  }
   for (int st = 0; st < nsteps; ++st) {
     const int t = tbeg + st / p.nchunks, c = st % p.nchunks;
     const int mt = t % ntm;
@@ -373,12 +366,18 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
             }
             coef[ci] = be - m * a;   // x * a + (beta - mean * a)  ==  (x - mean) * a + beta
             coef[cinp + ci] = a;
-            coef[2 * cinp + ci] = al;
+            coef[2 * cinp + ci] = C::BF ? al * 0.15915494309189535f : al;  // bf16: alpha in revolutions
             coef[3 * cinp + ci] = 1.0f / al;  // the reference's (1 / alpha), once per channel
           }
         }
-        if (resident && nt != cur_nt)
-          for (int cc = 0; cc < p.nchunks; ++cc) stage_w(cc, 0, p.KS, Ws + (size_t)cc * p.KS * W_TAP, n0);
+        if (nt != cur_nt) {
+          for (int cc = tid; cc < BN; cc += NT) {
+            const int n = n0 + cc;
+            bias_s[cc] = (p.bias && n < p.N) ? p.bias[n % p.Cout] : 0.f;
+          }
+          if (resident)
+            for (int cc = 0; cc < p.nchunks; ++cc) stage_w(cc, 0, p.KS, Ws + (size_t)cc * p.KS * W_TAP, n0);
+        }
         cur_nt = nt;
         cur_b = b;
       }
@@ -417,7 +416,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
           }
       }
     }
-    __syncthreads();  // previous readers of Xs (MFMA / epilogue scratch) are done; coef / W visible
+    __syncthreads();  // previous readers of Xs (MFMA) are done; coef / bias / W visible
     write_x(t, c);
     if (st + 1 < nsteps) issue(tbeg + (st + 1) / p.nchunks, (st + 1) % p.nchunks);
     // ---- taps (weights resident, or staged in groups that fit the budget) ----
@@ -427,8 +426,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
       if (resident) {
         wbase = Ws + (size_t)c * p.KS * W_TAP;
       } else {
-        if (tap0 > 0) __syncthreads();
-        stage_w(c, tap0, ntap, Ws, n0);
+        if (tap0 > 0) __syncthreads();  // every wave is done reading the previous group
+        put_w(ntap);
+        if (tap0 + p.tg < p.KS) issue_w(t, c, tap0 + p.tg);
+        else if (st + 1 < nsteps) issue_w(tbeg + (st + 1) / p.nchunks, (st + 1) % p.nchunks, 0);
         wbase = Ws;
       }
       __syncthreads();
@@ -455,7 +456,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
             for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
               for (int ni = 0; ni < WN; ++ni)
-                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bw[ni], acc[mi][ni], 0, 0, 0);
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[ni], af[mi], acc[mi][ni], 0, 0, 0);
           }
         } else {
 #pragma unroll 4
@@ -475,16 +476,14 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
             for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
               for (int ni = 0; ni < WN; ++ni)
-                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi], bw[ni], acc[mi][ni], 0, 0, 0);
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[ni], af[mi], acc[mi][ni], 0, 0, 0);
           }
         }
       }
     }
     if (c != p.nchunks - 1) continue;
 
-    // ---------------- epilogue: per-wave transpose, lane = (frame, 16 channels) ----------------
-    __syncthreads();  // every wave is done reading Xs / Ws
-    float* ws = scr + (size_t)wid * 32 * EP;
+    // ---------------- epilogue, straight from registers: lane = (frame, 16 channels) ----------------
     T* yT = reinterpret_cast<T*>(p.y) + (size_t)b * p.y_bs;
     float* yF = reinterpret_cast<float*>(p.y) + (size_t)b * p.y_bs;
     const T* resb = p.res ? reinterpret_cast<const T*>(p.res) + (size_t)b * p.res_bs : nullptr;
@@ -493,19 +492,13 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
     for (int mi = 0; mi < WM; ++mi) {
 #pragma unroll
       for (int ni = 0; ni < WN; ++ni) {
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) ws[((reg & 3) + 8 * (reg >> 2) + 4 * hi) * EP + l32] = acc[mi][ni][reg];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         float v[16];
 #pragma unroll
-        for (int j = 0; j < 16; j += 4) {
-          const float4 f = *reinterpret_cast<const float4*>(ws + l32 * EP + hi * 16 + j);
-          v[j] = f.x; v[j + 1] = f.y; v[j + 2] = f.z; v[j + 3] = f.w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int r = 0; r < 16; ++r) v[r] = acc[mi][ni][r];
         const int q = q0 + (wm * WM + mi) * 32 + l32;
-        const int nb = n0 + (wn * WN + ni) * 32 + hi * 16;  // first of this lane's 16 columns
-        // v becomes the stored values (0 where nothing is stored) for the statistics pass
+        const int nl = (wn * WN + ni) * 32 + hi * 16;  // first of this lane's 16 columns, in the tile
+        const int nb = n0 + nl;
+        // v becomes the stored values (0 where nothing is stored) for the statistics
         bool stored = false;
         if (q < p.Lq && nb < p.N) {
           if constexpr (!NARROW) {
@@ -519,12 +512,12 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
                 for (int j = 0; j < 16; ++j) v[j] = 0.f;
                 store16(yT + (size_t)orow * p.y_ld + co0, v);
               } else {
-                if (p.bias) {
+                {
+                  float bb[16];
+                  ld8_lds(bias_s + nl, *reinterpret_cast<float(*)[8]>(&bb[0]));
+                  ld8_lds(bias_s + nl + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
 #pragma unroll
-                  for (int j = 0; j < 16; j += 4) {
-                    const float4 bb = *reinterpret_cast<const float4*>(p.bias + co0 + j);
-                    v[j] += bb.x; v[j + 1] += bb.y; v[j + 2] += bb.z; v[j + 3] += bb.w;
-                  }
+                  for (int i = 0; i < 8; ++i) pw(v, i, pr(v, i) + pr(bb, i));
                 }
                 if (p.reflect_front && o == 1) {  // iSTFTNet ReflectionPad1d((1,0)) (istftnet.py:538, 558-559)
                   float r[16];
@@ -544,26 +537,34 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
                   float r[16];
                   if constexpr (PREF) raw16_to_f32(rres[PREF ? mi : 0][PREF ? ni : 0], r);
                   else load16(resb + (size_t)(orow >> p.res_shift) * p.res_ld + co0, r);
+                  const f2v sc = f2v{p.out_scale, p.out_scale};
 #pragma unroll
-                  for (int j = 0; j < 16; ++j) v[j] = (v[j] + r[j]) * p.out_scale;
+                  for (int i = 0; i < 8; ++i) pw(v, i, (pr(v, i) + pr(r, i)) * sc);
                 }
                 if (accb) {
                   float r[16];
                   if constexpr (PREF) raw16_to_f32(racc[PREF ? mi : 0][PREF ? ni : 0], r);
                   else load16(accb + (size_t)orow * p.acc_ld + co0, r);
                   if (p.acc_div != 0.f) {
-                    // the reference divides (xs / num_kernels); bf16 mode multiplies by the reciprocal
-                    const float inv_div = 1.0f / p.acc_div;
+                    if constexpr (C::BF) {  // bf16 mode multiplies by the reciprocal
+                      const float id = 1.0f / p.acc_div;
+                      const f2v inv = f2v{id, id};
 #pragma unroll
-                    for (int j = 0; j < 16; ++j) v[j] = C::BF ? (r[j] + v[j]) * inv_div : (r[j] + v[j]) / p.acc_div;
+                      for (int i = 0; i < 8; ++i) pw(v, i, (pr(r, i) + pr(v, i)) * inv);
+                    } else {  // the reference divides (xs / num_kernels)
+#pragma unroll
+                      for (int j = 0; j < 16; ++j) v[j] = (r[j] + v[j]) / p.acc_div;
+                    }
                   } else {
 #pragma unroll
-                    for (int j = 0; j < 16; ++j) v[j] = r[j] + v[j];
+                    for (int i = 0; i < 8; ++i) pw(v, i, pr(r, i) + pr(v, i));
                   }
                 }
                 store16(yT + (size_t)orow * p.y_ld + co0, v);
+                if constexpr (!C::BF) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) v[j] = to_f32(from_f32<T>(v[j]));
+                  for (int j = 0; j < 16; ++j) v[j] = to_f32(from_f32<T>(v[j]));
+                }
                 stored = true;
               }
             }
@@ -578,7 +579,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
                 const int o = q * p.up + ph - p.opad;
                 if (o >= 0 && o < p.Lout) {
                   const int orow = o + p.y_row_off;
-                  x = v[j] + (p.bias ? p.bias[co] : 0.f);
+                  x = v[j] + bias_s[nl + j];
                   if (resb) x = (x + to_f32(resb[(size_t)(orow >> p.res_shift) * p.res_ld + co])) * p.out_scale;
                   if (p.epi_tanh) x = tanhf(x);
                   if (p.y_f32) {
@@ -594,25 +595,25 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv1d_igemm_kernel(co
             }
           }
         }
-        if (!stored) {
+        if (p.stats) {  // column pass over the wave scratch: lane = column l32, frames of half hi
+          if (!stored) {
 #pragma unroll
-          for (int j = 0; j < 16; ++j) v[j] = 0.f;
-        }
-        if (p.stats) {  // column pass over the wave scratch: lane = column l32, rows of half hi
+            for (int j = 0; j < 16; ++j) v[j] = 0.f;
+          }
 #pragma unroll
           for (int j = 0; j < 16; j += 4)
             *reinterpret_cast<float4*>(ws + l32 * EP + hi * 16 + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          float a = 0.f, q2 = 0.f;
+          f2v a2 = f2v{0.f, 0.f}, q2 = f2v{0.f, 0.f};
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float x = ws[(hi * 16 + r) * EP + l32];
-            a += x;
-            q2 += x * x;
+          for (int r = 0; r < 16; r += 2) {
+            const f2v x = f2v{ws[(hi * 16 + r) * EP + l32], ws[(hi * 16 + r + 1) * EP + l32]};
+            a2 += x;
+            q2 = __builtin_elementwise_fma(x, x, q2);
           }
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          st_s[ni] += a;
-          st_q[ni] += q2;
+          st_s[ni] += a2.x + a2.y;
+          st_q[ni] += q2.x + q2.y;
         }
       }
     }
@@ -636,8 +637,11 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
     p.tg = p.KS;
   } else {
     p.w_resident = 0;
-    int tg = (int)(WBUDGET / wtap);
-    if (tg < 1) tg = 1;
+    // a tap group must fit the per-thread W prefetch registers (MAXW 16-byte units per thread)
+    const int units_per_tap = C::BF ? C::BN * 4 : BK * (C::BN / 4);
+    int tg = 4 * C::NT / units_per_tap;
+    if ((size_t)tg * wtap > (size_t)WBUDGET) tg = (int)(WBUDGET / wtap);
+    if (tg < 1) return ST_EINVAL;
     if (tg > p.KS) tg = p.KS;
     while (tg > 1 && C::lds_bytes(p, tg) > (size_t)LDS_MAX) --tg;
     p.tg = tg;
@@ -693,6 +697,8 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   ConvParams q = p;
   if (q.kw <= 0) q.kw = q.KS;
   if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);
-  if (dtype == ST_BF16) return launch_typed<bf16_t, bf16_t>(q, stream);
+  if (dtype == ST_BF16) {
+    return launch_typed<bf16_t, bf16_t>(q, stream);
+  }
   return ST_EDTYPE;
 }

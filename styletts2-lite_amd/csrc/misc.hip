@@ -406,13 +406,14 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float* __restrict__ w, 
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   int c, tap, n, kl;
-  if (std::is_same<MT, bf16_t>::value) {  // [chunk][tap][Np][32]
-    kl = (int)(i % 32);
+  if (std::is_same<MT, bf16_t>::value) {  // [chunk][tap][Np][32], 16-B units XOR-swizzled by (n>>2)&3
+    const int kp = (int)(i % 32);
     size_t r = i / 32;
     n = (int)(r % Np);
     r /= Np;
     tap = (int)(r % taps);
     c = (int)(r / taps);
+    kl = 8 * ((kp >> 3) ^ ((n >> 2) & 3)) + (kp & 7);  // physical unit kp>>3 holds logical unit kl>>3
   } else {  // [chunk][tap][32][Np]
     n = (int)(i % Np);
     size_t r = i / Np;
@@ -420,6 +421,12 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float* __restrict__ w, 
     r /= 32;
     tap = (int)(r % taps);
     c = (int)(r / taps);
+  }
+  // row permutation inside each 32-block: packed row m holds column 16*((m>>2)&1) + (m&3) + 4*(m>>3),
+  // so the transposed MFMA output (C^T = W^T X^T) gives each lane 16 consecutive columns
+  {
+    const int m = n & 31;
+    n = (n & ~31) + 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3);
   }
   const int ci = c * 32 + kl;
   float val = 0.f;

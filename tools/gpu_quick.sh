@@ -1,0 +1,12 @@
+# quick GPU iteration: parity tests, per-layer roofline table, bench line
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -q -x --timeout 300 -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/layer_profile.py ${LAYER_ARGS} > gpurun_out/layers.txt 2>&1 || exit $?
+tail -1 gpurun_out/layers.txt
+timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/bench.log 2>&1 || exit $?
+tail -1 gpurun_out/bench.log | cut -c1-400
