@@ -90,6 +90,13 @@ int stts_style_fwd(stts_model* m, int dtype, const float* mel, int B, int T, flo
 
 const char* stts_error_string(int code);
 
+/* Engine options (process-wide, take effect on the next launch):
+ *   STTS_OPT_RESCONV  1 (default) = the specialised resblock conv engine serves the bf16
+ *                     C = 32 / 64 dilated convs; 0 = the general implicit-GEMM engine serves them
+ *                     (A/B measurement and cross-checking of the two engines). */
+#define STTS_OPT_RESCONV 1
+int stts_set_option(int key, int value);
+
 /* Optional per-kernel timing of the dominant kernel class (conv1d_igemm) with hipEvents recorded
  * on `stream` around each launch: enable, run, then read totals (ms, launches). */
 int stts_profile_enable(int on);

@@ -690,12 +690,15 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
 
 }  // namespace
 
+int g_opt_resconv = 1;
+
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (p.B <= 0 || p.Lq <= 0 || p.N <= 0) return ST_OK;
   if (p.KS <= 0 || p.stride <= 0 || p.dil <= 0 || p.Cout <= 0 || p.up <= 0) return ST_EINVAL;
   if (p.x_ld % 8 != 0 || p.nchunks * BK < p.Cin) return ST_EINVAL;
   ConvParams q = p;
   if (q.kw <= 0) q.kw = q.KS;
+  if (g_opt_resconv && st_resconv_eligible(q, dtype)) return st_resconv(q, stream);
   if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);
   if (dtype == ST_BF16) {
     return launch_typed<bf16_t, bf16_t>(q, stream);

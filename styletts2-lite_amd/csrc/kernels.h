@@ -48,6 +48,11 @@ struct ConvParams {
 };
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);
+// resblock conv engine (resconv.hip): bf16, C = 32 / 64, 1-D 'same' dilated conv with the
+// AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.
+bool st_resconv_eligible(const ConvParams& p, int dtype);
+int st_resconv(const ConvParams& p, hipStream_t stream);
+extern int g_opt_resconv;
 
 // ---------------------------------------------------------------- misc kernels
 // src [B][C][L] fp32 (torch NCL) -> dst frames [B][L][ld] at channel offset c0; optional stats.

@@ -1150,6 +1150,13 @@ const char* stts_error_string(int code) {
   }
 }
 
+int stts_set_option(int key, int value) {
+  switch (key) {
+    case STTS_OPT_RESCONV: g_opt_resconv = value != 0; return 0;
+    default: return ST_EINVAL;
+  }
+}
+
 int stts_profile_enable(int on) {
   g_prof.on = on != 0;
   g_prof.used = 0;

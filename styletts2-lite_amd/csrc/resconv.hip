@@ -1,0 +1,384 @@
+// Resblock conv engine for the small-channel generator stages (C = 32 / 64; HBM-bound):
+// the dilated Conv1d(C, C, K, dilation d, padding d(K-1)/2) of every AdaINResBlock1 iteration
+// (Modules/hifigan.py:26-80, forward :65-74), with the AdaIN -> Snake prologue and the bias /
+// residual / resblock-average / InstanceNorm-statistics epilogue fused.  bf16 storage, bf16 MFMA
+// (v_mfma_f32_32x32x16_bf16), fp32 accumulation.  The general engine (conv1d.hip) serves every
+// other conv; st_conv1d routes eligible launches here.
+//
+// What differs from the general engine (profiles/r01_pmc_*: waves parked ~45 % on s_waitcnt,
+// ~950 VALU instructions per tile-wave):
+//   * taps, dilation and channel count are template parameters: LDS operand addresses in the
+//     MFMA loop are one base per tap + immediates;
+//   * the raw input window is prefetched TWO tiles ahead (two named register sets, the tile
+//     loop unrolled by two), so each load has a full tile of MFMA + epilogue time to land;
+//   * the weights of the whole layer stay in LDS for the block's lifetime;
+//   * statistics are accumulated per lane in registers (a lane owns 16 channels of one frame)
+//     and reduced across lanes only when the block leaves an utterance.
+#include "common.h"
+#include "conv_common.h"
+#include "kernels.h"
+
+namespace {
+
+template <int C, int K, int DIL, int WAVES, int WAVES_N>
+struct RC {
+  static constexpr int NT = 64 * WAVES;              // threads per block
+  static constexpr int FW = 64;                      // frames per wave
+  static constexpr int MT = FW / 32;                 // 32-frame blocks per wave
+  static constexpr int BM = (WAVES / WAVES_N) * FW;  // frames per tile
+  static constexpr int NTL = C / 32 / WAVES_N;       // 32-channel output blocks per wave
+  static constexpr int NCH = C / 32;                 // 32-channel K chunks
+  static constexpr int PAD = DIL * (K - 1) / 2;      // 'same' padding
+  static constexpr int R = BM + DIL * (K - 1);       // window rows
+  static constexpr int XP = C + 8;                   // window row pitch (bf16): conflict-free ds_read_b128
+  static constexpr int WP = 40;                      // weight row pitch (bf16): 32 + 8
+  static constexpr int G8 = C / 8;                   // 8-channel groups per window row
+  static constexpr int UNITS = R * G8;               // 16-byte window units per tile
+  static constexpr int MAXU = (UNITS + NT - 1) / NT;
+  static constexpr int OFF_BIAS = 4 * C * 4;         // after coef [4][C] f32
+  static constexpr int OFF_W = OFF_BIAS + C * 4;
+  static constexpr int W_B = NCH * K * C * WP * 2;
+  static constexpr int OFF_X = OFF_W + W_B;
+  static constexpr int LDS = OFF_X + R * XP * 2;
+  static_assert(NT % G8 == 0, "a thread's window units must share one 8-channel group");
+  static_assert(OFF_W % 16 == 0 && OFF_X % 16 == 0, "LDS carve alignment");
+  static_assert(NTL >= 1 && WAVES % WAVES_N == 0, "wave grid");
+};
+
+__device__ __forceinline__ void bf8_to_f32(const uint4& r, float (&v)[8]) {
+  const unsigned w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 f32_to_bf8(const float* v) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16_t)v[j];
+  uint4 r;
+  __builtin_memcpy(&r, &o, 16);
+  return r;
+}
+
+// ACC: the launch adds the output into the resblock running sum (p.accb, p.acc_div) and keeps
+// no statistics (hifigan.py:336-342); otherwise statistics are kept when p.stats is set.
+template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC>
+__global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvParams p) {
+  using G = RC<C, K, DIL, WAVES, WAVES_N>;
+  constexpr int NT = G::NT, BM = G::BM, MT = G::MT, NTL = G::NTL, NCH = G::NCH, XP = G::XP, WP = G::WP;
+  constexpr int G8 = G::G8, UNITS = G::UNITS, MAXU = G::MAXU, FW = G::FW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* coef = reinterpret_cast<float*>(smem);  // [4][C]: beta - mean*a, a, alpha/2pi, 1/alpha
+  float* bias_s = reinterpret_cast<float*>(smem + G::OFF_BIAS);
+  bf16_t* Ws = reinterpret_cast<bf16_t*>(smem + G::OFF_W);  // [chunk][tap][n][WP], logical k order
+  bf16_t* Xs = reinterpret_cast<bf16_t*>(smem + G::OFF_X);  // [R][XP], prologue applied
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int wn = wid % WAVES_N, wm = wid / WAVES_N;
+  const int ntm = (p.Lq + BM - 1) / BM;
+  const long long total = (long long)ntm * p.B;
+  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
+  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
+  if (tbeg >= tend) return;  // uniform over the block
+
+  // ---- layer constants -> LDS, once per block
+  {
+    const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)NCH * K * C * 32 * 2));
+    constexpr int WU = NCH * K * C * 4;  // 16-byte units
+    for (int u = tid; u < WU; u += NT) {
+      const int g = u & 3, n = (u >> 2) % C, ct = (u >> 2) / C;  // ct = chunk * K + tap
+      const unsigned off = (unsigned)((((size_t)ct * C + n) * 32 + 8 * (g ^ ((n >> 2) & 3))) * 2);
+      *reinterpret_cast<uint4*>(Ws + ((size_t)ct * C + n) * WP + 8 * g) = bload16(rw, off);
+    }
+    for (int i = tid; i < C; i += NT) bias_s[i] = p.bias ? p.bias[i] : 0.f;
+  }
+
+  const int g8 = tid % G8;  // this thread's 8-channel group in every window unit
+  auto issue = [&](int t, uint4 (&pre)[MAXU]) __attribute__((always_inline)) {
+    const int b = t / ntm, mt = t - b * ntm;
+    const Rsrc rx = make_rsrc(reinterpret_cast<const bf16_t*>(p.x) + (size_t)b * p.x_bs,
+                              (unsigned)((size_t)p.Lin * p.x_ld * 2));
+    const int gr0 = mt * BM - G::PAD;
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      const int u = tid + k * NT;
+      const int e = (gr0 + u / G8) * p.x_ld + 8 * g8;  // rows past Lin read 0 (descriptor range)
+      const bool in = (k + 1) * NT <= UNITS || u < UNITS;
+      pre[k] = bload16(rx, in && e >= 0 ? (unsigned)e * 2u : OOB);
+    }
+  };
+
+  // epilogue prefetch: residual rows of the tile (16 channels of one frame per lane)
+  uint4 rres[MT][NTL][2];
+  auto issue_epi = [&](int t) __attribute__((always_inline)) {
+    const int b = t / ntm, mt = t - b * ntm;
+    const bool hr = p.res != nullptr;
+    const Rsrc rr = make_rsrc(hr ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr,
+                              hr ? (unsigned)((size_t)p.Lq * p.res_ld * 2) : 0u);
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int q = mt * BM + wm * FW + mi * 32 + l32;
+#pragma unroll
+      for (int ni = 0; ni < NTL; ++ni) {
+        const int co0 = (wn * NTL + ni) * 32 + hi * 16;
+        const unsigned er = (unsigned)(q * p.res_ld + co0) * 2u;
+        rres[mi][ni][0] = bload16(rr, er);
+        rres[mi][ni][1] = bload16(rr, er + 16u);
+      }
+    }
+  };
+
+  // per-lane statistics of the stored outputs: lane (frame l32, half hi) owns channels
+  // (wn*NTL + ni)*32 + 16*hi + r of every frame it stores
+  float st_s[ACC ? 1 : NTL][16], st_q[ACC ? 1 : NTL][16];
+  if constexpr (!ACC) {
+#pragma unroll
+    for (int ni = 0; ni < NTL; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st_s[ni][r] = st_q[ni][r] = 0.f;
+  }
+  auto flush = [&](int b) __attribute__((always_inline)) {
+    if constexpr (!ACC) {
+#pragma unroll
+      for (int ni = 0; ni < NTL; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float a = st_s[ni][r], q = st_q[ni][r];
+#pragma unroll
+          for (int o = 16; o >= 1; o >>= 1) {
+            a += __shfl_xor(a, o);
+            q += __shfl_xor(q, o);
+          }
+          if (l32 == 0) {
+            double* d = p.stats + ((size_t)b * p.stats_ld + (wn * NTL + ni) * 32 + hi * 16 + r) * 2;
+            atomicAdd(d, (double)a);
+            atomicAdd(d + 1, (double)q);
+          }
+          st_s[ni][r] = st_q[ni][r] = 0.f;
+        }
+    }
+  };
+
+  auto transform = [&](int t, const uint4 (&pre)[MAXU]) __attribute__((always_inline)) {
+    const int mt = t % ntm;
+    const int gr0 = mt * BM - G::PAD;
+    float a[8], m[8], al[8], ia[8];
+    ld8_lds(coef + 8 * g8, m);
+    ld8_lds(coef + C + 8 * g8, a);
+    ld8_lds(coef + 2 * C + 8 * g8, al);
+    ld8_lds(coef + 3 * C + 8 * g8, ia);
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      const int u = tid + k * NT;
+      if ((k + 1) * NT <= UNITS || u < UNITS) {
+        const int r = u / G8;
+        const bool ok = (unsigned)(gr0 + r) < (unsigned)p.Lin;  // conv zero padding is post-prologue
+        float v[8];
+        bf8_to_f32(pre[k], v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = __builtin_fmaf(v[j], a[j], m[j]);  // (x - mean) * a + beta
+          const float s = __builtin_amdgcn_sinf(x * al[j]);  // v_sin_f32 takes revolutions
+          v[j] = ok ? __builtin_fmaf(s * s, ia[j], x) : 0.f;
+        }
+        *reinterpret_cast<uint4*>(Xs + r * XP + 8 * g8) = f32_to_bf8(v);
+      }
+    }
+  };
+
+  int cur_b = -1;
+  auto step = [&](int t, uint4 (&pre)[MAXU]) __attribute__((always_inline)) {
+    const int b = t / ntm, mt = t - b * ntm;
+    if (b != cur_b) {
+      if (cur_b >= 0 && p.stats) flush(cur_b);
+      // every wave is past its previous transform (barrier B of the previous step): coef is free
+      for (int ci = tid; ci < C; ci += NT) {
+        float mm, aa, be;
+        adain_coeffs(p.pro, b, ci, mm, aa, be);
+        const float al = p.pro.alpha[ci];
+        coef[ci] = be - mm * aa;
+        coef[C + ci] = aa;
+        coef[2 * C + ci] = al * 0.15915494309189535f;
+        coef[3 * C + ci] = 1.0f / al;
+      }
+      cur_b = b;
+    }
+    issue_epi(t);
+    __syncthreads();  // (A) coef / weights visible; every wave done reading Xs of the previous tile
+    transform(t, pre);
+    if (t + 2 < tend) issue(t + 2, pre);
+    __syncthreads();  // (B) window complete
+
+    f32x16 acc[MT][NTL];
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NTL; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+    const bf16_t* xw = Xs + (size_t)(wm * FW + l32) * XP + hi * 8;
+    const bf16_t* ww = Ws + (size_t)(wn * NTL * 32 + l32) * WP + hi * 8;
+#pragma unroll 1
+    for (int tap = 0; tap < K; ++tap) {
+      const bf16_t* xt = xw + tap * DIL * XP;
+      const bf16_t* wt = ww + tap * C * WP;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          bf16x8 wa[NTL], xb[MT];
+#pragma unroll
+          for (int ni = 0; ni < NTL; ++ni)
+            wa[ni] = *reinterpret_cast<const bf16x8*>(wt + (c * K * C + ni * 32) * WP + kk * 16);
+#pragma unroll
+          for (int mi = 0; mi < MT; ++mi)
+            xb[mi] = *reinterpret_cast<const bf16x8*>(xt + mi * 32 * XP + c * 32 + kk * 16);
+#pragma unroll
+          for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NTL; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ni], xb[mi], acc[mi][ni], 0, 0, 0);
+        }
+    }
+
+    // ---- epilogue: lane = frame l32 of block mi, channels (wn*NTL + ni)*32 + 16*hi + r
+    bf16_t* yb = reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs;
+    const bf16_t* ab = ACC ? reinterpret_cast<const bf16_t*>(p.accb) + (size_t)b * p.acc_bs : nullptr;
+    const bool hr = p.res != nullptr;
+    const float osc = p.out_scale;
+    const float adiv = (ACC && p.acc_div != 0.f) ? 1.0f / p.acc_div : 1.0f;
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int q = mt * BM + wm * FW + mi * 32 + l32;
+      const bool valid = q < p.Lq;
+#pragma unroll
+      for (int ni = 0; ni < NTL; ++ni) {
+        const int co0 = (wn * NTL + ni) * 32 + hi * 16;
+        float v[16], bb[16];
+        ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
+        ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[mi][ni][r] + bb[r];
+        if (hr) {
+          float r0[8], r1[8];
+          bf8_to_f32(rres[mi][ni][0], r0);
+          bf8_to_f32(rres[mi][ni][1], r1);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            v[r] = (v[r] + r0[r]) * osc;
+            v[8 + r] = (v[8 + r] + r1[r]) * osc;
+          }
+        }
+        if (valid) {
+          if constexpr (ACC) {
+            const uint4* ap = reinterpret_cast<const uint4*>(ab + (size_t)q * p.acc_ld + co0);
+            float r0[8], r1[8];
+            bf8_to_f32(ap[0], r0);
+            bf8_to_f32(ap[1], r1);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              v[r] = (r0[r] + v[r]) * adiv;
+              v[8 + r] = (r1[r] + v[8 + r]) * adiv;
+            }
+          }
+          bf16_t* dst = yb + (size_t)q * p.y_ld + co0;
+          *reinterpret_cast<uint4*>(dst) = f32_to_bf8(&v[0]);
+          *reinterpret_cast<uint4*>(dst + 8) = f32_to_bf8(&v[8]);
+          if constexpr (!ACC) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              st_s[ni][r] += v[r];
+              st_q[ni][r] = __builtin_fmaf(v[r], v[r], st_q[ni][r]);
+            }
+          }
+        }
+      }
+    }
+  };
+
+  uint4 preA[MAXU], preB[MAXU];
+  issue(tbeg, preA);
+  if (tbeg + 1 < tend) issue(tbeg + 1, preB);
+  for (int t = tbeg; t < tend; t += 2) {
+    step(t, preA);
+    if (t + 1 < tend) step(t + 1, preB);
+  }
+  if (p.stats) flush(cur_b);
+}
+
+int g_num_cu_rc = 0;
+
+template <int C, int K, int DIL, bool ACC>
+int launch_rc(const ConvParams& p, hipStream_t stream) {
+  constexpr int WAVES = C == 32 ? 4 : 8;
+  constexpr int WAVES_N = C == 32 ? 1 : 2;
+  using G = RC<C, K, DIL, WAVES, WAVES_N>;
+  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC>;
+  static bool attr = false;
+  if (!attr) {
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    attr = true;
+  }
+  if (!g_num_cu_rc) {
+    int dev = 0;
+    ST_CHECK_HIP(hipGetDevice(&dev));
+    ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_rc, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  int per_cu = 0;
+  ST_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, G::NT, G::LDS));
+  if (per_cu < 1) per_cu = 1;
+  const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
+  long long grid = (long long)g_num_cu_rc * per_cu;
+  if (grid > tiles) grid = tiles;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, p);
+  return (int)hipGetLastError();
+}
+
+template <int C, int K, int DIL>
+int launch_rc_a(const ConvParams& p, hipStream_t s) {
+  return p.accb ? launch_rc<C, K, DIL, true>(p, s) : launch_rc<C, K, DIL, false>(p, s);
+}
+
+template <int C, int K>
+int launch_rc_d(const ConvParams& p, hipStream_t s) {
+  switch (p.dil) {
+    case 1: return launch_rc_a<C, K, 1>(p, s);
+    case 3: return launch_rc_a<C, K, 3>(p, s);
+    case 5: return launch_rc_a<C, K, 5>(p, s);
+    default: return ST_EINVAL;
+  }
+}
+
+template <int C>
+int launch_rc_k(const ConvParams& p, hipStream_t s) {
+  switch (p.KS) {
+    case 3: return launch_rc_d<C, 3>(p, s);
+    case 7: return launch_rc_d<C, 7>(p, s);
+    case 11: return launch_rc_d<C, 11>(p, s);
+    default: return ST_EINVAL;
+  }
+}
+
+}  // namespace
+
+bool st_resconv_eligible(const ConvParams& p, int dtype) {
+  if (dtype != ST_BF16) return false;
+  const int C = p.Cout;
+  if (!(C == 32 || C == 64) || p.Cin != C || p.N != C || p.nchunks * 32 != C) return false;
+  if (!(p.KS == 3 || p.KS == 7 || p.KS == 11) || !(p.dil == 1 || p.dil == 3 || p.dil == 5)) return false;
+  if ((p.kw != 0 && p.kw != p.KS) || p.row_off != 0 || p.stride != 1 || p.up != 1 || p.opad != 0) return false;
+  if (p.pad != p.dil * (p.KS - 1) / 2 || p.Lq != p.Lout || p.Lq != p.Lin) return false;
+  if (p.y_row_off || p.y_f32 || p.epi_tanh || p.reflect_front || p.zc_period || p.res_shift) return false;
+  if (p.pro.mode != (PRO_AFFINE | PRO_SNAKE) || !p.pro.alpha || !p.pro.stats || !p.pro.gamma) return false;
+  if (p.accb && p.stats) return false;  // the running-sum launch keeps no statistics
+  if (p.x_ld % 8 || p.y_ld % 8 || (p.res && p.res_ld % 8) || (p.accb && p.acc_ld % 8)) return false;
+  return true;
+}
+
+int st_resconv(const ConvParams& p, hipStream_t stream) {
+  if (p.Cout == 32) return launch_rc_k<32>(p, stream);
+  if (p.Cout == 64) return launch_rc_k<64>(p, stream);
+  return ST_EINVAL;
+}

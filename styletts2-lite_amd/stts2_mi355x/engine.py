@@ -67,8 +67,18 @@ def lib():
     L.stts_profile_read.restype = c_int
     L.stts_profile_launch.argtypes = [c_ll, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double)]
     L.stts_profile_launch.restype = c_int
+    L.stts_set_option.argtypes = [c_int, c_int]
+    L.stts_set_option.restype = c_int
     _LIB = L
     return L
+
+
+OPT_RESCONV = 1
+
+
+def set_option(key: int, value: int) -> None:
+    """Process-wide engine option (include/stts2.h STTS_OPT_*)."""
+    check(lib().stts_set_option(int(key), int(value)), "stts_set_option")
 
 
 def check(rc: int, what: str = "stts"):

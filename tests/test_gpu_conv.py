@@ -18,6 +18,10 @@ CASES = [
     ("rb64_k7_d3", 64, 64, 7, 0, 1, 3, 9, 0, 333, 3),
     ("rb128_k3_d1", 128, 128, 3, 0, 1, 1, 1, 0, 257, 3),
     ("rb256_k11_d1", 256, 256, 11, 0, 1, 1, 5, 0, 130, 3),
+    ("rb32_k3_d1", 32, 32, 3, 0, 1, 1, 1, 0, 1300, 3),
+    ("rb32_k7_d3", 32, 32, 7, 0, 1, 3, 9, 0, 517, 3),
+    ("rb64_k11_d5", 64, 64, 11, 0, 1, 5, 25, 0, 600, 3),
+    ("rb64_k3_d1", 64, 64, 3, 0, 1, 1, 1, 0, 2049, 3),
     ("front_1090_1024", 1090, 1024, 3, 0, 1, 1, 1, 0, 40, 5),
     ("sc_1x1", 514, 1024, 1, 0, 1, 1, 0, 0, 37, 0),
     ("istft_noise_s6", 22, 256, 12, 0, 6, 1, 3, 0, 481, 0),
@@ -52,9 +56,7 @@ def reference(x, w, b, gb, alpha, slope, res, scale, c):
     return y * scale
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_conv_engine(case, dtype):
+def run_case(case, dtype):
     name, Cin, Cout, K, tr, st, dil, pad, op, L, pro = case
     g = torch.Generator().manual_seed(hash(name) % 1000)
     B = 2
@@ -78,11 +80,17 @@ def test_conv_engine(case, dtype):
                                   pro, P(gbd), P(ad), ctypes.c_float(slope), P(rd), ctypes.c_float(scale), P(y), Lout,
                                   P(st_out))
     E.check(rc)
-    y = y.cpu()
+    return ref, y.cpu(), st_out.cpu()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_conv_engine(case, dtype):
+    name = case[0]
+    ref, y, s = run_case(case, dtype)
     err = (y - ref).abs().max().item()
     tol = 2e-4 if dtype == "fp32" else 0.03 * max(1.0, ref.abs().max().item() / 4)
     assert err < tol, f"{name} {dtype}: max err {err}"
-    s = st_out.cpu()
     yd = y.double()
     if dtype == "fp32":
         np.testing.assert_allclose(s[..., 0].numpy(), yd.sum(1).numpy(), rtol=1e-5, atol=1e-3)
@@ -94,3 +102,23 @@ def test_conv_engine(case, dtype):
         bound_q = (yd ** 2).sum(1) * 2.0 ** -7 + 1e-3
         assert ((s[..., 0] - yd.sum(1)).abs() <= bound_s).all(), f"{name}: sum statistics"
         assert ((s[..., 1] - (yd ** 2).sum(1)).abs() <= bound_q).all(), f"{name}: square statistics"
+
+
+RB_CASES = [c for c in CASES if c[0].startswith("rb32") or c[0].startswith("rb64")]
+
+
+@pytest.mark.parametrize("case", RB_CASES, ids=[c[0] for c in RB_CASES])
+def test_resconv_engine_matches_general_engine(case):
+    """bf16: the specialised resblock engine (resconv.hip) against the general implicit-GEMM
+    engine on the same launch: same bf16 operands, fp32 accumulation in a different order."""
+    try:
+        E.set_option(E.OPT_RESCONV, 1)
+        _, y1, s1 = run_case(case, "bf16")
+        E.set_option(E.OPT_RESCONV, 0)
+        _, y0, s0 = run_case(case, "bf16")
+    finally:
+        E.set_option(E.OPT_RESCONV, 1)
+    scale = max(1.0, y0.abs().max().item())
+    err = (y1 - y0).abs().max().item()
+    assert err <= 2 ** -7 * scale, f"{case[0]}: engines differ by {err}"
+    np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)

@@ -89,3 +89,20 @@ def test_decoder_deterministic_repeat():
     a = run("hifigan", 2, 16, "fp32")
     b = run("hifigan", 2, 16, "fp32")
     assert np.abs(a - b).max() < 1e-5  # fp64 stats atomics may reorder; within rounding
+
+
+def test_resconv_engine_decoder_ab():
+    """bf16 HiFi-GAN decode with the resblock engine on and off: both are the same bf16 model;
+    they differ only by fp32 accumulation order (and bf16 rounding of intermediates)."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_RESCONV, 0)
+        ref = run("hifigan", 2, 40, "bf16")
+        E.set_option(E.OPT_RESCONV, 1)
+        out = run("hifigan", 2, 40, "bf16")
+    finally:
+        E.set_option(E.OPT_RESCONV, 1)
+    corr = np.corrcoef(out.ravel(), ref.ravel())[0, 1]
+    err = np.abs(out - ref).max()
+    print(f"resconv A/B: max-abs {err:.3e} corr {corr:.7f}")
+    assert corr > 0.9995 and err < 5e-2
