@@ -73,6 +73,14 @@ struct SmallConvDst {
 int st_conv_cin1(const float* in, long long in_bs, int Lin, int B, const float* w, const float* bias, int C,
                  int K, int stride, int pad, int Lout, const SmallConvDst* dst, int ndst, int dtype,
                  hipStream_t s);
+// HiFi-GAN noise_convs[s] = Conv1d(1, C, K, stride S, padding P) over har fp32 [B][L] ->
+// frames (dtype) [B][Lout][C] + statistics (K in {1, 4, 12}; VALU kernel)
+int st_noise_conv(const float* har, int B, int L, const float* w, const float* bias, int C, int K, int S, int P,
+                  int Lout, void* y, double* stats, int dtype, hipStream_t s);
+// har fp32 [B][L] -> S-sample frames (dtype) [B][rows][ld]: x[r][j] = har[S*r - P + j] (j < S), else 0
+int st_har_frames(const float* har, int B, int L, int S, int P, int rows, int ld, void* x, int dtype, hipStream_t s);
+// noise_convs weight [C][1][2S] -> [C][S][2] (the 2-tap conv over S-sample frames)
+int st_reframe_w(const float* w, int C, int S, float* out, hipStream_t s);
 // SineGen phase: ph[b][h][j] = ((cumsum_f64(rad)[j] * 2) * pi) * scale  (fp32)
 int st_sine_phase(const float* f0, int B, int n, int scale, float* ph, hipStream_t s);
 // SineGen + SourceModuleHnNSF: har[b][t] (fp32), t < n*scale

@@ -178,21 +178,29 @@ __global__ void __launch_bounds__(256) k_conv_cin1(const float* __restrict__ in,
 // equal samples of the nearest-upsampled curve (src = scale*j + (scale-1)/2), so the
 // downsampled value is rad(f0[j]) exactly; cumsum accumulates in fp64 and rounds per
 // element (PyTorch-CPU semantics); phase = (cum*2)*pi, then *scale.
-__global__ void k_sine_phase(const float* __restrict__ f0, int B, int n, int scale, float* ph) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * 9) return;
-  const int b = i / 9, h = i % 9;
+// One block per utterance: the F0 row is staged in LDS (coalesced), then one thread per
+// harmonic runs the serial fp64 prefix sum (PyTorch-CPU cumsum accumulates in fp64 and rounds
+// each prefix: SURVEY.md App. B) out of LDS instead of a dependent global load per step.
+__global__ void __launch_bounds__(64) k_sine_phase(const float* __restrict__ f0, int B, int n, int scale,
+                                                   float* __restrict__ ph) {
+  extern __shared__ float f0s[];
+  const int b = blockIdx.x;
+  for (int j = threadIdx.x; j < n; j += 64) f0s[j] = f0[(size_t)b * n + j];
+  __syncthreads();
+  const int h = threadIdx.x;
+  if (h >= 9) return;
   const float hm = (float)(h + 1);
   const float pi_f = (float)3.14159265358979323846;
   const float sc = (float)scale;
   double cum = 0.0;
+  float* out = ph + ((size_t)b * 9 + h) * n;
   for (int j = 0; j < n; ++j) {
-    const float fn = f0[(size_t)b * n + j] * hm;
+    const float fn = f0s[j] * hm;
     float r = fn / 24000.0f;
     r = r - floorf(r);
     cum += (double)r;
     const float c = (float)cum;
-    ph[((size_t)b * 9 + h) * n + j] = ((c * 2.0f) * pi_f) * sc;
+    out[j] = ((c * 2.0f) * pi_f) * sc;
   }
 }
 
@@ -284,25 +292,142 @@ __global__ void __launch_bounds__(256) k_pool_dw(const T* __restrict__ x, long l
 
 // ------------------------------------------------------------------ style projections
 // H[b][n] = bias[n] + sum_k s[b][k] * Wt[k][n]   (Wt packed [K][N] at load)
+// H[b][n] = bias[n] + sum_k s[b][k] * Wt[k][n] for up to 32 utterances per block: the style
+// rows sit in LDS, each thread owns one column n and streams Wt[:, n] (coalesced across the
+// block) with 8 loads in flight.
 __global__ void __launch_bounds__(256) k_linear(const float* __restrict__ s, int B, int K,
                                                 const float* __restrict__ Wt, const float* __restrict__ bias, int N,
-                                                float* H) {
+                                                float* __restrict__ H) {
+  extern __shared__ float ss[];  // [32][K]
+  const int b0 = blockIdx.y * 32, nb = min(32, B - b0);
+  for (int i = threadIdx.x; i < nb * K; i += 256) ss[i] = s[(size_t)b0 * K + i];
+  __syncthreads();
   const int n = blockIdx.x * 256 + threadIdx.x;
-  const int b0 = blockIdx.y * 16;
   if (n >= N) return;
-  float acc[16];
+  float acc[32];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  for (int k = 0; k < K; ++k) {
+  for (int i = 0; i < 32; ++i) acc[i] = 0.f;
+  int k = 0;
+  for (; k + 8 <= K; k += 8) {
+    float wv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) wv[u] = Wt[(size_t)(k + u) * N + n];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int i = 0; i < 32; ++i)
+        if (i < nb) acc[i] = fmaf(ss[i * K + k + u], wv[u], acc[i]);
+  }
+  for (; k < K; ++k) {
     const float wv = Wt[(size_t)k * N + n];
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (b0 + i < B) acc[i] = fmaf(s[(size_t)(b0 + i) * K + k], wv, acc[i]);
+    for (int i = 0; i < 32; ++i)
+      if (i < nb) acc[i] = fmaf(ss[i * K + k], wv, acc[i]);
   }
   const float bv = bias ? bias[n] : 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (b0 + i < B) H[(size_t)(b0 + i) * N + n] = acc[i] + bv;
+  for (int i = 0; i < 32; ++i)
+    if (i < nb) H[(size_t)(b0 + i) * N + n] = acc[i] + bv;
+}
+
+// ------------------------------------------------------------------ HiFi-GAN noise_convs
+// Conv1d(1, C, K = 2S, stride S, padding P) over the harmonic source (hifigan.py:296-303).
+// (a) small C*K (stages 1..3): one thread per (frame, 8 channels), weights in registers,
+//     16-byte stores, statistics reduced in registers -> shuffles -> one atomic per channel.
+template <typename T, int K>
+__global__ void __launch_bounds__(256) k_noise_conv(const float* __restrict__ har, int L,
+                                                    const float* __restrict__ w, const float* __restrict__ bias,
+                                                    int C, int S, int P, int Lout, int fpb, T* __restrict__ y,
+                                                    double* __restrict__ stats) {
+  const int G = C >> 3;  // C % 8 == 0, 256 % G == 0
+  const int b = blockIdx.y;
+  const int g = threadIdx.x % G, fl = threadIdx.x / G, fstep = 256 / G;
+  float wr[8][K], bb[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    bb[c] = bias ? bias[8 * g + c] : 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) wr[c][k] = w[(size_t)(8 * g + c) * K + k];
+  }
+  float sa[8], sq[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) sa[c] = sq[c] = 0.f;
+  const float* hb = har + (size_t)b * L;
+  T* yb = y + (size_t)b * Lout * C + 8 * g;
+  const int f1 = min((blockIdx.x + 1) * fpb, Lout);
+  for (int f = blockIdx.x * fpb + fl; f < f1; f += fstep) {
+    float x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = f * S - P + k;
+      x[k] = (i >= 0 && i < L) ? hb[i] : 0.f;
+    }
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) a = fmaf(wr[c][k], x[k], a);
+      v[c] = to_f32(from_f32<T>(a + bb[c]));  // statistics of the stored values
+    }
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 o;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[c] = (bf16_t)v[c];
+      *reinterpret_cast<bf16x8*>(yb + (size_t)f * C) = o;
+    } else {
+      *reinterpret_cast<float4*>(yb + (size_t)f * C) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(yb + (size_t)f * C + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      sa[c] += v[c];
+      sq[c] = fmaf(v[c], v[c], sq[c]);
+    }
+  }
+  if (!stats) return;
+  // lanes l, l+G, l+2G, ... of a wave share g
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    for (int o = G; o < 64; o <<= 1) {
+      sa[c] += __shfl_xor(sa[c], o);
+      sq[c] += __shfl_xor(sq[c], o);
+    }
+  if ((threadIdx.x & 63) < G) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) atomic_stats(stats + ((size_t)b * C + 8 * g + c) * 2, sa[c], sq[c]);
+  }
+}
+
+// (b) large C*K (stage 0, K = 60): the source is cut into S-sample frames,
+//     X[r][j] = har[S*r - P + j] (j < S, zero-padded to ld channels), so the strided conv is a
+//     2-tap stride-1 conv with Cin = S that runs on the MFMA engine (weights: k_reframe_w).
+template <typename T>
+__global__ void __launch_bounds__(256) k_har_frames(const float* __restrict__ har, int L, int S, int P, int rows,
+                                                    int ld, T* __restrict__ x) {
+  const int b = blockIdx.y;
+  const int gpr = ld >> 3;
+  const long long u = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (u >= (long long)rows * gpr) return;
+  const int r = (int)(u / gpr), j0 = (int)(u % gpr) * 8;
+  const float* hb = har + (size_t)b * L;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int i = r * S - P + j0 + j;
+    v[j] = (j0 + j < S && i >= 0 && i < L) ? hb[i] : 0.f;
+  }
+  T* dst = x + ((size_t)b * rows + r) * ld + j0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dst[j] = from_f32<T>(v[j]);
+}
+
+// w [C][1][2S] (nn.Conv1d) -> w' [C][S][2]: w'[c][j][t] = w[c][t*S + j]
+__global__ void k_reframe_w(const float* __restrict__ w, int C, int S, float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= C * S * 2) return;
+  const int t = i % 2, j = (i / 2) % S, c = i / (2 * S);
+  out[i] = w[(size_t)c * 2 * S + t * S + j];
 }
 
 // ------------------------------------------------------------------ column statistics
@@ -577,7 +702,12 @@ int st_conv_cin1(const float* in, long long in_bs, int Lin, int B, const float* 
 }
 
 int st_sine_phase(const float* f0, int B, int n, int scale, float* ph, hipStream_t s) {
-  hipLaunchKernelGGL(k_sine_phase, dim3((B * 9 + 63) / 64), dim3(64), 0, s, f0, B, n, scale, ph);
+  const size_t lds = (size_t)n * 4;
+  if (lds > 64 * 1024) {
+    if (lds > 160 * 1024) return ST_EINVAL;
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)k_sine_phase, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  }
+  hipLaunchKernelGGL(k_sine_phase, dim3(B), dim3(64), lds, s, f0, B, n, scale, ph);
   return (int)hipGetLastError();
 }
 
@@ -598,7 +728,9 @@ int st_pool_dw(const void* x, long long x_bs, int x_ld, int B, int Lin, int C, c
 }
 
 int st_linear(const float* s, int B, int K, const float* Wt, const float* bias, int N, float* H, hipStream_t st) {
-  hipLaunchKernelGGL(k_linear, dim3((N + 255) / 256, (B + 15) / 16), dim3(256), 0, st, s, B, K, Wt, bias, N, H);
+  const size_t lds = (size_t)32 * K * 4;
+  if (lds > 64 * 1024) return ST_EINVAL;
+  hipLaunchKernelGGL(k_linear, dim3((N + 255) / 256, (B + 31) / 32), dim3(256), lds, st, s, B, K, Wt, bias, N, H);
   return (int)hipGetLastError();
 }
 
@@ -688,5 +820,37 @@ int st_gap_linear(const void* z, int B, int rows, int Wv, int C, const float* w,
                   int dtype, hipStream_t s) {
   DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_gap_linear<T>, dim3(B), dim3(256), C * sizeof(float), s,
                                               reinterpret_cast<const T*>(z), rows, Wv, C, w, bias, N, out));
+  return (int)hipGetLastError();
+}
+
+int st_noise_conv(const float* har, int B, int L, const float* w, const float* bias, int C, int K, int S, int P,
+                  int Lout, void* y, double* stats, int dtype, hipStream_t s) {
+  if (C % 8 || 256 % (C / 8)) return ST_EINVAL;
+  const int fpb = 1024;
+  dim3 grid((Lout + fpb - 1) / fpb, B);
+#define NCONV(KC)                                                                                              \
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_noise_conv<T, KC>), grid, dim3(256), 0, s, har, L, w, bias, C, S, \
+                                              P, Lout, fpb, reinterpret_cast<T*>(y), stats))
+  switch (K) {
+    case 1: NCONV(1); break;
+    case 4: NCONV(4); break;
+    case 12: NCONV(12); break;
+    default: return ST_EINVAL;
+  }
+#undef NCONV
+  return (int)hipGetLastError();
+}
+
+int st_har_frames(const float* har, int B, int L, int S, int P, int rows, int ld, void* x, int dtype, hipStream_t s) {
+  if (ld % 8 || S > ld) return ST_EINVAL;
+  const long long units = (long long)rows * (ld / 8);
+  dim3 grid((unsigned)((units + 255) / 256), B);
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_har_frames<T>, grid, dim3(256), 0, s, har, L, S, P, rows, ld,
+                                              reinterpret_cast<T*>(x)));
+  return (int)hipGetLastError();
+}
+
+int st_reframe_w(const float* w, int C, int S, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_reframe_w, dim3((C * S * 2 + 255) / 256), dim3(256), 0, s, w, C, S, out);
   return (int)hipGetLastError();
 }

@@ -51,6 +51,7 @@ struct Params {
 struct WConv {
   int v = -1, g = -1, bias = -1;
   int Cin = 0, Cout = 0, K = 0, transposed = 0, u = 1;
+  int reframe = 0;  // > 0: a Conv1d(1, Cout, 2S, stride S) packed as a 2-tap conv over S-sample frames
   size_t off[2] = {0, 0};
   int taps() const { return transposed ? (K + u - 1) / u : K; }
   int N() const { return transposed ? u * Cout : Cout; }
@@ -96,7 +97,8 @@ struct stts_model {
   Small F0_conv, N_conv;
   WConv asr_res;
   int l_lin_w = -1, l_lin_b = -1;
-  std::vector<int> nc_w, nc_b;      // hifigan noise_convs (Cin=1): raw [C][K]
+  std::vector<int> nc_w, nc_b;      // hifigan noise_convs (Cin=1): raw [C][K] (VALU kernel), -1 if nc_mm
+  std::vector<WConv> nc_mm;         // hifigan noise_convs with K >= 16: 2-tap MFMA conv over S-sample frames
   std::vector<WConv> nc_conv;       // istftnet noise_convs (Cin=n_fft+2): igemm
   std::vector<WConv> ups;
   std::vector<ResBlock1> noise_res, resblocks;
@@ -241,6 +243,7 @@ int build_decoder(Model& m, const int* cfg, int n) {
   m.noise_res.resize(nup);
   m.resblocks.resize((size_t)nup * nrb);
   if (ist) m.nc_conv.resize(nup);
+  else m.nc_mm.resize(nup);
   static const int d135[3] = {1, 3, 5};
   for (int s = 0; s < nup; ++s) {
     const int u = m.rates[s], k = m.kernels[s];
@@ -253,6 +256,12 @@ int build_decoder(Model& m, const int* cfg, int n) {
     const int nk = last ? 1 : 2 * sf;
     if (ist) {
       add_wconv(m, m.nc_conv[s], gp + "noise_convs." + std::to_string(s), m.n_fft + 2, c, nk, false, true);
+    } else if (nk >= 16 && nk == 2 * sf && sf <= 32) {
+      // stride-S conv over the source = 2-tap conv over S-sample frames (k_har_frames)
+      add_wconv(m, m.nc_mm[s], gp + "noise_convs." + std::to_string(s), sf, c, 2, false, true);
+      m.nc_mm[s].reframe = sf;
+      m.nc_w.push_back(-1);
+      m.nc_b.push_back(-1);
     } else {
       m.nc_w.push_back(m.P.add(gp + "noise_convs." + std::to_string(s) + ".weight", (long long)c * nk));
       m.nc_b.push_back(m.P.add(gp + "noise_convs." + std::to_string(s) + ".bias", c));
@@ -356,7 +365,7 @@ void finalize_layout(Model& m) {
   m.aux_bytes = a;
   size_t sc = 0;
   for (auto* c : m.convs)
-    if (c->g >= 0) sc = std::max(sc, (size_t)c->Cin * c->Cout * c->K * 4);
+    if (c->g >= 0 || c->reframe) sc = std::max(sc, (size_t)c->Cin * c->Cout * c->K * 4);
   m.scratch_bytes = rup(sc, ALIGN);
   for (int dt = 0; dt < 2; ++dt) {
     m.aux_off[dt] = m.conv_bytes[dt];
@@ -671,6 +680,14 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     G[i].p = c.alloc((size_t)B * smax * esz);
     G[i].bs = smax;
   }
+  Buf HFR;  // S-sample frames of the source for the MFMA noise_convs (largest such stage)
+  {
+    int rows = 0;
+    for (int s = 0; s < nup; ++s)
+      if (!ist && m.nc_mm[s].reframe) rows = std::max(rows, Ls[s] + 1);
+    if (rows) HFR = c.frames(rows, 32);
+    HFR.ld = 32;
+  }
   const int F = ist ? L / m.hop + 1 : 0;
   const int ld_h = ist ? rup8(m.n_fft + 2) : 0;
   Buf HARF, POST;
@@ -739,10 +756,26 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     double* S_ns = c.stat(C);
     int sf = 1;
     for (int j = s + 1; j < nup; ++j) sf *= m.rates[j];
-    if (!ist) {
-      SmallConvDst d = {NS.p, NS.bs, C, 0, S_ns, C};
+    if (!ist && m.nc_mm[s].reframe) {  // noise_convs[s] on the MFMA engine over S-sample frames
+      const int S = m.nc_mm[s].reframe;
+      Buf hf = HFR;
+      hf.L = Ls_ + 1;
+      hf.bs = (long long)hf.L * 32;
+      RUN(st_har_frames(HAR, B, L, S, (S + 1) / 2, Ls_ + 1, 32, hf.p, c.dtype, c.s));
+      ConvParams p = conv_base(c, m.nc_mm[s], hf, 0);
+      p.Lq = Ls_;
+      conv_out(p, c, NS, 0, Ls_);
+      p.stats = S_ns;
+      p.stats_ld = C;
+      RUN(conv_run(c, p));
+    } else if (!ist) {
       const int K = last ? 1 : 2 * sf, st = last ? 1 : sf, pd = last ? 0 : (sf + 1) / 2;
-      RUN(st_conv_cin1(HAR, L, L, B, c.P(m.nc_w[s]), c.P(m.nc_b[s]), C, K, st, pd, Ls_, &d, 1, c.dtype, c.s));
+      if ((K == 1 || K == 4 || K == 12) && C % 8 == 0 && 256 % (C / 8) == 0) {
+        RUN(st_noise_conv(HAR, B, L, c.P(m.nc_w[s]), c.P(m.nc_b[s]), C, K, st, pd, Ls_, NS.p, S_ns, c.dtype, c.s));
+      } else {
+        SmallConvDst d = {NS.p, NS.bs, C, 0, S_ns, C};
+        RUN(st_conv_cin1(HAR, L, L, B, c.P(m.nc_w[s]), c.P(m.nc_b[s]), C, K, st, pd, Ls_, &d, 1, c.dtype, c.s));
+      }
     } else {
       Buf hf = HARF;
       ConvParams p = conv_base(c, m.nc_conv[s], hf, 0);
@@ -982,6 +1015,9 @@ int pack_model(Model& m, int dt, char* base, hipStream_t s) {
       const int rows = c->transposed ? c->Cin : c->Cout;
       const long long inner = (long long)c->Cin * c->Cout * c->K / rows;
       ST_CHECK(st_wn_fold(v, m.P[c->g], rows, (int)inner, scratch, s));
+      src = scratch;
+    } else if (c->reframe) {
+      ST_CHECK(st_reframe_w(v, c->Cout, c->reframe, scratch, s));
       src = scratch;
     }
     ST_CHECK(st_pack_conv(src, c->Cin, c->Cout, c->K, c->transposed, c->u, base + c->off[dt], dt, s));

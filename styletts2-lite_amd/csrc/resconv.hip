@@ -35,7 +35,7 @@ struct RC {
   static constexpr int G8 = C / 8;                   // 8-channel groups per window row
   static constexpr int UNITS = R * G8;               // 16-byte window units per tile
   static constexpr int MAXU = (UNITS + NT - 1) / NT;
-  static constexpr int OFF_BIAS = 4 * C * 4;         // after coef [4][C] f32
+  static constexpr int OFF_BIAS = 5 * C * 4;         // after coef [5][C] f32
   static constexpr int OFF_W = OFF_BIAS + C * 4;
   static constexpr int W_B = NCH * K * C * WP * 2;
   static constexpr int OFF_X = OFF_W + W_B;
@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, NTL = G::NTL, NCH = G::NCH, XP = G::XP, WP = G::WP;
   constexpr int G8 = G::G8, UNITS = G::UNITS, MAXU = G::MAXU, FW = G::FW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* coef = reinterpret_cast<float*>(smem);  // [4][C]: beta - mean*a, a, alpha/2pi, 1/alpha
+  float* coef = reinterpret_cast<float*>(smem);  // [5][C]: prologue coefficients (see step)
   float* bias_s = reinterpret_cast<float*>(smem + G::OFF_BIAS);
   bf16_t* Ws = reinterpret_cast<bf16_t*>(smem + G::OFF_W);  // [chunk][tap][n][WP], logical k order
   bf16_t* Xs = reinterpret_cast<bf16_t*>(smem + G::OFF_X);  // [R][XP], prologue applied
@@ -111,12 +111,14 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   };
 
   // epilogue prefetch: residual rows of the tile (16 channels of one frame per lane)
-  uint4 rres[MT][NTL][2];
+  uint4 rres[MT][NTL][2], racc[ACC ? MT : 1][ACC ? NTL : 1][2];
   auto issue_epi = [&](int t) __attribute__((always_inline)) {
     const int b = t / ntm, mt = t - b * ntm;
     const bool hr = p.res != nullptr;
     const Rsrc rr = make_rsrc(hr ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr,
                               hr ? (unsigned)((size_t)p.Lq * p.res_ld * 2) : 0u);
+    const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const bf16_t*>(p.accb) + (size_t)b * p.acc_bs : nullptr,
+                              ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * 2) : 0u);
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int q = mt * BM + wm * FW + mi * 32 + l32;
@@ -126,6 +128,11 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
         const unsigned er = (unsigned)(q * p.res_ld + co0) * 2u;
         rres[mi][ni][0] = bload16(rr, er);
         rres[mi][ni][1] = bload16(rr, er + 16u);
+        if constexpr (ACC) {
+          const unsigned ea = (unsigned)(q * p.acc_ld + co0) * 2u;
+          racc[mi][ni][0] = bload16(ra, ea);
+          racc[mi][ni][1] = bload16(ra, ea + 16u);
+        }
       }
     }
   };
@@ -161,29 +168,36 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     }
   };
 
+  // Prologue per element (AdaIN -> Snake), with sin^2(u) = (1 - cos 2u) / 2:
+  //   x = v*a + (beta - mean*a)            (hifigan.py:14-24)
+  //   y = x + sin^2(alpha x) / alpha        (hifigan.py:68)
+  //     = fma(v, a, m2) - ia2 * cos(2 alpha x),   m2 = beta - mean*a + ia2,  ia2 = 1 / (2 alpha)
+  // and the cosine argument (in revolutions, v_cos_f32) = fma(v, a*alpha/pi, (beta - mean*a)*alpha/pi).
   auto transform = [&](int t, const uint4 (&pre)[MAXU]) __attribute__((always_inline)) {
     const int mt = t % ntm;
     const int gr0 = mt * BM - G::PAD;
-    float a[8], m[8], al[8], ia[8];
-    ld8_lds(coef + 8 * g8, m);
+    float m2[8], a[8], ar[8], mr[8], nia[8];
+    ld8_lds(coef + 8 * g8, m2);
     ld8_lds(coef + C + 8 * g8, a);
-    ld8_lds(coef + 2 * C + 8 * g8, al);
-    ld8_lds(coef + 3 * C + 8 * g8, ia);
+    ld8_lds(coef + 2 * C + 8 * g8, ar);
+    ld8_lds(coef + 3 * C + 8 * g8, mr);
+    ld8_lds(coef + 4 * C + 8 * g8, nia);
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int u = tid + k * NT;
       if ((k + 1) * NT <= UNITS || u < UNITS) {
         const int r = u / G8;
-        const bool ok = (unsigned)(gr0 + r) < (unsigned)p.Lin;  // conv zero padding is post-prologue
         float v[8];
         bf8_to_f32(pre[k], v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float x = __builtin_fmaf(v[j], a[j], m[j]);  // (x - mean) * a + beta
-          const float s = __builtin_amdgcn_sinf(x * al[j]);  // v_sin_f32 takes revolutions
-          v[j] = ok ? __builtin_fmaf(s * s, ia[j], x) : 0.f;
+          const float x2 = __builtin_fmaf(v[j], a[j], m2[j]);
+          const float c = __builtin_amdgcn_cosf(__builtin_fmaf(v[j], ar[j], mr[j]));
+          v[j] = __builtin_fmaf(c, nia[j], x2);
         }
-        *reinterpret_cast<uint4*>(Xs + r * XP + 8 * g8) = f32_to_bf8(v);
+        uint4 o = f32_to_bf8(v);
+        if ((unsigned)(gr0 + r) >= (unsigned)p.Lin) o = make_uint4(0, 0, 0, 0);  // zero padding is post-prologue
+        *reinterpret_cast<uint4*>(Xs + r * XP + 8 * g8) = o;
       }
     }
   };
@@ -198,10 +212,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
         float mm, aa, be;
         adain_coeffs(p.pro, b, ci, mm, aa, be);
         const float al = p.pro.alpha[ci];
-        coef[ci] = be - mm * aa;
+        const float m1 = be - mm * aa, ia2 = 0.5f / al, alr = al * 0.31830988618379067f;  // alpha / pi
+        coef[ci] = m1 + ia2;
         coef[C + ci] = aa;
-        coef[2 * C + ci] = al * 0.15915494309189535f;
-        coef[3 * C + ci] = 1.0f / al;
+        coef[2 * C + ci] = aa * alr;
+        coef[3 * C + ci] = m1 * alr;
+        coef[4 * C + ci] = -ia2;
       }
       cur_b = b;
     }
@@ -245,7 +261,6 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
 
     // ---- epilogue: lane = frame l32 of block mi, channels (wn*NTL + ni)*32 + 16*hi + r
     bf16_t* yb = reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs;
-    const bf16_t* ab = ACC ? reinterpret_cast<const bf16_t*>(p.accb) + (size_t)b * p.acc_bs : nullptr;
     const bool hr = p.res != nullptr;
     const float osc = p.out_scale;
     const float adiv = (ACC && p.acc_div != 0.f) ? 1.0f / p.acc_div : 1.0f;
@@ -267,16 +282,19 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
           bf8_to_f32(rres[mi][ni][1], r1);
 #pragma unroll
           for (int r = 0; r < 8; ++r) {
-            v[r] = (v[r] + r0[r]) * osc;
-            v[8 + r] = (v[8 + r] + r1[r]) * osc;
+            v[r] += r0[r];
+            v[8 + r] += r1[r];
+          }
+          if (osc != 1.0f) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] *= osc;
           }
         }
         if (valid) {
           if constexpr (ACC) {
-            const uint4* ap = reinterpret_cast<const uint4*>(ab + (size_t)q * p.acc_ld + co0);
             float r0[8], r1[8];
-            bf8_to_f32(ap[0], r0);
-            bf8_to_f32(ap[1], r1);
+            bf8_to_f32(racc[mi][ni][0], r0);
+            bf8_to_f32(racc[mi][ni][1], r1);
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
               v[r] = (r0[r] + v[r]) * adiv;

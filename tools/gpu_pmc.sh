@@ -5,7 +5,7 @@ mkdir -p gpurun_out/pmc
 ARGS="--steps 1 --warmup 1 --no-cpu-baseline --no-profile ${BENCH_ARGS}"
 run() {  # name counters...
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --kernel-include-regex "conv1d_igemm" --pmc "$@" -d gpurun_out/pmc/$name -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc/$name.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-include-regex "${KREGEX:-conv1d_igemm}" --pmc "$@" -d gpurun_out/pmc/$name -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc"
   [ $rc -le 1 ] || exit $rc
