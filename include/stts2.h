@@ -95,6 +95,9 @@ const char* stts_error_string(int code);
  *                     C = 32 / 64 dilated convs; 0 = the general implicit-GEMM engine serves them
  *                     (A/B measurement and cross-checking of the two engines). */
 #define STTS_OPT_RESCONV 1
+/*   STTS_OPT_GRID_CAP n > 0 caps the persistent conv grids at n workgroups (testing: forces many
+ *                     tiles and utterance changes per workgroup); 0 (default) = one per CU. */
+#define STTS_OPT_GRID_CAP 2
 int stts_set_option(int key, int value);
 
 /* Optional per-kernel timing of the dominant kernel class (conv1d_igemm) with hipEvents recorded

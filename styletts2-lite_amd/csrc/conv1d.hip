@@ -668,6 +668,7 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
   if (tiles > 0x7fffffffLL) return ST_EINVAL;
   long long grid = (long long)g_num_cu * per_cu;
   if (grid > tiles) grid = tiles;
+  if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C::NT), lds, stream, p);
   return (int)hipGetLastError();
 }
@@ -691,6 +692,7 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
 }  // namespace
 
 int g_opt_resconv = 1;
+int g_opt_grid_cap = 0;
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (p.B <= 0 || p.Lq <= 0 || p.N <= 0) return ST_OK;
@@ -699,6 +701,7 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   ConvParams q = p;
   if (q.kw <= 0) q.kw = q.KS;
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return st_resconv(q, stream);
+  if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return st_bigconv(q, stream);
   if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);
   if (dtype == ST_BF16) {
     return launch_typed<bf16_t, bf16_t>(q, stream);

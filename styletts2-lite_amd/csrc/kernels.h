@@ -53,6 +53,10 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);
 bool st_resconv_eligible(const ConvParams& p, int dtype);
 int st_resconv(const ConvParams& p, hipStream_t stream);
 extern int g_opt_resconv;
+extern int g_opt_grid_cap;  // > 0: cap persistent conv grids (tests: many tiles per block)
+// wide-stage resblock conv engine (bigconv.hip): bf16, C = 128 / 256, same contract
+bool st_bigconv_eligible(const ConvParams& p, int dtype);
+int st_bigconv(const ConvParams& p, hipStream_t stream);
 
 // ---------------------------------------------------------------- misc kernels
 // src [B][C][L] fp32 (torch NCL) -> dst frames [B][L][ld] at channel offset c0; optional stats.

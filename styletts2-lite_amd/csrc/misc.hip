@@ -292,42 +292,39 @@ __global__ void __launch_bounds__(256) k_pool_dw(const T* __restrict__ x, long l
 
 // ------------------------------------------------------------------ style projections
 // H[b][n] = bias[n] + sum_k s[b][k] * Wt[k][n]   (Wt packed [K][N] at load)
-// H[b][n] = bias[n] + sum_k s[b][k] * Wt[k][n] for up to 32 utterances per block: the style
-// rows sit in LDS, each thread owns one column n and streams Wt[:, n] (coalesced across the
-// block) with 8 loads in flight.
+// H[b][n] = bias[n] + sum_k s[b][k] * Wt[k][n] for up to 32 utterances per block: 64 columns
+// per block (one per lane), the 4 waves split K, the style rows sit in LDS, partial sums meet in LDS.
 __global__ void __launch_bounds__(256) k_linear(const float* __restrict__ s, int B, int K,
                                                 const float* __restrict__ Wt, const float* __restrict__ bias, int N,
                                                 float* __restrict__ H) {
-  extern __shared__ float ss[];  // [32][K]
+  extern __shared__ float ss[];  // [32][K] style rows, then [4][32][64] partial sums
+  float* part = ss + 32 * K;
   const int b0 = blockIdx.y * 32, nb = min(32, B - b0);
-  for (int i = threadIdx.x; i < nb * K; i += 256) ss[i] = s[(size_t)b0 * K + i];
+  for (int i = threadIdx.x; i < 32 * K; i += 256) ss[i] = i < nb * K ? s[(size_t)b0 * K + i] : 0.f;
   __syncthreads();
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
+  const int kq = (K + 3) / 4, k0 = wv * kq, k1 = min(K, k0 + kq);
   float acc[32];
 #pragma unroll
   for (int i = 0; i < 32; ++i) acc[i] = 0.f;
-  int k = 0;
-  for (; k + 8 <= K; k += 8) {
-    float wv[8];
+  if (n < N) {
+#pragma unroll 4
+    for (int k = k0; k < k1; ++k) {
+      const float wv_ = Wt[(size_t)k * N + n];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) wv[u] = Wt[(size_t)(k + u) * N + n];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int i = 0; i < 32; ++i)
-        if (i < nb) acc[i] = fmaf(ss[i * K + k + u], wv[u], acc[i]);
+      for (int i = 0; i < 32; ++i) acc[i] = fmaf(ss[i * K + k], wv_, acc[i]);
+    }
   }
-  for (; k < K; ++k) {
-    const float wv = Wt[(size_t)k * N + n];
 #pragma unroll
-    for (int i = 0; i < 32; ++i)
-      if (i < nb) acc[i] = fmaf(ss[i * K + k], wv, acc[i]);
+  for (int i = 0; i < 32; ++i) part[(wv * 32 + i) * 64 + lane] = acc[i];
+  __syncthreads();
+  const float bv = (n < N && bias) ? bias[n] : 0.f;
+  for (int i = wv; i < nb; i += 4) {
+    const float h = part[(0 * 32 + i) * 64 + lane] + part[(1 * 32 + i) * 64 + lane] +
+                    part[(2 * 32 + i) * 64 + lane] + part[(3 * 32 + i) * 64 + lane];
+    if (n < N) H[(size_t)(b0 + i) * N + n] = h + bv;
   }
-  const float bv = bias ? bias[n] : 0.f;
-#pragma unroll
-  for (int i = 0; i < 32; ++i)
-    if (i < nb) H[(size_t)(b0 + i) * N + n] = acc[i] + bv;
 }
 
 // ------------------------------------------------------------------ HiFi-GAN noise_convs
@@ -386,16 +383,29 @@ __global__ void __launch_bounds__(256) k_noise_conv(const float* __restrict__ ha
     }
   }
   if (!stats) return;
-  // lanes l, l+G, l+2G, ... of a wave share g
+  // lanes l, l+G, l+2G, ... of a wave share g; then the 4 waves combine in LDS and ONE atomic
+  // pair per (block, channel) goes out (same-line atomics from many blocks serialise in L2)
+  __shared__ float red[4][2][256];
 #pragma unroll
   for (int c = 0; c < 8; ++c)
     for (int o = G; o < 64; o <<= 1) {
       sa[c] += __shfl_xor(sa[c], o);
       sq[c] += __shfl_xor(sq[c], o);
     }
+  const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) < G) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) atomic_stats(stats + ((size_t)b * C + 8 * g + c) * 2, sa[c], sq[c]);
+    for (int c = 0; c < 8; ++c) {
+      red[wv][0][8 * g + c] = sa[c];
+      red[wv][1][8 * g + c] = sq[c];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    const double a = (double)red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    const double q = (double)red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    atomic_stats(stats + ((size_t)b * C + c) * 2, a, q);
   }
 }
 
@@ -728,9 +738,9 @@ int st_pool_dw(const void* x, long long x_bs, int x_ld, int B, int Lin, int C, c
 }
 
 int st_linear(const float* s, int B, int K, const float* Wt, const float* bias, int N, float* H, hipStream_t st) {
-  const size_t lds = (size_t)32 * K * 4;
+  const size_t lds = ((size_t)32 * K + 4 * 32 * 64) * 4;
   if (lds > 64 * 1024) return ST_EINVAL;
-  hipLaunchKernelGGL(k_linear, dim3((N + 255) / 256, (B + 31) / 32), dim3(256), lds, st, s, B, K, Wt, bias, N, H);
+  hipLaunchKernelGGL(k_linear, dim3((N + 63) / 64, (B + 31) / 32), dim3(256), lds, st, s, B, K, Wt, bias, N, H);
   return (int)hipGetLastError();
 }
 
@@ -825,8 +835,8 @@ int st_gap_linear(const void* z, int B, int rows, int Wv, int C, const float* w,
 
 int st_noise_conv(const float* har, int B, int L, const float* w, const float* bias, int C, int K, int S, int P,
                   int Lout, void* y, double* stats, int dtype, hipStream_t s) {
-  if (C % 8 || 256 % (C / 8)) return ST_EINVAL;
-  const int fpb = 1024;
+  if (C % 8 || 256 % (C / 8) || C > 256) return ST_EINVAL;
+  const int fpb = 8192;
   dim3 grid((Lout + fpb - 1) / fpb, B);
 #define NCONV(KC)                                                                                              \
   DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_noise_conv<T, KC>), grid, dim3(256), 0, s, har, L, w, bias, C, S, \

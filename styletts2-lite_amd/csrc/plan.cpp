@@ -1189,6 +1189,7 @@ const char* stts_error_string(int code) {
 int stts_set_option(int key, int value) {
   switch (key) {
     case STTS_OPT_RESCONV: g_opt_resconv = value != 0; return 0;
+    case STTS_OPT_GRID_CAP: g_opt_grid_cap = value > 0 ? value : 0; return 0;
     default: return ST_EINVAL;
   }
 }

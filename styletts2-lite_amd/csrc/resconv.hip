@@ -350,6 +350,7 @@ int launch_rc(const ConvParams& p, hipStream_t stream) {
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   long long grid = (long long)g_num_cu_rc * per_cu;
   if (grid > tiles) grid = tiles;
+  if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, p);
   return (int)hipGetLastError();
 }

@@ -74,6 +74,7 @@ def lib():
 
 
 OPT_RESCONV = 1
+OPT_GRID_CAP = 2
 
 
 def set_option(key: int, value: int) -> None:

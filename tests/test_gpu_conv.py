@@ -22,6 +22,10 @@ CASES = [
     ("rb32_k7_d3", 32, 32, 7, 0, 1, 3, 9, 0, 517, 3),
     ("rb64_k11_d5", 64, 64, 11, 0, 1, 5, 25, 0, 600, 3),
     ("rb64_k3_d1", 64, 64, 3, 0, 1, 1, 1, 0, 2049, 3),
+    ("rb128_k7_d3", 128, 128, 7, 0, 1, 3, 9, 0, 1000, 3),
+    ("rb128_k11_d5", 128, 128, 11, 0, 1, 5, 25, 0, 777, 3),
+    ("rb256_k3_d5", 256, 256, 3, 0, 1, 5, 5, 0, 600, 3),
+    ("rb256_k7_d1", 256, 256, 7, 0, 1, 1, 3, 0, 513, 3),
     ("front_1090_1024", 1090, 1024, 3, 0, 1, 1, 1, 0, 40, 5),
     ("sc_1x1", 514, 1024, 1, 0, 1, 1, 0, 0, 37, 0),
     ("istft_noise_s6", 22, 256, 12, 0, 6, 1, 3, 0, 481, 0),
@@ -104,7 +108,7 @@ def test_conv_engine(case, dtype):
         assert ((s[..., 1] - (yd ** 2).sum(1)).abs() <= bound_q).all(), f"{name}: square statistics"
 
 
-RB_CASES = [c for c in CASES if c[0].startswith("rb32") or c[0].startswith("rb64")]
+RB_CASES = [c for c in CASES if c[0].startswith("rb")]
 
 
 @pytest.mark.parametrize("case", RB_CASES, ids=[c[0] for c in RB_CASES])
@@ -122,3 +126,19 @@ def test_resconv_engine_matches_general_engine(case):
     err = (y1 - y0).abs().max().item()
     assert err <= 2 ** -7 * scale, f"{case[0]}: engines differ by {err}"
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("case", RB_CASES, ids=[c[0] for c in RB_CASES])
+def test_resblock_engines_many_tiles_per_workgroup(case):
+    """Persistent grids capped at 3 workgroups: every workgroup walks many tiles and crosses
+    utterance boundaries (coefficient switch, statistics flush, cross-tile prefetch)."""
+    ref, _, _ = run_case(case, "bf16")
+    try:
+        E.set_option(E.OPT_GRID_CAP, 3)
+        _, y, s = run_case(case, "bf16")
+    finally:
+        E.set_option(E.OPT_GRID_CAP, 0)
+    _, y0, s0 = run_case(case, "bf16")
+    scale = max(1.0, y0.abs().max().item())
+    assert (y - y0).abs().max().item() <= 2 ** -7 * scale, case[0]
+    np.testing.assert_allclose(s.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
