@@ -78,6 +78,60 @@ def cpu_baseline(kind, dec, cfg, T, budget_s=12.0):
                       f"{'decoder_hifigan' if kind == 'hifigan' else 'decoder_istft'} fp32 on torch-CPU"}
 
 
+def roofline(recs, args, el, B, T):
+    """Roofline of the dominant kernel (the conv engine with the most hipEvent-timed time in the
+    timed region).  achieved = its algorithmic work (SURVEY.md §8(d) byte / flop model, summed over
+    its launches) / its measured time; bound = whichever of MFMA / HBM floors is larger for that
+    work.  traffic = HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes (tools/pmc_traffic.py -> profiles/*_traffic.json) when they were taken on this exact
+    workload and kernel, else null."""
+    fam = {}
+    for r in recs:
+        f = fam.setdefault(r["kernel"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "launches": 0})
+        f["ms"] += r["ms"]
+        f["flops"] += r["flops"]
+        f["bytes"] += r["bytes"]
+        f["launches"] += 1
+    name, f = max(fam.items(), key=lambda kv: kv[1]["ms"])
+    t_k = f["ms"] / 1e3
+    t_mfma, t_hbm = f["flops"] / PEAK_MFMA[args.dtype], f["bytes"] / PEAK_HBM
+    if t_mfma >= t_hbm:
+        roof = {"bound": "mfma", "achieved": f["flops"] / t_k / 1e12, "peak": PEAK_MFMA[args.dtype] / 1e12,
+                "unit": "TFLOP/s"}
+    else:
+        roof = {"bound": "hbm", "achieved": f["bytes"] / t_k / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s"}
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    roof["traffic"] = None
+    roof["kernel"] = name
+    roof["launches"] = f["launches"]
+    roof["avg_launch_us"] = f["ms"] * 1e3 / f["launches"]
+    roof["alg_flops_per_launch"] = f["flops"] / f["launches"]
+    roof["alg_bytes_per_launch"] = f["bytes"] / f["launches"]
+    roof["kernel_share_of_step"] = f["ms"] / (el * 1e3)
+    roof["conv_engines"] = {k: {"ms_per_step": v["ms"] / args.steps, "launches_per_step": v["launches"] // args.steps,
+                                "tflops": v["flops"] / (v["ms"] / 1e3) / 1e12,
+                                "alg_GBps": v["bytes"] / (v["ms"] / 1e3) / 1e9} for k, v in sorted(fam.items())}
+    tr = _pmc_traffic(name, args, B, T)
+    if tr is not None:
+        roof["traffic"] = tr["hbm_bytes_per_launch"]
+        roof["traffic_source"] = tr["source"]
+    return roof
+
+
+def _pmc_traffic(kernel, args, B, T):
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            with open(path) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if (d.get("kernel") == kernel and d.get("decoder") == args.decoder and d.get("dtype") == args.dtype
+                and d.get("batch") == B and d.get("frames") == T):
+            return {"hbm_bytes_per_launch": d["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,7 +184,7 @@ def main():
         step(args.warmup + i)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    prof = E.profile_read() if not args.no_profile else None
+    prof_recs = E.profile_launches() if not args.no_profile else None
     E.profile_enable(False)
     if dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
@@ -144,22 +198,7 @@ def main():
     samples = world * B * 600 * T * args.steps
     value = samples / el
     ms = el / args.steps * 1e3
-    roof = None
-    if prof and prof["launches"]:
-        t_k = prof["ms"] / 1e3
-        fl, by = prof["flops"], prof["bytes"]
-        t_mfma, t_hbm = fl / PEAK_MFMA[args.dtype], by / PEAK_HBM
-        if t_mfma >= t_hbm:
-            roof = {"bound": "mfma", "achieved": fl / t_k / 1e12, "peak": PEAK_MFMA[args.dtype] / 1e12,
-                    "unit": "TFLOP/s"}
-        else:
-            roof = {"bound": "hbm", "achieved": by / t_k / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s"}
-        roof["frac"] = roof["achieved"] / roof["peak"]
-        roof["traffic"] = None
-        roof["kernel"] = "conv1d_igemm_kernel (all launches in the timed region)"
-        roof["launches"] = prof["launches"]
-        roof["avg_launch_us"] = prof["ms"] * 1e3 / prof["launches"]
-        roof["kernel_share_of_step"] = prof["ms"] / (el * 1e3)
+    roof = roofline(prof_recs, args, el, B, T) if prof_recs else None
     line = {
         "metric": "24 kHz audio samples/sec/GPU + real-time factor, 10-s utterance batch",
         "value": value,

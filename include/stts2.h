@@ -100,11 +100,12 @@ const char* stts_error_string(int code);
 #define STTS_OPT_GRID_CAP 2
 int stts_set_option(int key, int value);
 
-/* Optional per-kernel timing of the dominant kernel class (conv1d_igemm) with hipEvents recorded
- * on `stream` around each launch: enable, run, then read totals (ms, launches). */
+/* Optional per-launch timing of the conv engines (conv1d_igemm, resconv, bigconv) with hipEvents
+ * recorded on `stream` around each launch: enable, run, then read totals (ms, launches). */
 int stts_profile_enable(int on);
 int stts_profile_read(double* total_ms, long long* launches, double* alg_flops, double* alg_bytes);
-/* Launch i of the timed region: shape = {B, rows, N, Cin, taps, dilation, Lout, res|acc<<1},
+/* Launch i of the timed region: shape = {B, rows, N, Cin, taps, dilation, Lout,
+ * res | acc<<1 | engine<<4} with engine 0 = conv1d_igemm, 1 = resconv, 2 = bigconv,
  * ms_flops_bytes = {hipEvent ms, algorithmic flops, algorithmic bytes}. */
 int stts_profile_launch(long long i, int* shape, double* ms_flops_bytes);
 

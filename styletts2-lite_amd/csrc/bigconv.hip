@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
       }
   };
 
-  uint4 wA[WPT];
+  uint4 wA[WPT], wB[WPT];
   int cur_b = tbeg / ntm;
   auto step = [&](int g, uint4 (&wnext)[WPT]) __attribute__((always_inline)) {
     const int tl = g / NS, s = g - tl * NS, t = tbeg + tl;
@@ -416,8 +416,8 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
           for (int r = 0; r < 16; ++r) acc[mi][ni][r] = bb[r];
       }
     }
-    if (g + 1 < nsteps) store_w((g + 1) & 1, wnext);  // slice g+1 (loaded during step g-1)
-    issue_w(g + 2, wnext);                          // slice g+2: one step of cover
+    if (g + 1 < nsteps) store_w((g + 1) & 1, wnext);  // slice g+1 (loaded two steps ago)
+    issue_w(g + 3, wnext);                          // same register set: slice g+3
     if (tap == 0) {
       issue_x(gg + 1);  // window of the next group (K steps of cover)
       // the next group opens a new tile of another utterance: its coefficients, visible after
@@ -435,11 +435,15 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   issue_x(0);
   issue_w(0, wA);
   store_w(0, wA);
-  issue_w(1, wA);
+  issue_w(1, wB);
+  issue_w(2, wA);
   __syncthreads();  // coef visible
   transform_x(0);
 
-  for (int g = 0; g < nsteps; ++g) step(g, wA);  // stores slice g+1, loads g+2
+  for (int g = 0; g < nsteps; g += 2) {  // two named register sets: slices of odd / even steps
+    step(g, wB);                         // stores slice g+1, loads g+3
+    if (g + 1 < nsteps) step(g + 1, wA);  // stores slice g+2, loads g+4
+  }
   __syncthreads();
   if constexpr (SREG) {
     if (p.stats) flush_reg(cur_b);

@@ -694,6 +694,14 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
 int g_opt_resconv = 1;
 int g_opt_grid_cap = 0;
 
+int st_conv1d_engine(const ConvParams& p, int dtype) {
+  ConvParams q = p;
+  if (q.kw <= 0) q.kw = q.KS;
+  if (g_opt_resconv && st_resconv_eligible(q, dtype)) return ST_ENGINE_RESCONV;
+  if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
+  return ST_ENGINE_IGEMM;
+}
+
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (p.B <= 0 || p.Lq <= 0 || p.N <= 0) return ST_OK;
   if (p.KS <= 0 || p.stride <= 0 || p.dil <= 0 || p.Cout <= 0 || p.up <= 0) return ST_EINVAL;

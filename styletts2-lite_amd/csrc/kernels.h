@@ -48,6 +48,9 @@ struct ConvParams {
 };
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);
+// which engine st_conv1d routes p to (profiling records; bench.py names the dominant kernel)
+enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2 };
+int st_conv1d_engine(const ConvParams& p, int dtype);
 // resblock conv engine (resconv.hip): bf16, C = 32 / 64, 1-D 'same' dilated conv with the
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.
 bool st_resconv_eligible(const ConvParams& p, int dtype);

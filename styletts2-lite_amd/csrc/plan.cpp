@@ -503,7 +503,8 @@ int conv_run(Ctx& c, ConvParams& p) {
     const double by = elems * c.esz + (p.y_f32 ? (double)p.B * p.Lout * p.Cout * (4.0 - c.esz) : 0.0);
     g_prof.flops += fl;
     g_prof.bytes += by;
-    g_prof.rec.push_back({{p.B, p.Lq, p.N, p.Cin, p.KS, p.dil, p.Lout, (p.res ? 1 : 0) | (p.accb ? 2 : 0)}, fl, by});
+    const int flags = (p.res ? 1 : 0) | (p.accb ? 2 : 0) | (st_conv1d_engine(p, c.dtype) << 4);
+    g_prof.rec.push_back({{p.B, p.Lq, p.N, p.Cin, p.KS, p.dil, p.Lout, flags}, fl, by});
   }
   return 0;
 }

@@ -291,14 +291,18 @@ def profile_read():
     return {"ms": t.value, "launches": n.value, "flops": f.value, "bytes": b.value}
 
 
+ENGINE_KERNELS = ("conv1d_igemm_kernel", "k_resconv", "k_bigconv")  # st_conv1d_engine ids 0, 1, 2
+
+
 def profile_launches():
-    """Per-launch records of the timed region: dicts with the GEMM shape, ms, flops, bytes."""
+    """Per-launch records of the timed region: dicts with the GEMM shape, the kernel the launch
+    was routed to, ms, flops, bytes."""
     out = []
     n = profile_read()["launches"]
     shape, v = (ctypes.c_int * 8)(), (ctypes.c_double * 3)()
     for i in range(n):
         check(lib().stts_profile_launch(i, shape, v))
         out.append({"B": shape[0], "rows": shape[1], "N": shape[2], "Cin": shape[3], "taps": shape[4],
-                    "dil": shape[5], "Lout": shape[6], "res_acc": shape[7], "ms": v[0], "flops": v[1],
-                    "bytes": v[2]})
+                    "dil": shape[5], "Lout": shape[6], "res_acc": shape[7] & 3,
+                    "kernel": ENGINE_KERNELS[(shape[7] >> 4) & 3], "ms": v[0], "flops": v[1], "bytes": v[2]})
     return out

@@ -40,7 +40,7 @@ def main():
     E.profile_enable(False)
     pf, pb = bench.PEAK_MFMA[a.dtype], bench.PEAK_HBM
     print(f"{'i':>3} {'rows':>8} {'N':>5} {'Cin':>5} {'k':>3} {'d':>2} {'ra':>2} {'us':>8} {'TF/s':>7} {'GB/s':>7} "
-          f"{'bound':>5} {'frac':>5} {'floor_us':>8}")
+          f"{'bound':>5} {'frac':>5} {'floor_us':>8} kernel")
     tot, tot_floor = 0.0, 0.0
     for i, r in enumerate(recs):
         t = r["ms"] / 1e3
@@ -51,7 +51,7 @@ def main():
         tot += t
         tot_floor += floor
         print(f"{i:3d} {r['B'] * r['rows']:8d} {r['N']:5d} {r['Cin']:5d} {r['taps']:3d} {r['dil']:2d} {r['res_acc']:2d} "
-              f"{t * 1e6:8.1f} {tf:7.1f} {gb:7.0f} {bound:>5} {floor / t:5.2f} {floor * 1e6:8.1f}")
+              f"{t * 1e6:8.1f} {tf:7.1f} {gb:7.0f} {bound:>5} {floor / t:5.2f} {floor * 1e6:8.1f} {r['kernel']}")
     print(f"total {tot * 1e3:.3f} ms over {len(recs)} launches; roofline floor {tot_floor * 1e3:.3f} ms "
           f"({tot_floor / tot:.3f})")
 
