@@ -98,6 +98,10 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_GRID_CAP n > 0 caps the persistent conv grids at n workgroups (testing: forces many
  *                     tiles and utterance changes per workgroup); 0 (default) = one per CU. */
 #define STTS_OPT_GRID_CAP 2
+/*   STTS_OPT_RESFUSED 1 (default) = bf16 AdaINResBlock1 iterations at C = 32 (and C = 64, K = 3) run
+ *                     as a statistics-only conv1 launch + one fused conv1 -> conv2 launch
+ *                     (resfused.hip); 0 = two conv launches per iteration (A/B, cross-checking). */
+#define STTS_OPT_RESFUSED 3
 int stts_set_option(int key, int value);
 
 /* Optional per-launch timing of the conv engines (conv1d_igemm, resconv, bigconv) with hipEvents
@@ -105,7 +109,7 @@ int stts_set_option(int key, int value);
 int stts_profile_enable(int on);
 int stts_profile_read(double* total_ms, long long* launches, double* alg_flops, double* alg_bytes);
 /* Launch i of the timed region: shape = {B, rows, N, Cin, taps, dilation, Lout,
- * res | acc<<1 | engine<<4} with engine 0 = conv1d_igemm, 1 = resconv, 2 = bigconv,
+ * res | acc<<1 | engine<<4} with engine 0 = conv1d_igemm, 1 = resconv, 2 = bigconv, 3 = resfused,
  * ms_flops_bytes = {hipEvent ms, algorithmic flops, algorithmic bytes}. */
 int stts_profile_launch(long long i, int* shape, double* ms_flops_bytes);
 

@@ -47,11 +47,12 @@ struct BG {
   static constexpr int OFF_BIAS = 2 * 5 * C * 4;    // coef [2][5][C] f32 (utterance parity)
   static constexpr int OFF_ST = OFF_BIAS + C * 4;   // stats [C][2] f32 (per-tile reduction path)
   static constexpr int OFF_W = OFF_ST + 2 * C * 4;
-  static constexpr int OFF_X = OFF_W + 2 * WSLICE * 2;
+  static constexpr int OFF_X = OFF_W + 4 * WSLICE * 2;  // 4-slot weight ring
   static constexpr int LDS = OFF_X + 2 * R * XP * 2;
   static_assert(F::WAVES_M * MT * 32 == BM && F::WAVES_N * NTL * 32 == C, "wave grid");
   static_assert(WPT * 16 * NT == WSLICE * 2, "weight slice split");
   static_assert(NT % G8 == 0 && K >= 3, "pipeline shape");
+  static_assert(NS % 2 == 0, "super-steps of two sub-steps must not straddle tiles");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
@@ -365,7 +366,7 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   auto mfma_step = [&](int g) __attribute__((always_inline)) {
     const int s = g % NS, tap = s % K;
     const int gg = g / K;  // global group index
-    const bf16_t* wt = wbase + (size_t)(g & 1) * G::WSLICE;
+    const bf16_t* wt = wbase + (size_t)(g & 3) * G::WSLICE;
     const bf16_t* xt = xbase + (size_t)(gg & 1) * G::R * XP + tap * DIL * XP;
 #pragma unroll
     for (int cg = 0; cg < CG; ++cg)
@@ -387,13 +388,13 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
       }
   };
 
-  uint4 wA[WPT], wB[WPT];
+  // ---------------- sub-step g (one (group, tap) slice): MFMAs plus the staging it owns
+  uint4 wr[2][WPT];  // weight slices of the next super-step (registers, one super-step of cover)
   int cur_b = tbeg / ntm;
-  auto step = [&](int g, uint4 (&wnext)[WPT]) __attribute__((always_inline)) {
+  auto sub = [&](int g, bool first) __attribute__((always_inline)) {
     const int tl = g / NS, s = g - tl * NS, t = tbeg + tl;
     const int gi = s / K, tap = s - gi * K;
     const int gg = tl * NG + gi;
-    __syncthreads();  // slot (g+1)&1 and window slot (gg+1)&1 are free; slot g&1 / window gg&1 visible
     if (s == 0) {
       const int b = t / ntm;
       if (b != cur_b) {  // statistics of the utterance the block just left
@@ -404,6 +405,9 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
         }
         cur_b = b;
       }
+      // the next tile opens another utterance: its coefficients (other parity slot), first read
+      // by the transform at sub-step NS-2 of this tile, >= 1 barrier later
+      if (t + 1 < tend && (t + 1) / ntm != b) set_coef((t + 1) / ntm);
 #pragma unroll
       for (int ni = 0; ni < NTL; ++ni) {  // the accumulators start at the bias
         float bb[16];
@@ -416,33 +420,44 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
           for (int r = 0; r < 16; ++r) acc[mi][ni][r] = bb[r];
       }
     }
-    if (g + 1 < nsteps) store_w((g + 1) & 1, wnext);  // slice g+1 (loaded two steps ago)
-    issue_w(g + 3, wnext);                          // same register set: slice g+3
-    if (tap == 0) {
-      issue_x(gg + 1);  // window of the next group (K steps of cover)
-      // the next group opens a new tile of another utterance: its coefficients, visible after
-      // the next barrier (K >= 3 steps before the transform that uses them)
-      if (gi == NG - 1 && t + 1 < tend && (t + 1) / ntm != t / ntm) set_coef((t + 1) / ntm);
+    if (first) {  // slices g+2, g+3 -> their ring slots (last read one super-step ago); load g+4, g+5
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (g + 2 + j < nsteps) store_w((g + 2 + j) & 3, wr[j]);
+        issue_w(g + 4 + j, wr[j]);
+      }
     }
-    if (tap == K - 1) transform_x(gg + 1);
-    if (s == NS - 1) issue_epi(t);  // residual rows (C = 128 path): the last step's MFMAs cover them
+    if (tap == K - 2) {
+      // window of group gg+1 into the other window slot: its last reader (group gg-1) finished
+      // >= 1 barrier ago, its first reader (group gg+1, sub-step s+2) runs >= 1 barrier later
+      transform_x(gg + 1);
+      issue_x(gg + 2);  // the next window's raw loads: one full group (K sub-steps) of cover
+    }
+    if (s == NS - 1) issue_epi(t);  // residual rows (C = 128 path): this sub-step's MFMAs cover them
     mfma_step(g);
     if (s == NS - 1) epilogue(t);
   };
 
-  // ---------------- prologue
+  // ---------------- prologue: slices 0, 1 in LDS, 2, 3 in registers; window 0 transformed,
+  // window 1's raw loads in flight
   set_coef(cur_b);
   issue_x(0);
-  issue_w(0, wA);
-  store_w(0, wA);
-  issue_w(1, wB);
-  issue_w(2, wA);
+  issue_w(0, wr[0]);
+  issue_w(1, wr[1]);
+  store_w(0, wr[0]);
+  store_w(1, wr[1]);
+  issue_w(2, wr[0]);
+  issue_w(3, wr[1]);
   __syncthreads();  // coef visible
   transform_x(0);
+  issue_x(1);
 
-  for (int g = 0; g < nsteps; g += 2) {  // two named register sets: slices of odd / even steps
-    step(g, wB);                         // stores slice g+1, loads g+3
-    if (g + 1 < nsteps) step(g + 1, wA);  // stores slice g+2, loads g+4
+  // super-steps of two sub-steps per barrier (NS is even: a tile never splits a super-step); the
+  // weight ring has 4 slots, the window ring 2 (transform at tap K-2, see sub)
+  for (int g = 0; g < nsteps; g += 2) {
+    __syncthreads();  // slices g, g+1 and their windows visible; slots of g-2, g-1 free
+    sub(g, true);
+    sub(g + 1, false);
   }
   __syncthreads();
   if constexpr (SREG) {

@@ -115,6 +115,13 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   const int Np = (p.N + 31) & ~31;
   const int mode = p.pro.mode;
   const bool resident = p.w_resident != 0;
+  // tile t -> (row tile mt, utterance b, column tile nt), time fastest: a block's contiguous tile
+  // range stays in one column tile.  (Column-tile-fastest orders, tried for the streamed-weight
+  // upsamplers to re-read each input window from L2, measured 10-30 % slower: every tile then
+  // re-stages its window's prologue and flushes statistics.)
+  auto t_mt = [&](int t) { return t % ntm; };
+  auto t_b = [&](int t) { return (t / ntm) % p.B; };
+  auto t_nt = [&](int t) { return t / (ntm * p.B); };
   constexpr bool FAST_SIN = C::BF;
 
   // statistics partials: lane = column l32 of tile ni, summed over the frames of its half (hi)
@@ -169,7 +176,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   constexpr int MAXW = 4;  // 16-byte W units per thread per group (launch_cfg sizes tg to fit)
   uint4 wpre[MAXW];
   auto issue_w = [&](int t, int c, int tap0) {
-    const int n0 = (t / (ntm * p.B)) * BN;
+    const int n0 = t_nt(t) * BN;
     const int ntap = min(p.tg, p.KS - tap0);
 #pragma unroll
     for (int k = 0; k < MAXW; ++k) {
@@ -213,7 +220,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   const int g8 = tid & 3;
 
   auto issue = [&](int t, int c) {
-    const int mt = t % ntm, b = (t / ntm) % p.B;
+    const int mt = t_mt(t), b = t_b(t);
     const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * p.x_bs;
     const Rsrc rx = make_rsrc(xb, (unsigned)((size_t)p.Lin * p.x_ld * sizeof(T)));
     const int gr0 = mt * BM * p.stride - p.pad, ci0 = c * BK;
@@ -307,7 +314,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
 
   auto write_x = [&](int t, int c) {
     const int ci0 = c * BK;
-    const int gr0 = (t % ntm) * BM * p.stride - p.pad;
+    const int gr0 = t_mt(t) * BM * p.stride - p.pad;
     Coef8 k;
     load_coef(ci0, k);
 #pragma unroll
@@ -320,7 +327,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       if (u < units) put(u, v, gr >= 0 && gr < p.Lin, ci0, k);
     }
     if (units > MAXU * NT) {  // large windows (2-D style convs): synchronous remainder
-      const int b = (t / ntm) % p.B;
+      const int b = t_b(t);
       const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * p.x_bs;
       const Rsrc rx = make_rsrc(xb, (unsigned)((size_t)p.Lin * p.x_ld * sizeof(T)));
       for (int u = tid + MAXU * NT; u < units; u += NT) {
@@ -348,9 +355,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   }
   for (int st = 0; st < nsteps; ++st) {
     const int t = tbeg + st / p.nchunks, c = st % p.nchunks;
-    const int mt = t % ntm;
-    const int b = (t / ntm) % p.B;
-    const int nt = t / (ntm * p.B);
+    const int mt = t_mt(t);
+    const int b = t_b(t);
+    const int nt = t_nt(t);
     const int q0 = mt * BM, n0 = nt * BN;
 
     if (c == 0) {
@@ -685,13 +692,16 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
   if (p.epi_tanh) return ST_EINVAL;  // tanh only on narrow heads
   if (p.stride > 1) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);  // BM 64 x BN 128 (short window)
   if (p.N <= 32) return launch_cfg<T, MT, 4, 1, 2, 1>(p, stream);     // BM 256 x BN 32, 4 waves
-  if (p.N <= 64) return launch_cfg<T, MT, 8, 1, 1, 2>(p, stream);     // BM 256 x BN 64, 8 waves
+  // BM 256 x BN 64, 8 waves.  (N = 192 keeps BN 128: the window prologue is paid per tile, so
+  // three 64-column tiles measured slower than a half-empty 128-column one.)
+  if (p.N <= 64) return launch_cfg<T, MT, 8, 1, 1, 2>(p, stream);
   return launch_cfg<T, MT, 4, 2, 2, 2>(p, stream);                    // BM 256 x BN 128, 8 waves
 }
 
 }  // namespace
 
 int g_opt_resconv = 1;
+int g_opt_resfused = 0;
 int g_opt_grid_cap = 0;
 
 int st_conv1d_engine(const ConvParams& p, int dtype) {

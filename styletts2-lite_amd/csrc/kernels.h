@@ -49,7 +49,7 @@ struct ConvParams {
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);
 // which engine st_conv1d routes p to (profiling records; bench.py names the dominant kernel)
-enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2 };
+enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2, ST_ENGINE_RESFUSED = 3 };
 int st_conv1d_engine(const ConvParams& p, int dtype);
 // resblock conv engine (resconv.hip): bf16, C = 32 / 64, 1-D 'same' dilated conv with the
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.
@@ -60,6 +60,35 @@ extern int g_opt_grid_cap;  // > 0: cap persistent conv grids (tests: many tiles
 // wide-stage resblock conv engine (bigconv.hip): bf16, C = 128 / 256, same contract
 bool st_bigconv_eligible(const ConvParams& p, int dtype);
 int st_bigconv(const ConvParams& p, hipStream_t stream);
+
+// fused AdaINResBlock1 iteration (resfused.hip): bf16, C = 32 (K = 3/7/11) or 64 (K = 3).
+//   y = conv2(Snake2(AdaIN2(conv1(Snake1(AdaIN1(x)))))) + x     (hifigan.py:65-74)
+// pro2.stats must already hold the statistics of conv1's output (a statistics-only conv1 launch).
+// y must not alias x (neighbouring tiles read x halos).  accb != null: y = (accb + .) / acc_div
+// (acc_div 0 = no division) and no statistics; otherwise statistics of y when stats != null.
+struct ResFusedParams {
+  const void* x;
+  long long x_bs;
+  int x_ld, B, L, C, K, dil;
+  const void* w1;
+  const float* b1;
+  Prologue pro1;
+  const void* w2;
+  const float* b2;
+  Prologue pro2;
+  void* y;
+  long long y_bs;
+  int y_ld;
+  const void* accb;
+  long long acc_bs;
+  int acc_ld;
+  float acc_div;
+  double* stats;
+  int stats_ld;
+};
+extern int g_opt_resfused;
+bool st_resfused_eligible(int C, int K, int dil, int dtype);
+int st_resfused(const ResFusedParams& p, hipStream_t stream);
 
 // ---------------------------------------------------------------- misc kernels
 // src [B][C][L] fp32 (torch NCL) -> dst frames [B][L][ld] at channel offset c0; optional stats.

@@ -479,32 +479,61 @@ void conv_out(ConvParams& p, Ctx& c, const Buf& y, int c0, int Lout) {
   p.Lout = Lout;
 }
 
+// hipEvent pair around one profiled launch (stts_profile_*)
+int prof_begin(Ctx& c) {
+  while (g_prof.ev.size() < g_prof.used + 2) {
+    hipEvent_t e;
+    ST_CHECK_HIP(hipEventCreate(&e));
+    g_prof.ev.push_back(e);
+  }
+  ST_CHECK_HIP(hipEventRecord(g_prof.ev[g_prof.used], c.s));
+  return 0;
+}
+int prof_end(Ctx& c, const int (&shape)[8], double fl, double by) {
+  ST_CHECK_HIP(hipEventRecord(g_prof.ev[g_prof.used + 1], c.s));
+  g_prof.used += 2;
+  g_prof.launches++;
+  g_prof.flops += fl;
+  g_prof.bytes += by;
+  Prof::Rec r;
+  for (int k = 0; k < 8; ++k) r.shape[k] = shape[k];
+  r.flops = fl;
+  r.bytes = by;
+  g_prof.rec.push_back(r);
+  return 0;
+}
+
 int conv_run(Ctx& c, ConvParams& p) {
   if (c.dry) return 0;
   const bool prof = g_prof.on;
-  if (prof) {
-    while (g_prof.ev.size() < g_prof.used + 2) {
-      hipEvent_t e;
-      ST_CHECK_HIP(hipEventCreate(&e));
-      g_prof.ev.push_back(e);
-    }
-    ST_CHECK_HIP(hipEventRecord(g_prof.ev[g_prof.used], c.s));
-  }
+  if (prof) ST_CHECK(prof_begin(c));
   int r = st_conv1d(p, c.dtype, c.s);
   if (r) return r;
   if (prof) {
-    ST_CHECK_HIP(hipEventRecord(g_prof.ev[g_prof.used + 1], c.s));
-    g_prof.used += 2;
-    g_prof.launches++;
-    // algorithmic work: a (transposed) conv is 2 * rows * N * Cin * taps flops on its GEMM view
+    // algorithmic work: a (transposed) conv is 2 * rows * N * Cin * taps flops on its GEMM view;
+    // bytes = one read of the input, residual and running sum, one write of the output (none for a
+    // statistics-only launch, y == null)
     const double fl = 2.0 * p.B * (double)p.Lq * p.N * p.Cin * p.KS;
-    double elems = (double)p.B * ((double)p.Lin * p.Cin + (double)p.Lout * p.Cout * (1 + (p.res ? 1 : 0) +
-                                                                                     (p.accb ? 1 : 0)));
+    const double outs = (p.y ? 1 : 0) + (p.res ? 1 : 0) + (p.accb ? 1 : 0);
+    double elems = (double)p.B * ((double)p.Lin * p.Cin + (double)p.Lout * p.Cout * outs);
     const double by = elems * c.esz + (p.y_f32 ? (double)p.B * p.Lout * p.Cout * (4.0 - c.esz) : 0.0);
-    g_prof.flops += fl;
-    g_prof.bytes += by;
     const int flags = (p.res ? 1 : 0) | (p.accb ? 2 : 0) | (st_conv1d_engine(p, c.dtype) << 4);
-    g_prof.rec.push_back({{p.B, p.Lq, p.N, p.Cin, p.KS, p.dil, p.Lout, flags}, fl, by});
+    ST_CHECK(prof_end(c, {p.B, p.Lq, p.N, p.Cin, p.KS, p.dil, p.Lout, flags}, fl, by));
+  }
+  return 0;
+}
+
+int resfused_run(Ctx& c, const ResFusedParams& p) {
+  if (c.dry) return 0;
+  const bool prof = g_prof.on;
+  if (prof) ST_CHECK(prof_begin(c));
+  ST_CHECK(st_resfused(p, c.s));
+  if (prof) {
+    // algorithmic work of the two convs; bytes = x once (window + residual), running sum, y
+    const double fl = 2.0 * 2.0 * p.B * (double)p.L * p.C * p.C * p.K;
+    const double by = (double)p.B * p.L * p.C * (2.0 + (p.accb ? 1.0 : 0.0)) * c.esz;
+    const int flags = 1 | (p.accb ? 2 : 0) | (ST_ENGINE_RESFUSED << 4);
+    ST_CHECK(prof_end(c, {p.B, p.L, p.C, p.C, p.K, p.dil, p.L, flags}, fl, by));
   }
   return 0;
 }
@@ -587,6 +616,63 @@ int resblock1(Ctx& c, const ResBlock1& rb, const Buf& X, const double* st_x, Buf
   const int L = X.L, C = rb.C;
   const Buf* xc = &X;
   const double* st_c = st_x;
+  if (st_resfused_eligible(C, rb.K, 1, c.dtype)) {
+    // fused iterations (resfused.hip): a statistics-only conv1 launch, then one launch for
+    // conv1 -> AdaIN2 -> Snake2 -> conv2 -> +x.  Outputs ping-pong X -> R -> XT -> R (or ACC):
+    // a fused launch reads its input's halos, so it cannot write in place.
+    Buf* outs[3] = {&R, &XT, &R};
+    for (int d = 0; d < 3; ++d) {
+      if (!st_resfused_eligible(C, rb.K, rb.dil[d], c.dtype)) return ST_EINVAL;
+      double* st_xt = c.stat(C);
+      ConvParams p = conv_base(c, rb.c1[d], *xc, 0);
+      p.pro = pro_adain(c, rb.a1[d], st_c, C, L, PRO_SNAKE, rb.al1[d], 0.f);
+      p.dil = rb.dil[d];
+      p.pad = rb.dil[d] * (rb.K - 1) / 2;
+      p.Lq = L;
+      conv_out(p, c, XT, 0, L);
+      p.y = nullptr;  // statistics only
+      p.stats = st_xt;
+      p.stats_ld = C;
+      RUN(conv_run(c, p));
+      ResFusedParams f;
+      memset(&f, 0, sizeof(f));
+      f.x = xc->p;
+      f.x_bs = xc->bs;
+      f.x_ld = xc->ld;
+      f.B = c.B;
+      f.L = L;
+      f.C = C;
+      f.K = rb.K;
+      f.dil = rb.dil[d];
+      f.w1 = c.wpk(rb.c1[d]);
+      f.b1 = c.P(rb.c1[d].bias);
+      f.pro1 = p.pro;
+      f.w2 = c.wpk(rb.c2[d]);
+      f.b2 = c.P(rb.c2[d].bias);
+      f.pro2 = pro_adain(c, rb.a2[d], st_xt, C, L, PRO_SNAKE, rb.al2[d], 0.f);
+      const bool final = d == 2;
+      const Buf* y = (final && ro != RO_PLAIN) ? ACC : outs[d];
+      f.y = y->p;
+      f.y_bs = y->bs;
+      f.y_ld = y->ld;
+      if (final && ro != RO_PLAIN) {
+        if (ro != RO_ACC_FIRST) {
+          f.accb = ACC->p;
+          f.acc_bs = ACC->bs;
+          f.acc_ld = ACC->ld;
+          if (ro == RO_ACC_LAST) f.acc_div = (float)nk;
+        }
+      } else if (!final) {
+        double* st_r = c.stat(C);
+        f.stats = st_r;
+        f.stats_ld = C;
+        st_c = st_r;
+      }
+      RUN(resfused_run(c, f));
+      xc = outs[d];
+    }
+    return 0;
+  }
   for (int d = 0; d < 3; ++d) {
     double* st_xt = c.stat(C);
     {
@@ -1191,6 +1277,7 @@ int stts_set_option(int key, int value) {
   switch (key) {
     case STTS_OPT_RESCONV: g_opt_resconv = value != 0; return 0;
     case STTS_OPT_GRID_CAP: g_opt_grid_cap = value > 0 ? value : 0; return 0;
+    case STTS_OPT_RESFUSED: g_opt_resfused = value != 0; return 0;
     default: return ST_EINVAL;
   }
 }

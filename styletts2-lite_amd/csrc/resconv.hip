@@ -261,6 +261,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
 
     // ---- epilogue: lane = frame l32 of block mi, channels (wn*NTL + ni)*32 + 16*hi + r
     bf16_t* yb = reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs;
+    const bool store = p.y != nullptr;
     const bool hr = p.res != nullptr;
     const float osc = p.out_scale;
     const float adiv = (ACC && p.acc_div != 0.f) ? 1.0f / p.acc_div : 1.0f;
@@ -290,7 +291,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
             for (int r = 0; r < 16; ++r) v[r] *= osc;
           }
         }
-        if (valid) {
+        if (valid) {  // y == null: statistics-only pass (resfused.hip needs conv1's statistics)
           if constexpr (ACC) {
             float r0[8], r1[8];
             bf8_to_f32(racc[mi][ni][0], r0);
@@ -301,9 +302,11 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
               v[8 + r] = (r1[r] + v[8 + r]) * adiv;
             }
           }
-          bf16_t* dst = yb + (size_t)q * p.y_ld + co0;
-          *reinterpret_cast<uint4*>(dst) = f32_to_bf8(&v[0]);
-          *reinterpret_cast<uint4*>(dst + 8) = f32_to_bf8(&v[8]);
+          if (store) {
+            bf16_t* dst = yb + (size_t)q * p.y_ld + co0;
+            *reinterpret_cast<uint4*>(dst) = f32_to_bf8(&v[0]);
+            *reinterpret_cast<uint4*>(dst + 8) = f32_to_bf8(&v[8]);
+          }
           if constexpr (!ACC) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {

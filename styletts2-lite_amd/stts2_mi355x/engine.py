@@ -75,6 +75,7 @@ def lib():
 
 OPT_RESCONV = 1
 OPT_GRID_CAP = 2
+OPT_RESFUSED = 3
 
 
 def set_option(key: int, value: int) -> None:
@@ -291,7 +292,7 @@ def profile_read():
     return {"ms": t.value, "launches": n.value, "flops": f.value, "bytes": b.value}
 
 
-ENGINE_KERNELS = ("conv1d_igemm_kernel", "k_resconv", "k_bigconv")  # st_conv1d_engine ids 0, 1, 2
+ENGINE_KERNELS = ("conv1d_igemm_kernel", "k_resconv", "k_bigconv", "k_resfused")  # engine ids 0..3
 
 
 def profile_launches():

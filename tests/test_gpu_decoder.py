@@ -106,3 +106,25 @@ def test_resconv_engine_decoder_ab():
     err = np.abs(out - ref).max()
     print(f"resconv A/B: max-abs {err:.3e} corr {corr:.7f}")
     assert corr > 0.9995 and err < 5e-2
+
+
+@pytest.mark.parametrize("cap", [0, 3])
+def test_resfused_decoder_ab(cap):
+    """bf16 HiFi-GAN decode with the fused resblock iterations (resfused.hip: statistics-only conv1
+    + one conv1 -> conv2 launch) on and off.  Same bf16 model; the fused path keeps xt in LDS
+    (rounded to bf16 once, like the unfused store) and accumulates in the same order.  cap = 3:
+    three workgroups walk every tile, crossing utterances (coefficient switch, statistics flush)."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_GRID_CAP, cap)
+        E.set_option(E.OPT_RESFUSED, 0)
+        ref = run("hifigan", 2, 40, "bf16")
+        E.set_option(E.OPT_RESFUSED, 1)
+        out = run("hifigan", 2, 40, "bf16")
+    finally:
+        E.set_option(E.OPT_RESFUSED, 1)
+        E.set_option(E.OPT_GRID_CAP, 0)
+    corr = np.corrcoef(out.ravel(), ref.ravel())[0, 1]
+    err = np.abs(out - ref).max()
+    print(f"resfused A/B (grid cap {cap}): max-abs {err:.3e} corr {corr:.7f}")
+    assert corr > 0.9995 and err < 5e-2
