@@ -106,8 +106,11 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   const int ntn = (p.N + BN - 1) / BN;
   const int ntm = (p.Lq + BM - 1) / BM;
   const long long total = (long long)ntn * ntm * p.B;
-  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
-  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
+  // XCD-aware: the tile ranges of consecutive logical blocks (same column tile, same weights)
+  // land on one XCD, so each XCD's L2 holds the weights of ~1/8 of the column tiles
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tbeg = (int)(total * bid / gridDim.x);
+  const int tend = (int)(total * (bid + 1) / gridDim.x);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
@@ -174,8 +177,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   // software-pipelined through registers like the input window — group g+1's loads are issued
   // right after group g is written to LDS, so the L2 latency hides under group g's MFMAs.
   constexpr int MAXW = 4;  // 16-byte W units per thread per group (launch_cfg sizes tg to fit)
-  uint4 wpre[MAXW];
-  auto issue_w = [&](int t, int c, int tap0) {
+  auto issue_w = [&](int t, int c, int tap0, uint4 (&wpre)[MAXW]) {
     const int n0 = t_nt(t) * BN;
     const int ntap = min(p.tg, p.KS - tap0);
 #pragma unroll
@@ -196,7 +198,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       wpre[k] = bload16(rw, off);
     }
   };
-  auto put_w = [&](int ntap) {
+  auto put_w = [&](int ntap, const uint4 (&wpre)[MAXW]) {
 #pragma unroll
     for (int k = 0; k < MAXW; ++k) {
       const int u = tid + k * NT;
@@ -213,13 +215,15 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   // ---- input-window staging, software-pipelined over (tile, chunk) steps: the raw loads of
   // step s+1 are issued into registers right after step s's window is written to LDS, so HBM
   // latency hides under step s's MFMAs and epilogue.
-  constexpr int MAXU = 6;  // prefetched 8-channel units per thread; the rest load synchronously
-  typename RawT<T>::type pre[MAXU];
+  // prefetched 8-channel units per thread (two sets in flight); the rest load synchronously.
+  // Sized for a 'same' window of BM + a few rows; the strided config (iSTFTNet noise_convs)
+  // has windows of ~6 BM rows.
+  constexpr int MAXU = (!C::BF || (WAVES_M == 2 && WAVES_N == 2)) ? 6 : (BM * 4 + NT - 1) / NT + 1;
   const int units = R * 4;
   // every unit of a thread is the same 8-channel group: u = tid + k*NT, NT % 4 == 0
   const int g8 = tid & 3;
 
-  auto issue = [&](int t, int c) {
+  auto issue = [&](int t, int c, typename RawT<T>::type (&pre)[MAXU]) {
     const int mt = t_mt(t), b = t_b(t);
     const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * p.x_bs;
     const Rsrc rx = make_rsrc(xb, (unsigned)((size_t)p.Lin * p.x_ld * sizeof(T)));
@@ -312,7 +316,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
     }
   };
 
-  auto write_x = [&](int t, int c) {
+  auto write_x = [&](int t, int c, const typename RawT<T>::type (&pre)[MAXU]) {
     const int ci0 = c * BK;
     const int gr0 = t_mt(t) * BM * p.stride - p.pad;
     Coef8 k;
@@ -349,11 +353,20 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   };
   Raw16 rres[PREF ? WM : 1][PREF ? WN : 1], racc[PREF ? WM : 1][PREF ? WN : 1];
   const int nsteps = (tend - tbeg) * p.nchunks;
+  // two register sets: the raw window / weight loads of step s+2 are issued while step s is
+  // staged, so each load has a full step of MFMAs (not just the staging) to land
+  constexpr int PD = 2;
+  typename RawT<T>::type preA[MAXU], preB[PD == 2 ? MAXU : 1];
+  uint4 wpA[MAXW], wpB[PD == 2 ? MAXW : 1];
   if (nsteps > 0) {
-    issue(tbeg, 0);
-    if (!resident) issue_w(tbeg, 0, 0);
+    issue(tbeg, 0, preA);
+    if (!resident) issue_w(tbeg, 0, 0, wpA);
   }
-  for (int st = 0; st < nsteps; ++st) {
+  if (PD == 2 && nsteps > 1) {
+    issue(tbeg + 1 / p.nchunks, 1 % p.nchunks, reinterpret_cast<decltype(preA)&>(preB));
+    if (!resident) issue_w(tbeg + 1 / p.nchunks, 1 % p.nchunks, 0, reinterpret_cast<decltype(wpA)&>(wpB));
+  }
+  auto step = [&](int st, typename RawT<T>::type (&pre)[MAXU], uint4 (&wpre)[MAXW]) {
     const int t = tbeg + st / p.nchunks, c = st % p.nchunks;
     const int mt = t_mt(t);
     const int b = t_b(t);
@@ -424,8 +437,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       }
     }
     __syncthreads();  // previous readers of Xs (MFMA) are done; coef / bias / W visible
-    write_x(t, c);
-    if (st + 1 < nsteps) issue(tbeg + (st + 1) / p.nchunks, (st + 1) % p.nchunks);
+    write_x(t, c, pre);
+    if (st + PD < nsteps) issue(tbeg + (st + PD) / p.nchunks, (st + PD) % p.nchunks, pre);
     // ---- taps (weights resident, or staged in groups that fit the budget) ----
     for (int tap0 = 0; tap0 < p.KS; tap0 += resident ? p.KS : p.tg) {
       const int ntap = resident ? p.KS : min(p.tg, p.KS - tap0);
@@ -434,16 +447,17 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
         wbase = Ws + (size_t)c * p.KS * W_TAP;
       } else {
         if (tap0 > 0) __syncthreads();  // every wave is done reading the previous group
-        put_w(ntap);
-        if (tap0 + p.tg < p.KS) issue_w(t, c, tap0 + p.tg);
-        else if (st + 1 < nsteps) issue_w(tbeg + (st + 1) / p.nchunks, (st + 1) % p.nchunks, 0);
+        put_w(ntap, wpre);
+        if (tap0 + p.tg < p.KS) issue_w(t, c, tap0 + p.tg, wpre);
+        else if (st + PD < nsteps) issue_w(tbeg + (st + PD) / p.nchunks, (st + PD) % p.nchunks, 0, wpre);
         wbase = Ws;
       }
       __syncthreads();
 #pragma unroll 1
       for (int tl = 0; tl < ntap; ++tl) {
         const int tap = tap0 + tl;
-        const int toff = (tap / p.kw) * p.row_off + (tap % p.kw) * p.dil;
+        // 1-D convs (row_off == 0): no per-tap division on the scalar unit
+        const int toff = p.row_off == 0 ? tap * p.dil : (tap / p.kw) * p.row_off + (tap % p.kw) * p.dil;
         const MT* wt = wbase + (size_t)tl * W_TAP;
         if constexpr (C::BF) {
 #pragma unroll
@@ -488,7 +502,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
         }
       }
     }
-    if (c != p.nchunks - 1) continue;
+    if (c != p.nchunks - 1) return;
 
     // ---------------- epilogue, straight from registers: lane = (frame, 16 channels) ----------------
     T* yT = reinterpret_cast<T*>(p.y) + (size_t)b * p.y_bs;
@@ -624,6 +638,14 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
         }
       }
     }
+  };
+  if constexpr (PD == 2) {
+    for (int st = 0; st < nsteps; st += 2) {
+      step(st, preA, wpA);
+      if (st + 1 < nsteps) step(st + 1, preB, wpB);
+    }
+  } else {
+    for (int st = 0; st < nsteps; ++st) step(st, preA, wpA);
   }
   if (cur_nt >= 0 && p.stats) flush_stats(cur_nt, cur_b);
 }
