@@ -102,6 +102,9 @@ const char* stts_error_string(int code);
  *                     as a statistics-only conv1 launch + one fused conv1 -> conv2 launch
  *                     (resfused.hip); 0 = two conv launches per iteration (A/B, cross-checking). */
 #define STTS_OPT_RESFUSED 3
+/*   STTS_OPT_DEBUG    bit mask skipping phases of the resblock engine (1 prologue math, 2 MFMAs,
+ *                     4 epilogue) for timing experiments; outputs are WRONG while set.  0 = off. */
+#define STTS_OPT_DEBUG 4
 int stts_set_option(int key, int value);
 
 /* Optional per-launch timing of the conv engines (conv1d_igemm, resconv, bigconv) with hipEvents

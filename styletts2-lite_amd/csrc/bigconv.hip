@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
             v[4 * h + j] = __builtin_fmaf(c, ani[j], x2);
           }
         }
-        uint4 o = f32_to_bf8(v);
+        uint4 o = (p.dbg & 1) ? xr[k] : f32_to_bf8(v);
         if ((unsigned)(gr0 + r) >= (unsigned)p.Lin) o = make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4*>(X + r * XP + 8 * g8) = o;
         asm volatile("" ::: "memory");  // reload the coefficients per unit (register budget)
@@ -261,6 +261,7 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
 
   f32x16 acc[MT][NTL];
   auto epilogue = [&](int t) __attribute__((always_inline)) {
+    if (p.dbg & 4) return;
     const int b = t / ntm, mt = t - b * ntm;
     bf16_t* yb = reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs;
     const bf16_t* rb = p.res ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr;
@@ -364,6 +365,7 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   const bf16_t* wbase = Ws + (size_t)((wn * NTL) * 32 + l32) * 32;
   const bf16_t* xbase = Xs + (size_t)((wm * MT) * 32 + l32) * XP + hi * 8;
   auto mfma_step = [&](int g) __attribute__((always_inline)) {
+    if (p.dbg & 2) return;
     const int s = g % NS, tap = s % K;
     const int gg = g / K;  // global group index
     const bf16_t* wt = wbase + (size_t)(g & 3) * G::WSLICE;
@@ -388,17 +390,18 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
       }
   };
 
-  // ---------------- sub-step g (one (group, tap) slice): MFMAs plus the staging it owns
+  // ---------------- sub-step g (one (group, tap) slice), split into the staging it owns (for
+  // later sub-steps) and its MFMAs + epilogue
   uint4 wr[2][WPT];  // weight slices of the next super-step (registers, one super-step of cover)
   int cur_b = tbeg / ntm;
-  auto sub = [&](int g, bool first) __attribute__((always_inline)) {
+  auto stage_sub = [&](int g, bool first) __attribute__((always_inline)) {
     const int tl = g / NS, s = g - tl * NS, t = tbeg + tl;
     const int gi = s / K, tap = s - gi * K;
     const int gg = tl * NG + gi;
     if (s == 0) {
       const int b = t / ntm;
-      if (b != cur_b) {  // statistics of the utterance the block just left
-        if constexpr (SREG) {
+      if (b != cur_b) {  // statistics of the utterance the block just left (every epilogue of its
+        if constexpr (SREG) {  // last tile ran >= 1 barrier ago; the next one runs a tile later)
           if (p.stats) flush_reg(cur_b);
         } else if (!ACC) {
           if (p.stats) flush_lds(cur_b);
@@ -408,6 +411,26 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
       // the next tile opens another utterance: its coefficients (other parity slot), first read
       // by the transform at sub-step NS-2 of this tile, >= 1 barrier later
       if (t + 1 < tend && (t + 1) / ntm != b) set_coef((t + 1) / ntm);
+    }
+    if (first && !(p.dbg & 8)) {  // slices g+2, g+3 -> their ring slots (last read one super-step ago); load g+4, g+5
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (g + 2 + j < nsteps) store_w((g + 2 + j) & 3, wr[j]);
+        issue_w(g + 4 + j, wr[j]);
+      }
+    }
+    if (tap == K - 2) {
+      // window of group gg+1 into the other window slot: its last reader (group gg-1) finished
+      // >= 1 super-step ago, its first reader (group gg+1, sub-step s+2) runs >= 1 super-step later
+      if (!(p.dbg & 16)) {
+        transform_x(gg + 1);
+        issue_x(gg + 2);  // the next window's raw loads: one full group (K sub-steps) of cover
+      }
+    }
+  };
+  auto mfma_sub = [&](int g) __attribute__((always_inline)) {
+    const int tl = g / NS, s = g - tl * NS, t = tbeg + tl;
+    if (s == 0) {
 #pragma unroll
       for (int ni = 0; ni < NTL; ++ni) {  // the accumulators start at the bias
         float bb[16];
@@ -419,19 +442,6 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[mi][ni][r] = bb[r];
       }
-    }
-    if (first) {  // slices g+2, g+3 -> their ring slots (last read one super-step ago); load g+4, g+5
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (g + 2 + j < nsteps) store_w((g + 2 + j) & 3, wr[j]);
-        issue_w(g + 4 + j, wr[j]);
-      }
-    }
-    if (tap == K - 2) {
-      // window of group gg+1 into the other window slot: its last reader (group gg-1) finished
-      // >= 1 barrier ago, its first reader (group gg+1, sub-step s+2) runs >= 1 barrier later
-      transform_x(gg + 1);
-      issue_x(gg + 2);  // the next window's raw loads: one full group (K sub-steps) of cover
     }
     if (s == NS - 1) issue_epi(t);  // residual rows (C = 128 path): this sub-step's MFMAs cover them
     mfma_step(g);
@@ -453,11 +463,16 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   issue_x(1);
 
   // super-steps of two sub-steps per barrier (NS is even: a tile never splits a super-step); the
-  // weight ring has 4 slots, the window ring 2 (transform at tap K-2, see sub)
+  // weight ring has 4 slots, the window ring 2 (transform at tap K-2, see stage_sub).  stage(h)
+  // writes only what MFMA(h+1..) reads and overwrites only what MFMA(h-1..) read.  (A ping-pong
+  // variant, the two wave groups half a super-step apart so one stages while the other issues
+  // MFMAs, measured no faster: the staging, not the MFMA pipe, is what the waves wait on.)
   for (int g = 0; g < nsteps; g += 2) {
     __syncthreads();  // slices g, g+1 and their windows visible; slots of g-2, g-1 free
-    sub(g, true);
-    sub(g + 1, false);
+    stage_sub(g, true);
+    mfma_sub(g);
+    stage_sub(g + 1, false);
+    mfma_sub(g + 1);
   }
   __syncthreads();
   if constexpr (SREG) {

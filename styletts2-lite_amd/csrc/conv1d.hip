@@ -725,6 +725,7 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
 int g_opt_resconv = 1;
 int g_opt_resfused = 0;
 int g_opt_grid_cap = 0;
+int g_opt_debug = 0;
 
 int st_conv1d_engine(const ConvParams& p, int dtype) {
   ConvParams q = p;
@@ -740,6 +741,7 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (p.x_ld % 8 != 0 || p.nchunks * BK < p.Cin) return ST_EINVAL;
   ConvParams q = p;
   if (q.kw <= 0) q.kw = q.KS;
+  q.dbg = g_opt_debug;
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return st_resconv(q, stream);
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return st_bigconv(q, stream);
   if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);

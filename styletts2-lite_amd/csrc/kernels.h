@@ -43,6 +43,7 @@ struct ConvParams {
   // zero columns: output rows o with (o % zc_period) >= zc_valid are written as 0 and excluded
   // from the statistics (keeps the padded image borders zero); zc_period = 0 disables.
   int zc_period, zc_valid;
+  int dbg;         // phase-skipping timing knob (STTS_OPT_DEBUG; results are wrong when set)
   int tg;          // taps per staged weight group (set by the launcher)
   int w_resident;  // weights of the column tile stay in LDS across tiles (set by the launcher)
 };
@@ -57,6 +58,7 @@ bool st_resconv_eligible(const ConvParams& p, int dtype);
 int st_resconv(const ConvParams& p, hipStream_t stream);
 extern int g_opt_resconv;
 extern int g_opt_grid_cap;  // > 0: cap persistent conv grids (tests: many tiles per block)
+extern int g_opt_debug;     // resconv phase-skipping knob (timing experiments only)
 // wide-stage resblock conv engine (bigconv.hip): bf16, C = 128 / 256, same contract
 bool st_bigconv_eligible(const ConvParams& p, int dtype);
 int st_bigconv(const ConvParams& p, hipStream_t stream);

@@ -1278,6 +1278,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_RESCONV: g_opt_resconv = value != 0; return 0;
     case STTS_OPT_GRID_CAP: g_opt_grid_cap = value > 0 ? value : 0; return 0;
     case STTS_OPT_RESFUSED: g_opt_resfused = value != 0; return 0;
+    case STTS_OPT_DEBUG: g_opt_debug = value; return 0;
     default: return ST_EINVAL;
   }
 }

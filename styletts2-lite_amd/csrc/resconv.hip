@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
           const float c = __builtin_amdgcn_cosf(__builtin_fmaf(v[j], ar[j], mr[j]));
           v[j] = __builtin_fmaf(c, nia[j], x2);
         }
-        uint4 o = f32_to_bf8(v);
+        uint4 o = (p.dbg & 1) ? pre[k] : f32_to_bf8(v);
         if ((unsigned)(gr0 + r) >= (unsigned)p.Lin) o = make_uint4(0, 0, 0, 0);  // zero padding is post-prologue
         *reinterpret_cast<uint4*>(Xs + r * XP + 8 * g8) = o;
       }
@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     const bf16_t* xw = Xs + (size_t)(wm * FW + l32) * XP + hi * 8;
     const bf16_t* ww = Ws + (size_t)(wn * NTL * 32 + l32) * WP + hi * 8;
 #pragma unroll 1
-    for (int tap = 0; tap < K; ++tap) {
+    for (int tap = 0; tap < ((p.dbg & 2) ? 0 : K); ++tap) {
       const bf16_t* xt = xw + tap * DIL * XP;
       const bf16_t* wt = ww + tap * C * WP;
 #pragma unroll
@@ -260,6 +260,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     }
 
     // ---- epilogue: lane = frame l32 of block mi, channels (wn*NTL + ni)*32 + 16*hi + r
+    if (p.dbg & 4) return;
     bf16_t* yb = reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs;
     const bool store = p.y != nullptr;
     const bool hr = p.res != nullptr;

@@ -76,6 +76,7 @@ def lib():
 OPT_RESCONV = 1
 OPT_GRID_CAP = 2
 OPT_RESFUSED = 3
+OPT_DEBUG = 4
 
 
 def set_option(key: int, value: int) -> None:
