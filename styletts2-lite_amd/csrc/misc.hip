@@ -836,11 +836,17 @@ int st_gap_linear(const void* z, int B, int rows, int Wv, int C, const float* w,
 int st_noise_conv(const float* har, int B, int L, const float* w, const float* bias, int C, int K, int S, int P,
                   int Lout, void* y, double* stats, int dtype, hipStream_t s) {
   if (C % 8 || 256 % (C / 8) || C > 256) return ST_EINVAL;
-  const int fpb = 8192;
-  dim3 grid((Lout + fpb - 1) / fpb, B);
+  // frames per block: about 2048 blocks over the batch (8 per CU), a multiple of the frames one
+  // block covers per pass (256 / (C/8)); statistics cost one atomic pair per (block, channel)
+  const int fstep = 256 / (C / 8);
+  long long fpb = ((long long)Lout * B + 2047) / 2048;
+  fpb = (fpb + fstep - 1) / fstep * fstep;
+  if (fpb < fstep) fpb = fstep;
+  if (fpb > 8192) fpb = 8192;
+  dim3 grid((unsigned)((Lout + fpb - 1) / fpb), B);
 #define NCONV(KC)                                                                                              \
   DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_noise_conv<T, KC>), grid, dim3(256), 0, s, har, L, w, bias, C, S, \
-                                              P, Lout, fpb, reinterpret_cast<T*>(y), stats))
+                                              P, Lout, (int)fpb, reinterpret_cast<T*>(y), stats))
   switch (K) {
     case 1: NCONV(1); break;
     case 4: NCONV(4); break;
