@@ -66,8 +66,8 @@ struct ConvCfg {
   __host__ __device__ static size_t xs_bytes(const ConvParams& p) {
     return (((size_t)rows(p) * XP * sizeof(MT)) + 15) & ~(size_t)15;
   }
-  static size_t lds_bytes(const ConvParams& p, int nwslices) {
-    return coef_bytes(p) + xs_bytes(p) + (size_t)nwslices * W_TAP * sizeof(MT);
+  static size_t lds_bytes(const ConvParams& p, int nwslices, int nx = 1) {
+    return coef_bytes(p) + (size_t)nx * xs_bytes(p) + (size_t)nwslices * W_TAP * sizeof(MT);
   }
 };
 
@@ -88,7 +88,7 @@ __device__ __forceinline__ void pw(float (&v)[16], int i, f2v x) {
 // 16*((m>>2)&1) + (m&3) + 4*(m>>3)), 16 CONSECUTIVE channels 16*(lane>>5) + r.  The epilogue
 // therefore works straight from registers: no LDS transpose, 16-channel vector loads/stores,
 // and per-lane statistics accumulated across tiles (reduced across lanes once per utterance).
-template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW>
+template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW, int CPS>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
     conv1d_igemm_kernel(const ConvParams p) {
   using C = ConvCfg<T, MT, WAVES_M, WAVES_N, WM, WN>;
@@ -101,7 +101,11 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   float* bias_s = coef + 4 * cinp;               // [BN]: bias of the column tile's (phase, channel) columns
   float* ws = bias_s + BN + (size_t)(threadIdx.x >> 6) * 32 * EP;  // this wave's stats scratch [frame][EP]
   MT* Xs = reinterpret_cast<MT*>(smem + C::coef_bytes(p));
-  MT* Ws = reinterpret_cast<MT*>(smem + C::coef_bytes(p) + C::xs_bytes(p));
+  // chunks per step (set by the launcher): 2 = two 32-channel chunks (two windows, two weight
+  // slices) per barrier pair, half the barriers and twice the MFMAs between them
+  constexpr int cps = CPS;
+  MT* Ws = reinterpret_cast<MT*>(smem + C::coef_bytes(p) + (size_t)cps * C::xs_bytes(p));
+  const size_t xs_el = C::xs_bytes(p) / sizeof(MT);
 
   const int ntn = (p.N + BN - 1) / BN;
   const int ntm = (p.Lq + BM - 1) / BM;
@@ -198,16 +202,16 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       wpre[k] = bload16(rw, off);
     }
   };
-  auto put_w = [&](int ntap, const uint4 (&wpre)[MAXW]) {
+  auto put_w = [&](int ntap, const uint4 (&wpre)[MAXW], MT* Wd) {
 #pragma unroll
     for (int k = 0; k < MAXW; ++k) {
       const int u = tid + k * NT;
       if constexpr (C::BF) {
         const int tl = u / (BN * 4), rem = u % (BN * 4), n = rem >> 2, g = rem & 3;
-        if (tl < ntap) *reinterpret_cast<uint4*>(Ws + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = wpre[k];
+        if (tl < ntap) *reinterpret_cast<uint4*>(Wd + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = wpre[k];
       } else {
         const int tl = u / (BK * (BN / 4)), rem = u % (BK * (BN / 4)), kq = rem / (BN / 4), g = rem % (BN / 4);
-        if (tl < ntap) *reinterpret_cast<uint4*>(Ws + (size_t)tl * W_TAP + kq * WPITCH + 4 * g) = wpre[k];
+        if (tl < ntap) *reinterpret_cast<uint4*>(Wd + (size_t)tl * W_TAP + kq * WPITCH + 4 * g) = wpre[k];
       }
     }
   };
@@ -263,7 +267,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
     }
   };
 
-  auto put = [&](int u, float (&v)[8], bool ok, int ci0, const Coef8& k) {
+  auto put = [&](int u, float (&v)[8], bool ok, int ci0, const Coef8& k, MT* Xd) {
     const int r = u >> 2;
     const int ch = ci0 + 8 * g8;
     if (ok) {
@@ -304,7 +308,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = 0.f;
     }
-    MT* dst = Xs + r * XP + 8 * g8;
+    MT* dst = Xd + r * XP + 8 * g8;
     if constexpr (C::BF) {
       bf16x8 o;
 #pragma unroll
@@ -316,7 +320,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
     }
   };
 
-  auto write_x = [&](int t, int c, const typename RawT<T>::type (&pre)[MAXU]) {
+  auto write_x = [&](int t, int c, const typename RawT<T>::type (&pre)[MAXU], MT* Xd) {
     const int ci0 = c * BK;
     const int gr0 = t_mt(t) * BM * p.stride - p.pad;
     Coef8 k;
@@ -328,7 +332,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       float v[8];
       raw_to_f32(pre[kk], v);
       // conv zero padding applies to the post-prologue activation
-      if (u < units) put(u, v, gr >= 0 && gr < p.Lin, ci0, k);
+      if (u < units) put(u, v, gr >= 0 && gr < p.Lin, ci0, k, Xd);
     }
     if (units > MAXU * NT) {  // large windows (2-D style convs): synchronous remainder
       const int b = t_b(t);
@@ -341,7 +345,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
         bload_raw(rx, (unsigned)(gr * p.x_ld + ch), raw, (const T*)nullptr);
         float v[8];
         raw_to_f32(raw, v);
-        put(u, v, gr >= 0 && gr < p.Lin, ci0, k);
+        put(u, v, gr >= 0 && gr < p.Lin, ci0, k, Xd);
       }
     }
   };
@@ -352,22 +356,32 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
     typename RawT<T>::type a, b;
   };
   Raw16 rres[PREF ? WM : 1][PREF ? WN : 1], racc[PREF ? WM : 1][PREF ? WN : 1];
-  const int nsteps = (tend - tbeg) * p.nchunks;
-  // two register sets: the raw window / weight loads of step s+2 are issued while step s is
-  // staged, so each load has a full step of MFMAs (not just the staging) to land
-  constexpr int PD = 2;
-  typename RawT<T>::type preA[MAXU], preB[PD == 2 ? MAXU : 1];
-  uint4 wpA[MAXW], wpB[PD == 2 ? MAXW : 1];
+  const int npt = (p.nchunks + cps - 1) / cps;  // steps per tile
+  const int nsteps = (tend - tbeg) * npt;
+  // Two register sets (A, B).  cps == 1: the window / weight loads of step s+2 are issued while
+  // step s is staged (A and B alternate).  cps == 2: a step stages chunks c (A) and c+1 (B) and
+  // issues the next step's two chunks, so each load still has a full step of MFMAs to land.
+  constexpr int PD = cps == 2 ? 1 : 2;
+  auto st_tile = [&](int st) { return tbeg + st / npt; };
+  auto st_chunk = [&](int st) { return (st % npt) * cps; };
+  typename RawT<T>::type preA[MAXU], preB[MAXU];
+  uint4 wpA[MAXW], wpB[MAXW];
   if (nsteps > 0) {
     issue(tbeg, 0, preA);
     if (!resident) issue_w(tbeg, 0, 0, wpA);
+    if constexpr (cps == 2) {
+      issue(tbeg, 1, preB);
+      if (!resident) issue_w(tbeg, 1, 0, wpB);
+    } else if (nsteps > 1) {
+      issue(st_tile(1), st_chunk(1), preB);
+      if (!resident) issue_w(st_tile(1), st_chunk(1), 0, wpB);
+    }
   }
-  if (PD == 2 && nsteps > 1) {
-    issue(tbeg + 1 / p.nchunks, 1 % p.nchunks, reinterpret_cast<decltype(preA)&>(preB));
-    if (!resident) issue_w(tbeg + 1 / p.nchunks, 1 % p.nchunks, 0, reinterpret_cast<decltype(wpA)&>(wpB));
-  }
-  auto step = [&](int st, typename RawT<T>::type (&pre)[MAXU], uint4 (&wpre)[MAXW]) {
-    const int t = tbeg + st / p.nchunks, c = st % p.nchunks;
+  auto step = [&](int st, typename RawT<T>::type (&pre)[MAXU], uint4 (&wpre)[MAXW],
+                  typename RawT<T>::type (&pre2)[MAXU], uint4 (&wpre2)[MAXW]) {
+    const int t = st_tile(st), c = st_chunk(st);
+    const bool last = c + cps >= p.nchunks;     // the tile's epilogue follows this step
+    const bool has2 = cps == 2 && c + 1 < p.nchunks;
     const int mt = t_mt(t);
     const int b = t_b(t);
     const int nt = t_nt(t);
@@ -412,7 +426,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
     // residual / running-sum rows of this tile's epilogue: issued before the MFMAs so their
     // HBM latency hides under them (small-channel configs, where the epilogue dominates)
     if constexpr (PREF) {
-      if (c == p.nchunks - 1) {
+      if (last) {
         const Rsrc rr = make_rsrc(p.res ? reinterpret_cast<const T*>(p.res) + (size_t)b * p.res_bs : (const T*)p.y,
                                   p.res ? (unsigned)(p.res_bs * sizeof(T)) : 0u);
         const Rsrc ra = make_rsrc(p.accb ? reinterpret_cast<const T*>(p.accb) + (size_t)b * p.acc_bs : (const T*)p.y,
@@ -437,28 +451,43 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       }
     }
     __syncthreads();  // previous readers of Xs (MFMA) are done; coef / bias / W visible
-    write_x(t, c, pre);
-    if (st + PD < nsteps) issue(tbeg + (st + PD) / p.nchunks, (st + PD) % p.nchunks, pre);
+    write_x(t, c, pre, Xs);
+    if (has2) write_x(t, c + 1, pre2, Xs + xs_el);
+    if (st + PD < nsteps) {
+      issue(st_tile(st + PD), st_chunk(st + PD), pre);
+      if (cps == 2) issue(st_tile(st + 1), st_chunk(st + 1) + 1, pre2);
+    }
     // ---- taps (weights resident, or staged in groups that fit the budget) ----
     for (int tap0 = 0; tap0 < p.KS; tap0 += resident ? p.KS : p.tg) {
       const int ntap = resident ? p.KS : min(p.tg, p.KS - tap0);
       const MT* wbase;
+      const MT* wbase2;  // chunk c+1 (cps == 2; the launcher allows it with one tap group only)
       if (resident) {
         wbase = Ws + (size_t)c * p.KS * W_TAP;
+        wbase2 = wbase + (size_t)p.KS * W_TAP;
       } else {
         if (tap0 > 0) __syncthreads();  // every wave is done reading the previous group
-        put_w(ntap, wpre);
-        if (tap0 + p.tg < p.KS) issue_w(t, c, tap0 + p.tg, wpre);
-        else if (st + PD < nsteps) issue_w(tbeg + (st + PD) / p.nchunks, (st + PD) % p.nchunks, 0, wpre);
+        put_w(ntap, wpre, Ws);
+        if (has2) put_w(ntap, wpre2, Ws + (size_t)p.tg * W_TAP);
+        if (tap0 + p.tg < p.KS) {
+          issue_w(t, c, tap0 + p.tg, wpre);
+        } else if (st + PD < nsteps) {
+          issue_w(st_tile(st + PD), st_chunk(st + PD), 0, wpre);
+          if (cps == 2) issue_w(st_tile(st + 1), st_chunk(st + 1) + 1, 0, wpre2);
+        }
         wbase = Ws;
+        wbase2 = Ws + (size_t)p.tg * W_TAP;
       }
       __syncthreads();
+      for (int half = 0; half < (has2 ? 2 : 1); ++half) {
+      const MT* Xc = half ? Xs + xs_el : Xs;
+      const MT* wb = half ? wbase2 : wbase;
 #pragma unroll 1
       for (int tl = 0; tl < ntap; ++tl) {
         const int tap = tap0 + tl;
         // 1-D convs (row_off == 0): no per-tap division on the scalar unit
         const int toff = p.row_off == 0 ? tap * p.dil : (tap / p.kw) * p.row_off + (tap % p.kw) * p.dil;
-        const MT* wt = wbase + (size_t)tl * W_TAP;
+        const MT* wt = wb + (size_t)tl * W_TAP;
         if constexpr (C::BF) {
 #pragma unroll
           for (int kk = 0; kk < BK / 16; ++kk) {
@@ -466,7 +495,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi) {
               const int r = (wm * WM + mi) * 32 + l32;
-              af[mi] = *reinterpret_cast<const bf16x8*>(Xs + (r * p.stride + toff) * XP + kk * 16 + hi * 8);
+              af[mi] = *reinterpret_cast<const bf16x8*>(Xc + (r * p.stride + toff) * XP + kk * 16 + hi * 8);
             }
 #pragma unroll
             for (int ni = 0; ni < WN; ++ni) {
@@ -486,7 +515,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi) {
               const int r = (wm * WM + mi) * 32 + l32;
-              af[mi] = Xs[(r * p.stride + toff) * XP + 2 * kk + hi];
+              af[mi] = Xc[(r * p.stride + toff) * XP + 2 * kk + hi];
             }
 #pragma unroll
             for (int ni = 0; ni < WN; ++ni) {
@@ -501,8 +530,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
           }
         }
       }
+      }
     }
-    if (c != p.nchunks - 1) return;
+    if (!last) return;
 
     // ---------------- epilogue, straight from registers: lane = (frame, 16 channels) ----------------
     T* yT = reinterpret_cast<T*>(p.y) + (size_t)b * p.y_bs;
@@ -639,13 +669,13 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       }
     }
   };
-  if constexpr (PD == 2) {
-    for (int st = 0; st < nsteps; st += 2) {
-      step(st, preA, wpA);
-      if (st + 1 < nsteps) step(st + 1, preB, wpB);
-    }
+  if constexpr (cps == 2) {
+    for (int st = 0; st < nsteps; ++st) step(st, preA, wpA, preB, wpB);
   } else {
-    for (int st = 0; st < nsteps; ++st) step(st, preA, wpA);
+    for (int st = 0; st < nsteps; st += 2) {
+      step(st, preA, wpA, preB, wpB);
+      if (st + 1 < nsteps) step(st + 1, preB, wpB, preA, wpA);
+    }
   }
   if (cur_nt >= 0 && p.stats) flush_stats(cur_nt, cur_b);
 }
@@ -675,13 +705,23 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
     while (tg > 1 && C::lds_bytes(p, tg) > (size_t)LDS_MAX) --tg;
     p.tg = tg;
   }
-  const size_t lds = C::lds_bytes(p, p.w_resident ? nres : p.tg);
+  // two chunks per step (bf16 wide configs with one tap group, when the second window and weight
+  // slice fit the LDS): half the barriers and twice the MFMAs between them
+  p.cps = 1;
+  if (C::BF && !NARROW && p.nchunks >= 2 && (p.w_resident || p.tg >= p.KS) &&
+      C::lds_bytes(p, p.w_resident ? nres : 2 * p.tg, 2) <= (size_t)LDS_MAX)
+    p.cps = 2;
+  const size_t lds = C::lds_bytes(p, p.w_resident ? nres : p.cps * p.tg, p.cps);
   if (lds > (size_t)LDS_MAX) return ST_EINVAL;
-  auto kern = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW>;
-  static bool attr_set = false;
-  if (!attr_set) {
+  auto kern1 = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 1>;
+  auto kern = kern1;
+  if constexpr (C::BF && !NARROW) {
+    if (p.cps == 2) kern = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 2>;
+  }
+  static bool attr_set[2] = {false, false};
+  if (!attr_set[p.cps - 1]) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
-    attr_set = true;
+    attr_set[p.cps - 1] = true;
   }
   if (!g_num_cu) {
     int dev = 0;

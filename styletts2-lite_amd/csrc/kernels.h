@@ -45,6 +45,7 @@ struct ConvParams {
   int zc_period, zc_valid;
   int dbg;         // phase-skipping timing knob (STTS_OPT_DEBUG; results are wrong when set)
   int tg;          // taps per staged weight group (set by the launcher)
+  int cps;         // 32-channel chunks per pipeline step, 1 or 2 (set by the launcher)
   int w_resident;  // weights of the column tile stay in LDS across tiles (set by the launcher)
 };
 
