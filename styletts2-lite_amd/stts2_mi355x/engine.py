@@ -216,6 +216,8 @@ class DecoderEngine(_Engine):
                 or tuple(s.shape) != (B, self.style_dim):
             raise ValueError(f"decoder inputs: asr {tuple(asr.shape)}, F0 {tuple(F0_curve.shape)}, "
                              f"N {tuple(N.shape)}, s {tuple(s.shape)}")
+        if T < 2:  # the reference's InstanceNorm1d raises on a single frame (torch F.instance_norm)
+            raise ValueError(f"decoder inputs: need at least 2 asr frames, got {T}")
         Lw = 2 * T * self.scale
         if noise is not None:
             noise = _dev_f32(noise, dev)
@@ -248,6 +250,8 @@ class F0NEngine(_Engine):
         B, T, D = x.shape
         if D != self.d_hid or tuple(s.shape) != (B, self.style_dim):
             raise ValueError(f"F0Ntrain inputs: x {tuple(x.shape)}, s {tuple(s.shape)}")
+        if T < 2:  # as the reference's InstanceNorm1d on a single frame
+            raise ValueError(f"F0Ntrain inputs: need at least 2 frames, got {T}")
         F0 = torch.empty(B, 2 * T, dtype=torch.float32, device=dev)
         Nn = torch.empty(B, 2 * T, dtype=torch.float32, device=dev)
         ws, nb = self.model.workspace(self.dtype, B, T)
