@@ -9,6 +9,7 @@
  *   stts_f0n_fwd      <- models.py:448           ProsodyPredictor.F0Ntrain(x, s)  (conv stacks
  *                        after the shared BiLSTM, models.py:451-461)
  *   stts_style_fwd    <- models.py:145           StyleEncoder.forward(x)
+ *   stts_wave_preprocess <- inference.py:43      Preprocess.wave_preprocess(wave)
  *   stts_model_create / stts_param_* / stts_set_param / stts_pack
  *                     <- the module constructors + load_state_dict (inference.py:93-124, 150-174)
  *
@@ -87,6 +88,17 @@ int stts_f0n_fwd(stts_model* m, int dtype, const float* x, const float* s, int B
 /* Style encoder: mel [B][1][80][T] -> style [B][style_dim]. */
 int stts_style_fwd(stts_model* m, int dtype, const float* mel, int B, int T, float* out, void* workspace,
                    long long ws_bytes, void* stream);
+
+/* Style front-end, <- inference.py:43-49 Preprocess.wave_preprocess(wave) (the torchaudio
+ * MelSpectrogram(n_mels=80, n_fft=2048, win_length=1200, hop_length=300) it builds, then
+ * (log(1e-5 + mel) + 4) / 4): wave [B][wave_ld] with L samples each (L > 1024) ->
+ * mel [B][80][F], F = stts_mel_frames(L) = 1 + L/300 (0 if L <= 1024).  No model handle: the
+ * window, twiddle and filterbank tables are rebuilt in the caller's workspace
+ * (>= stts_mel_workspace_bytes()) on every call. */
+long long stts_mel_frames(long long L);
+long long stts_mel_workspace_bytes(void);
+int stts_wave_preprocess(const float* wave, int B, long long L, long long wave_ld, float* mel, void* workspace,
+                         long long ws_bytes, void* stream);
 
 const char* stts_error_string(int code);
 

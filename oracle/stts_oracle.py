@@ -334,3 +334,68 @@ def style_encoder(mel, sd, prefix="", taps=None):
     h = F.leaky_relu(h, 0.2)
     h = h.view(h.size(0), -1)
     return F.linear(h, _t(sd, prefix + "unshared.weight"), _t(sd, prefix + "unshared.bias"))
+
+
+# ---------------------------------------------------------------- style front-end
+# Parity unpinned upstream: the reference builds its mel with torchaudio (absent from this image and
+# from the reference tree), so these restate torchaudio's published MelSpectrogram defaults as the
+# reference instantiates them (inference.py:43-49): MelSpectrogram(n_mels=80, n_fft=2048,
+# win_length=1200, hop_length=300) with every other argument at its default -- sample_rate 16000
+# (the reference never passes 24000), f_min 0, f_max sample_rate/2, hann_window(periodic), power 2,
+# center=True with reflect padding, onesided, norm None, HTK mel scale.
+MEL = dict(n_mels=80, n_fft=2048, win_length=1200, hop_length=300, sample_rate=16000, mean=-4.0, std=4.0)
+
+
+def _hz_to_mel_htk(f):
+    return 2595.0 * math.log10(1.0 + f / 700.0)
+
+
+def melscale_fbanks(n_freqs=1025, f_min=0.0, f_max=8000.0, n_mels=80, sample_rate=16000):
+    """torchaudio.functional.melscale_fbanks(norm=None, mel_scale="htk"): [n_freqs, n_mels] fp32."""
+    all_freqs = torch.linspace(0, sample_rate // 2, n_freqs)
+    m_pts = torch.linspace(_hz_to_mel_htk(f_min), _hz_to_mel_htk(f_max), n_mels + 2)
+    f_pts = 700.0 * (10 ** (m_pts / 2595.0) - 1.0)
+    f_diff = f_pts[1:] - f_pts[:-1]
+    slopes = f_pts.unsqueeze(0) - all_freqs.unsqueeze(1)
+    down = (-1.0 * slopes[:, :-2]) / f_diff[:-1]
+    up = slopes[:, 2:] / f_diff[1:]
+    return torch.clamp(torch.min(down, up), min=0.0)
+
+
+def mel_spectrogram(wave):
+    """torchaudio.transforms.MelSpectrogram(**reference args)(wave): [..., L] -> [..., 80, 1 + L // 300]."""
+    m = MEL
+    spec = torch.stft(wave, m["n_fft"], m["hop_length"], m["win_length"], torch.hann_window(m["win_length"]),
+                      center=True, pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
+    power = spec.abs().pow(2.0)
+    fb = melscale_fbanks(m["n_fft"] // 2 + 1, 0.0, m["sample_rate"] / 2, m["n_mels"], m["sample_rate"])
+    return torch.matmul(power.transpose(-1, -2), fb).transpose(-1, -2)
+
+
+def wave_preprocess(wave):
+    """reference inference.py:43-49 (Preprocess.wave_preprocess): np [L] -> [1, 80, F] log-mel."""
+    x = torch.from_numpy(np.asarray(wave)).float()
+    mel = mel_spectrogram(x)
+    return (torch.log(1e-5 + mel.unsqueeze(0)) - MEL["mean"]) / MEL["std"]
+
+
+def get_style(audio, sd, sr=24000, split_dur=3, prefix=""):
+    """reference inference.py:195-217 (StyleTTS2.get_styles, after the optional denoise): the style
+    vector of a reference clip, averaged over split_dur-second chunks when the clip is >= 4 s."""
+    audio = np.asarray(audio, dtype=np.float32)
+    enc = lambda a: style_encoder(wave_preprocess(a).unsqueeze(1), sd, prefix)  # noqa: E731
+    if split_dur > 0 and len(audio) / sr >= 4:
+        jump = sr * split_dur
+        total = len(audio)
+        ref = enc(audio[0:jump])
+        count = 1
+        for i in range(jump, total, jump):
+            if i + jump >= total:
+                if (total - i) / sr >= 1:
+                    ref = ref + enc(audio[i:total])
+                    count += 1
+                continue
+            ref = ref + enc(audio[i:i + jump])
+            count += 1
+        return ref / count
+    return enc(audio)

@@ -161,3 +161,10 @@ int st_avgpool_half(const void* x, int B, int H, int W, int C, void* y, int dtyp
 // AdaptiveAvgPool2d(1) over Wv valid rows of z [B][rows][C] -> LeakyReLU(0.2) -> Linear(C, N)
 int st_gap_linear(const void* z, int B, int rows, int Wv, int C, const float* w, const float* bias, int N,
                   float* out, int dtype, hipStream_t s);
+// ---------------------------------------------------------------- style front-end (mel.hip)
+// Preprocess.wave_preprocess (inference.py:43-49): wave fp32 [B][ld] (L samples each) -> log-mel
+// fp32 [B][80][F], F = 1 + L/300.  L must exceed 1024 (reflect padding).
+long long st_mel_frames(long long L);
+long long st_mel_workspace_bytes();
+int st_wave_preprocess(const float* wave, int B, long long L, long long ld, float* mel, void* ws, long long ws_bytes,
+                       hipStream_t stream);

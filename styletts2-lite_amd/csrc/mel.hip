@@ -1,0 +1,138 @@
+// Style front-end: the log-mel spectrogram of Preprocess.wave_preprocess (reference
+// inference.py:43-49), i.e. torchaudio MelSpectrogram(n_mels=80, n_fft=2048, win_length=1200,
+// hop_length=300) at its defaults (sample_rate 16000 -> f_max 8000 over the 1025 one-sided bins,
+// periodic Hann window zero-padded to n_fft, center=True with reflect padding, power 2, HTK mel
+// scale, no filter normalisation), then (log(1e-5 + mel) - (-4)) / 4.
+//
+// One workgroup per (utterance, frame): the 1200 windowed samples and a 2048-entry twiddle table
+// sit in LDS, each thread owns four or five DFT bins (the exact integer phase index k*(n+424)
+// mod 2048 picks the twiddle, so no phase error accumulates over the 1200 terms), the power
+// spectrum goes back to LDS and 80 threads apply their triangular filter over its nonzero bin
+// range.  The tables (window, twiddles, filterbank, per-mel bin ranges) are built into the
+// caller's workspace by a setup kernel on every call -- the library allocates nothing.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int NFFT = 2048, WIN = 1200, HOP = 300, NBIN = NFFT / 2 + 1, NMEL = 80;
+constexpr int WOFF = (NFFT - WIN) / 2;  // torch.stft centres the shorter window in n_fft: 424
+constexpr int NT = 256;
+
+// workspace layout (floats / ints)
+constexpr size_t T_WIN = 0;                      // [WIN]  periodic Hann
+constexpr size_t T_COS = T_WIN + WIN;            // [NFFT] cos(2 pi j / NFFT)
+constexpr size_t T_SIN = T_COS + NFFT;           // [NFFT] sin(2 pi j / NFFT)
+constexpr size_t T_FB = T_SIN + NFFT;            // [NMEL][NBIN] filterbank (mel-major)
+constexpr size_t T_RNG = T_FB + (size_t)NMEL * NBIN;  // [NMEL][2] int: first / last nonzero bin
+constexpr size_t T_END = T_RNG + 2 * NMEL;
+
+// torch.linspace(start, end, steps) in fp32: the first half counts up from start, the second
+// half down from end (aten/src/ATen/native/cpu/RangeFactoriesKernel.cpp)
+__device__ float linspace_f32(float start, float end, int steps, int i) {
+  const float step = (end - start) / (float)(steps - 1);
+  const int half = steps / 2;
+  return i < half ? start + step * (float)i : end - step * (float)(steps - i - 1);
+}
+
+__global__ void k_mel_tables(float* tab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < WIN) {  // torch.hann_window(1200, periodic=True) = 0.5 - 0.5 cos(2 pi n / 1200)
+    tab[T_WIN + i] = (float)(0.5 - 0.5 * cospi(2.0 * i / WIN));
+  }
+  if (i < NFFT) {
+    double s, c;
+    sincospi(2.0 * i / NFFT, &s, &c);
+    tab[T_COS + i] = (float)c;
+    tab[T_SIN + i] = (float)s;
+  }
+  if (i < NMEL) {  // torchaudio.functional.melscale_fbanks(1025, 0, 8000, 80, 16000, None, "htk")
+    const int m = i;
+    const float m_max = 2595.0f * log10f(1.0f + 8000.0f / 700.0f);
+    float f[3];
+    for (int j = 0; j < 3; ++j) {
+      const float mp = linspace_f32(0.0f, m_max, NMEL + 2, m + j);
+      f[j] = 700.0f * (powf(10.0f, mp / 2595.0f) - 1.0f);
+    }
+    const float d0 = f[1] - f[0], d1 = f[2] - f[1];
+    int lo = NBIN, hi = -1;
+    for (int k = 0; k < NBIN; ++k) {
+      const float fk = linspace_f32(0.0f, 8000.0f, NBIN, k);
+      const float down = -(f[0] - fk) / d0, up = (f[2] - fk) / d1;
+      const float w = fmaxf(0.0f, fminf(down, up));
+      tab[T_FB + (size_t)m * NBIN + k] = w;
+      if (w > 0.0f) {
+        lo = min(lo, k);
+        hi = k;
+      }
+    }
+    int* rng = reinterpret_cast<int*>(tab + T_RNG);
+    rng[2 * m] = lo;
+    rng[2 * m + 1] = hi;
+  }
+}
+
+__global__ void __launch_bounds__(NT) k_logmel(const float* __restrict__ wave, long long L, long long ld, int F,
+                                                const float* __restrict__ tab, float* __restrict__ out) {
+  __shared__ float xs[WIN];
+  __shared__ float cs[NFFT], sn[NFFT];
+  __shared__ float pw[NBIN];
+  const int t = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const float* x = wave + (size_t)b * ld;
+  // frame t reads padded samples [t*HOP + WOFF, +WIN) of the signal reflect-padded by NFFT/2
+  const long long base = (long long)t * HOP + WOFF - NFFT / 2;
+  for (int n = tid; n < WIN; n += NT) {
+    long long j = base + n;
+    if (j < 0) j = -j;
+    if (j >= L) j = 2 * (L - 1) - j;
+    xs[n] = x[j] * tab[T_WIN + n];
+  }
+  for (int j = tid; j < NFFT; j += NT) {
+    cs[j] = tab[T_COS + j];
+    sn[j] = tab[T_SIN + j];
+  }
+  __syncthreads();
+  // bins k = tid + NT*i; X[k] = sum_n xw[n] exp(-2 pi i k (n + WOFF) / NFFT)
+  for (int k = tid; k < NBIN; k += NT) {
+    float re = 0.f, im = 0.f;
+    unsigned idx = (unsigned)(k * WOFF) & (NFFT - 1);
+#pragma unroll 8
+    for (int n = 0; n < WIN; ++n) {
+      const float v = xs[n];
+      re = __builtin_fmaf(v, cs[idx], re);
+      im = __builtin_fmaf(v, sn[idx], im);
+      idx = (idx + (unsigned)k) & (NFFT - 1);
+    }
+    pw[k] = __builtin_fmaf(re, re, im * im);
+  }
+  __syncthreads();
+  if (tid < NMEL) {
+    const int* rng = reinterpret_cast<const int*>(tab + T_RNG);
+    const int lo = rng[2 * tid], hi = rng[2 * tid + 1];
+    const float* fb = tab + T_FB + (size_t)tid * NBIN;
+    float acc = 0.f;
+    for (int k = lo; k <= hi; ++k) acc = __builtin_fmaf(pw[k], fb[k], acc);
+    out[((size_t)b * NMEL + tid) * F + t] = (logf(1e-5f + acc) + 4.0f) * 0.25f;
+  }
+}
+
+}  // namespace
+
+long long st_mel_frames(long long L) { return L > NFFT / 2 ? 1 + L / HOP : 0; }
+
+long long st_mel_workspace_bytes() { return (long long)(T_END * sizeof(float)); }
+
+int st_wave_preprocess(const float* wave, int B, long long L, long long ld, float* mel, void* ws, long long ws_bytes,
+                       hipStream_t stream) {
+  if (B <= 0) return ST_OK;
+  if (!wave || !mel || L <= NFFT / 2 || ld < L) return ST_EINVAL;  // reflect padding needs L > 1024
+  if (!ws || ws_bytes < st_mel_workspace_bytes()) return ST_EWORKSPACE;
+  const long long F = st_mel_frames(L);
+  if (F > 0x7fffffff || B > 65535) return ST_EINVAL;
+  float* tab = static_cast<float*>(ws);
+  hipLaunchKernelGGL(k_mel_tables, dim3((NFFT + NT - 1) / NT), dim3(NT), 0, stream, tab);
+  ST_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_logmel, dim3((unsigned)F, (unsigned)B), dim3(NT), 0, stream, wave, L, ld, (int)F,
+                     (const float*)tab, mel);
+  return (int)hipGetLastError();
+}

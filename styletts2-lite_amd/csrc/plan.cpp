@@ -1261,6 +1261,15 @@ int stts_style_fwd(stts_model* m, int dtype, const float* mel, int B, int T, flo
   return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return style_forward(c, mel, T, out); }, nullptr);
 }
 
+long long stts_mel_frames(long long L) { return st_mel_frames(L); }
+
+long long stts_mel_workspace_bytes(void) { return st_mel_workspace_bytes(); }
+
+int stts_wave_preprocess(const float* wave, int B, long long L, long long wave_ld, float* mel, void* ws,
+                         long long ws_bytes, void* stream) {
+  return st_wave_preprocess(wave, B, L, wave_ld, mel, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
 const char* stts_error_string(int code) {
   switch (code) {
     case 0: return "ok";

@@ -58,6 +58,12 @@ def lib():
     L.stts_f0n_fwd.restype = c_int
     L.stts_style_fwd.argtypes = [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_ll, c_vp]
     L.stts_style_fwd.restype = c_int
+    L.stts_mel_frames.argtypes = [c_ll]
+    L.stts_mel_frames.restype = c_ll
+    L.stts_mel_workspace_bytes.argtypes = []
+    L.stts_mel_workspace_bytes.restype = c_ll
+    L.stts_wave_preprocess.argtypes = [c_vp, c_int, c_ll, c_ll, c_vp, c_vp, c_ll, c_vp]
+    L.stts_wave_preprocess.restype = c_int
     L.stts_error_string.argtypes = [c_int]
     L.stts_error_string.restype = ctypes.c_char_p
     L.stts_profile_enable.argtypes = [c_int]
@@ -285,6 +291,30 @@ class StyleEngine(_Engine):
         check(lib().stts_style_fwd(self.model.h, DTYPES[self.dtype], _ptr(mel), B, T, _ptr(out), _ptr(ws), nb,
                                    _stream()), "stts_style_fwd")
         return out if in_dev.type == "cuda" else out.to(in_dev)
+
+
+N_MELS, MEL_HOP, MEL_NFFT = 80, 300, 2048
+
+
+def wave_preprocess_batch(wave):
+    """HIP log-mel of B equal-length waves: wave [B, L] (any device) -> device [B, 80, 1 + L // 300]
+    (reference inference.py:43-49 per row).  L must exceed 1024, as the reference's reflect
+    padding requires."""
+    _require_device()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    w = _dev_f32(wave, dev)
+    if w.dim() != 2:
+        raise ValueError(f"wave must be [B, L], got {tuple(w.shape)}")
+    B, L = w.shape
+    if L <= MEL_NFFT // 2:
+        raise ValueError(f"wave of {L} samples: the reflect padding of n_fft {MEL_NFFT} needs more than "
+                         f"{MEL_NFFT // 2}")
+    F = int(lib().stts_mel_frames(L))
+    out = torch.empty(B, N_MELS, F, dtype=torch.float32, device=dev)
+    nb = int(lib().stts_mel_workspace_bytes())
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    check(lib().stts_wave_preprocess(_ptr(w), B, L, L, _ptr(out), _ptr(ws), nb, _stream()), "stts_wave_preprocess")
+    return out
 
 
 def profile_enable(on: bool = True):

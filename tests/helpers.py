@@ -51,3 +51,14 @@ def decoder_case(B, T, utt0=0):
     asr, f0, n, s = synth.decoder_inputs(B, T, utt0=utt0)
     noise = synth.source_noise(B, 600 * T, utt0=utt0)
     return [torch.from_numpy(a) for a in (asr, f0, n, s, noise)]
+
+
+def speech_like(name, L, sr=24000):
+    """A reproducible voiced-like clip: a gliding 90-260 Hz fundamental with decaying harmonics,
+    a syllabic envelope and formula noise (the mel front-end's test input)."""
+    t = np.arange(L, dtype=np.float64) / sr
+    f0 = 175 + 85 * np.sin(2 * np.pi * 0.7 * t)
+    ph = 2 * np.pi * np.cumsum(f0) / sr
+    x = sum(0.3 / h * np.sin(h * ph) for h in range(1, 9))
+    env = 0.5 + 0.5 * np.sin(2 * np.pi * 3.1 * t) ** 2
+    return (x * env + 0.01 * synth.normal(name, (L,)).astype(np.float64)).astype(np.float32)
