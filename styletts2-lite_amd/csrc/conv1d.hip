@@ -377,8 +377,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       if (!resident) issue_w(st_tile(1), st_chunk(1), 0, wpB);
     }
   }
+  // always_inline: left to itself the compiler outlines the fp32 instantiations' step into a
+  // called function, which puts the register sets (passed by reference) in scratch memory
   auto step = [&](int st, typename RawT<T>::type (&pre)[MAXU], uint4 (&wpre)[MAXW],
-                  typename RawT<T>::type (&pre2)[MAXU], uint4 (&wpre2)[MAXW]) {
+                  typename RawT<T>::type (&pre2)[MAXU], uint4 (&wpre2)[MAXW]) __attribute__((always_inline)) {
     const int t = st_tile(st), c = st_chunk(st);
     const bool last = c + cps >= p.nchunks;     // the tile's epilogue follows this step
     const bool has2 = cps == 2 && c + 1 < p.nchunks;
@@ -754,10 +756,17 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
   if (p.epi_tanh) return ST_EINVAL;  // tanh only on narrow heads
   if (p.stride > 1) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);  // BM 64 x BN 128 (short window)
   if (p.N <= 32) return launch_cfg<T, MT, 4, 1, 2, 1>(p, stream);     // BM 256 x BN 32, 4 waves
-  // BM 256 x BN 64, 8 waves.  (N = 192 keeps BN 128: the window prologue is paid per tile, so
-  // three 64-column tiles measured slower than a half-empty 128-column one.)
-  if (p.N <= 64) return launch_cfg<T, MT, 8, 1, 1, 2>(p, stream);
-  return launch_cfg<T, MT, 4, 2, 2, 2>(p, stream);                    // BM 256 x BN 128, 8 waves
+  if constexpr (!ConvCfg<T, MT, 1, 1, 1, 1>::BF) {
+    // fp32 (parity mode): 4-wave tiles, so a wave may hold its fp32 windows and weight slices in
+    // up to 512 registers (the 8-wave tiles are capped at 256 and spill)
+    if (p.N <= 64) return launch_cfg<T, MT, 2, 2, 2, 1>(p, stream);   // BM 128 x BN 64
+    return launch_cfg<T, MT, 2, 2, 2, 2>(p, stream);                  // BM 128 x BN 128
+  } else {
+    // BM 256 x BN 64, 8 waves.  (N = 192 keeps BN 128: the window prologue is paid per tile, so
+    // three 64-column tiles measured slower than a half-empty 128-column one.)
+    if (p.N <= 64) return launch_cfg<T, MT, 8, 1, 1, 2>(p, stream);
+    return launch_cfg<T, MT, 4, 2, 2, 2>(p, stream);                  // BM 256 x BN 128, 8 waves
+  }
 }
 
 }  // namespace

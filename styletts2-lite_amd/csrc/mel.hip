@@ -4,12 +4,12 @@
 // periodic Hann window zero-padded to n_fft, center=True with reflect padding, power 2, HTK mel
 // scale, no filter normalisation), then (log(1e-5 + mel) - (-4)) / 4.
 //
-// One workgroup per (utterance, frame): the 1200 windowed samples and a 2048-entry twiddle table
-// sit in LDS, each thread owns four or five DFT bins (the exact integer phase index k*(n+424)
-// mod 2048 picks the twiddle, so no phase error accumulates over the 1200 terms), the power
-// spectrum goes back to LDS and 80 threads apply their triangular filter over its nonzero bin
-// range.  The tables (window, twiddles, filterbank, per-mel bin ranges) are built into the
-// caller's workspace by a setup kernel on every call -- the library allocates nothing.
+// A workgroup walks a few frames of one utterance: the frame's 2048 padded, windowed samples are
+// transformed by a radix-2 FFT in LDS (twiddles from a float64-built table, so the rounding is
+// that of an fp32 FFT, like torch.stft's), the power spectrum goes back to LDS and 80 threads
+// apply their triangular filter over its nonzero bin range.  The tables (window, twiddles,
+// filterbank, per-mel bin ranges) are built into the caller's workspace by a setup kernel on
+// every call -- the library allocates nothing.
 #include "common.h"
 #include "kernels.h"
 
@@ -72,47 +72,64 @@ __global__ void k_mel_tables(float* tab) {
   }
 }
 
+// bit reversal of an 11-bit index
+__device__ __forceinline__ int brev11(int n) { return (int)(__brev((unsigned)n) >> 21); }
+
+// FPB consecutive frames of one utterance per workgroup (the twiddle table is staged once).
+// Per frame: the 2048 padded, windowed samples go to LDS in bit-reversed order, an in-place
+// radix-2 decimation-in-time FFT runs 11 stages (4 butterflies per thread per stage, a barrier
+// between stages), then |X[k]|^2 for k <= 1024 and the 80 triangular filters.
 __global__ void __launch_bounds__(NT) k_logmel(const float* __restrict__ wave, long long L, long long ld, int F,
-                                                const float* __restrict__ tab, float* __restrict__ out) {
-  __shared__ float xs[WIN];
-  __shared__ float cs[NFFT], sn[NFFT];
+                                                int fpb, const float* __restrict__ tab, float* __restrict__ out) {
+  __shared__ float2 a[NFFT];
+  __shared__ float2 tw[NFFT / 2];
   __shared__ float pw[NBIN];
-  const int t = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int b = blockIdx.y, tid = threadIdx.x;
   const float* x = wave + (size_t)b * ld;
-  // frame t reads padded samples [t*HOP + WOFF, +WIN) of the signal reflect-padded by NFFT/2
-  const long long base = (long long)t * HOP + WOFF - NFFT / 2;
-  for (int n = tid; n < WIN; n += NT) {
-    long long j = base + n;
-    if (j < 0) j = -j;
-    if (j >= L) j = 2 * (L - 1) - j;
-    xs[n] = x[j] * tab[T_WIN + n];
-  }
-  for (int j = tid; j < NFFT; j += NT) {
-    cs[j] = tab[T_COS + j];
-    sn[j] = tab[T_SIN + j];
-  }
-  __syncthreads();
-  // bins k = tid + NT*i; X[k] = sum_n xw[n] exp(-2 pi i k (n + WOFF) / NFFT)
-  for (int k = tid; k < NBIN; k += NT) {
-    float re = 0.f, im = 0.f;
-    unsigned idx = (unsigned)(k * WOFF) & (NFFT - 1);
-#pragma unroll 8
-    for (int n = 0; n < WIN; ++n) {
-      const float v = xs[n];
-      re = __builtin_fmaf(v, cs[idx], re);
-      im = __builtin_fmaf(v, sn[idx], im);
-      idx = (idx + (unsigned)k) & (NFFT - 1);
+  for (int j = tid; j < NFFT / 2; j += NT) tw[j] = make_float2(tab[T_COS + j], tab[T_SIN + j]);
+  const int* rng = reinterpret_cast<const int*>(tab + T_RNG);
+  const int t0 = blockIdx.x * fpb, t1 = min(F, t0 + fpb);
+  for (int t = t0; t < t1; ++t) {
+    // frame t = padded samples [t*HOP, t*HOP + NFFT) of the signal reflect-padded by NFFT/2; the
+    // window covers n in [WOFF, WOFF + WIN) of it, zeros elsewhere
+    const long long base = (long long)t * HOP - NFFT / 2;
+    for (int n = tid; n < NFFT; n += NT) {
+      float v = 0.f;
+      if (n >= WOFF && n < WOFF + WIN) {
+        long long j = base + n;
+        if (j < 0) j = -j;
+        if (j >= L) j = 2 * (L - 1) - j;
+        v = x[j] * tab[T_WIN + n - WOFF];
+      }
+      a[brev11(n)] = make_float2(v, 0.f);
     }
-    pw[k] = __builtin_fmaf(re, re, im * im);
-  }
-  __syncthreads();
-  if (tid < NMEL) {
-    const int* rng = reinterpret_cast<const int*>(tab + T_RNG);
-    const int lo = rng[2 * tid], hi = rng[2 * tid + 1];
-    const float* fb = tab + T_FB + (size_t)tid * NBIN;
-    float acc = 0.f;
-    for (int k = lo; k <= hi; ++k) acc = __builtin_fmaf(pw[k], fb[k], acc);
-    out[((size_t)b * NMEL + tid) * F + t] = (logf(1e-5f + acc) + 4.0f) * 0.25f;
+    __syncthreads();
+#pragma unroll 1
+    for (int lg = 0; lg < 11; ++lg) {  // butterflies of span h = 2^lg
+      const int h = 1 << lg;
+      for (int j = tid; j < NFFT / 2; j += NT) {
+        const int pos = j & (h - 1), i0 = ((j >> lg) << (lg + 1)) + pos, i1 = i0 + h;
+        const float2 w = tw[pos << (10 - lg)];  // exp(-2 pi i pos / 2h) = cos - i sin
+        const float2 u = a[i0], v = a[i1];
+        const float tr = w.x * v.x + w.y * v.y, ti = w.x * v.y - w.y * v.x;
+        a[i0] = make_float2(u.x + tr, u.y + ti);
+        a[i1] = make_float2(u.x - tr, u.y - ti);
+      }
+      __syncthreads();
+    }
+    for (int k = tid; k < NBIN; k += NT) {
+      const float2 c = a[k];
+      pw[k] = __builtin_fmaf(c.x, c.x, c.y * c.y);
+    }
+    __syncthreads();
+    if (tid < NMEL) {
+      const int lo = rng[2 * tid], hi = rng[2 * tid + 1];
+      const float* fb = tab + T_FB + (size_t)tid * NBIN;
+      float acc = 0.f;
+      for (int k = lo; k <= hi; ++k) acc = __builtin_fmaf(pw[k], fb[k], acc);
+      out[((size_t)b * NMEL + tid) * F + t] = (logf(1e-5f + acc) + 4.0f) * 0.25f;
+    }
+    // the next frame's loads overwrite a[] only (pw[] is rewritten after two more barriers)
   }
 }
 
@@ -132,7 +149,11 @@ int st_wave_preprocess(const float* wave, int B, long long L, long long ld, floa
   float* tab = static_cast<float*>(ws);
   hipLaunchKernelGGL(k_mel_tables, dim3((NFFT + NT - 1) / NT), dim3(NT), 0, stream, tab);
   ST_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_logmel, dim3((unsigned)F, (unsigned)B), dim3(NT), 0, stream, wave, L, ld, (int)F,
+  // about 2048 workgroups in all, each reusing its staged twiddles over fpb frames
+  const long long want = (long long)B * F / 2048;
+  const int fpb = (int)(want < 1 ? 1 : want > 64 ? 64 : want);
+  const unsigned gx = (unsigned)((F + fpb - 1) / fpb);
+  hipLaunchKernelGGL(k_logmel, dim3(gx, (unsigned)B), dim3(NT), 0, stream, wave, L, ld, (int)F, fpb,
                      (const float*)tab, mel);
   return (int)hipGetLastError();
 }
