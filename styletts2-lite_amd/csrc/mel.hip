@@ -7,9 +7,9 @@
 // A workgroup walks a few frames of one utterance: the frame's 2048 padded, windowed samples are
 // transformed by a radix-2 FFT in LDS (twiddles from a float64-built table, so the rounding is
 // that of an fp32 FFT, like torch.stft's), the power spectrum goes back to LDS and 80 threads
-// apply their triangular filter over its nonzero bin range.  The tables (window, twiddles,
-// filterbank, per-mel bin ranges) are built into the caller's workspace by a setup kernel on
-// every call -- the library allocates nothing.
+// apply their triangular filter (weights recomputed from the band edges) over its bin range.  The
+// window and twiddle tables are built into the caller's workspace by a setup kernel on every
+// call -- the library allocates nothing.
 #include "common.h"
 #include "kernels.h"
 
@@ -23,9 +23,7 @@ constexpr int NT = 256;
 constexpr size_t T_WIN = 0;                      // [WIN]  periodic Hann
 constexpr size_t T_COS = T_WIN + WIN;            // [NFFT] cos(2 pi j / NFFT)
 constexpr size_t T_SIN = T_COS + NFFT;           // [NFFT] sin(2 pi j / NFFT)
-constexpr size_t T_FB = T_SIN + NFFT;            // [NMEL][NBIN] filterbank (mel-major)
-constexpr size_t T_RNG = T_FB + (size_t)NMEL * NBIN;  // [NMEL][2] int: first / last nonzero bin
-constexpr size_t T_END = T_RNG + 2 * NMEL;
+constexpr size_t T_END = T_SIN + NFFT;
 
 // torch.linspace(start, end, steps) in fp32: the first half counts up from start, the second
 // half down from end (aten/src/ATen/native/cpu/RangeFactoriesKernel.cpp)
@@ -35,6 +33,16 @@ __device__ float linspace_f32(float start, float end, int steps, int i) {
   return i < half ? start + step * (float)i : end - step * (float)(steps - i - 1);
 }
 
+// mel band edges f[0..2] of filter m (HTK scale, 82 points linearly spaced in mel)
+__device__ void mel_edges(int m, float (&f)[3]) {
+  const float m_max = 2595.0f * log10f(1.0f + 8000.0f / 700.0f);
+  for (int j = 0; j < 3; ++j) {
+    const float mp = linspace_f32(0.0f, m_max, NMEL + 2, m + j);
+    f[j] = 700.0f * (powf(10.0f, mp / 2595.0f) - 1.0f);
+  }
+}
+
+// one thread per window / twiddle entry
 __global__ void k_mel_tables(float* tab) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < WIN) {  // torch.hann_window(1200, periodic=True) = 0.5 - 0.5 cos(2 pi n / 1200)
@@ -46,30 +54,14 @@ __global__ void k_mel_tables(float* tab) {
     tab[T_COS + i] = (float)c;
     tab[T_SIN + i] = (float)s;
   }
-  if (i < NMEL) {  // torchaudio.functional.melscale_fbanks(1025, 0, 8000, 80, 16000, None, "htk")
-    const int m = i;
-    const float m_max = 2595.0f * log10f(1.0f + 8000.0f / 700.0f);
-    float f[3];
-    for (int j = 0; j < 3; ++j) {
-      const float mp = linspace_f32(0.0f, m_max, NMEL + 2, m + j);
-      f[j] = 700.0f * (powf(10.0f, mp / 2595.0f) - 1.0f);
-    }
-    const float d0 = f[1] - f[0], d1 = f[2] - f[1];
-    int lo = NBIN, hi = -1;
-    for (int k = 0; k < NBIN; ++k) {
-      const float fk = linspace_f32(0.0f, 8000.0f, NBIN, k);
-      const float down = -(f[0] - fk) / d0, up = (f[2] - fk) / d1;
-      const float w = fmaxf(0.0f, fminf(down, up));
-      tab[T_FB + (size_t)m * NBIN + k] = w;
-      if (w > 0.0f) {
-        lo = min(lo, k);
-        hi = k;
-      }
-    }
-    int* rng = reinterpret_cast<int*>(tab + T_RNG);
-    rng[2 * m] = lo;
-    rng[2 * m + 1] = hi;
-  }
+}
+
+// weight of DFT bin k in mel filter m with band edges f[0..2]:
+// torchaudio.functional.melscale_fbanks(1025, 0, 8000, 80, 16000, None, "htk")
+__device__ __forceinline__ float mel_weight(const float* f, int k) {
+  const float fk = linspace_f32(0.0f, 8000.0f, NBIN, k);  // = 7.8125 k exactly
+  const float down = -(f[0] - fk) / (f[1] - f[0]), up = (f[2] - fk) / (f[2] - f[1]);
+  return fmaxf(0.0f, fminf(down, up));
 }
 
 // bit reversal of an 11-bit index
@@ -84,16 +76,18 @@ __global__ void __launch_bounds__(NT) k_logmel(const float* __restrict__ wave, l
   __shared__ float2 a[NFFT];
   __shared__ float2 tw[NFFT / 2];
   __shared__ float pw[NBIN];
+  __shared__ float fe[NMEL][3];
   const int b = blockIdx.y, tid = threadIdx.x;
+  if (tid < NMEL) mel_edges(tid, fe[tid]);
   const float* x = wave + (size_t)b * ld;
   for (int j = tid; j < NFFT / 2; j += NT) tw[j] = make_float2(tab[T_COS + j], tab[T_SIN + j]);
-  const int* rng = reinterpret_cast<const int*>(tab + T_RNG);
   const int t0 = blockIdx.x * fpb, t1 = min(F, t0 + fpb);
   for (int t = t0; t < t1; ++t) {
     // frame t = padded samples [t*HOP, t*HOP + NFFT) of the signal reflect-padded by NFFT/2; the
     // window covers n in [WOFF, WOFF + WIN) of it, zeros elsewhere
     const long long base = (long long)t * HOP - NFFT / 2;
-    for (int n = tid; n < NFFT; n += NT) {
+    for (int m = tid; m < NFFT; m += NT) {  // LDS slot m <- sample brev(m): conflict-free LDS
+      const int n = brev11(m);                // writes, gathered (cached) global reads
       float v = 0.f;
       if (n >= WOFF && n < WOFF + WIN) {
         long long j = base + n;
@@ -101,7 +95,7 @@ __global__ void __launch_bounds__(NT) k_logmel(const float* __restrict__ wave, l
         if (j >= L) j = 2 * (L - 1) - j;
         v = x[j] * tab[T_WIN + n - WOFF];
       }
-      a[brev11(n)] = make_float2(v, 0.f);
+      a[m] = make_float2(v, 0.f);
     }
     __syncthreads();
 #pragma unroll 1
@@ -122,11 +116,11 @@ __global__ void __launch_bounds__(NT) k_logmel(const float* __restrict__ wave, l
       pw[k] = __builtin_fmaf(c.x, c.x, c.y * c.y);
     }
     __syncthreads();
-    if (tid < NMEL) {
-      const int lo = rng[2 * tid], hi = rng[2 * tid + 1];
-      const float* fb = tab + T_FB + (size_t)tid * NBIN;
+    if (tid < NMEL) {  // the weights are recomputed (no table reads): bins strictly inside the band
+      const float* f = fe[tid];
+      const int lo = max(0, (int)floorf(f[0] / 7.8125f) - 1), hi = min(NBIN - 1, (int)ceilf(f[2] / 7.8125f) + 1);
       float acc = 0.f;
-      for (int k = lo; k <= hi; ++k) acc = __builtin_fmaf(pw[k], fb[k], acc);
+      for (int k = lo; k <= hi; ++k) acc = __builtin_fmaf(pw[k], mel_weight(f, k), acc);
       out[((size_t)b * NMEL + tid) * F + t] = (logf(1e-5f + acc) + 4.0f) * 0.25f;
     }
     // the next frame's loads overwrite a[] only (pw[] is rewritten after two more barriers)
