@@ -453,9 +453,13 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       }
     }
     __syncthreads();  // previous readers of Xs (MFMA) are done; coef / bias / W visible
-    write_x(t, c, pre, Xs);
-    if (has2) write_x(t, c + 1, pre2, Xs + xs_el);
-    if (st + PD < nsteps) {
+    // STTS_OPT_DEBUG (timing only, outputs wrong): 1 no window staging, 2 no MFMAs, 4 no
+    // epilogue, 8 no window loads
+    if (!(p.dbg & 1)) {
+      write_x(t, c, pre, Xs);
+      if (has2) write_x(t, c + 1, pre2, Xs + xs_el);
+    }
+    if (st + PD < nsteps && !(p.dbg & 8)) {
       issue(st_tile(st + PD), st_chunk(st + PD), pre);
       if (cps == 2) issue(st_tile(st + 1), st_chunk(st + 1) + 1, pre2);
     }
@@ -481,6 +485,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
         wbase2 = Ws + (size_t)p.tg * W_TAP;
       }
       __syncthreads();
+      if (p.dbg & 2) continue;
       for (int half = 0; half < (has2 ? 2 : 1); ++half) {
       const MT* Xc = half ? Xs + xs_el : Xs;
       const MT* wb = half ? wbase2 : wbase;
@@ -534,7 +539,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       }
       }
     }
-    if (!last) return;
+    if (!last || (p.dbg & 4)) return;
 
     // ---------------- epilogue, straight from registers: lane = (frame, 16 channels) ----------------
     T* yT = reinterpret_cast<T*>(p.y) + (size_t)b * p.y_bs;

@@ -3,7 +3,9 @@ phases skipped through STTS_OPT_DEBUG (1 prologue math, 2 MFMAs, 4 epilogue; big
 8 weight-slice staging, 16 window staging).  Outputs are wrong while a bit is set; only the
 timings mean anything.
 
-    python tools/phase_profile.py [modes, e.g. 0,2,8] [bigconv]
+    python tools/phase_profile.py [modes, e.g. 0,2,8] [bigconv | igemm]
+
+conv1d_igemm (conv1d.hip) bits: 1 window staging, 2 MFMAs, 4 epilogue, 8 window loads.
 """
 import os
 import sys
@@ -40,7 +42,8 @@ def main():
     args = tuple(torch.from_numpy(x).to(dev) for x in synth.decoder_inputs(32, 400))
     eng = dec.engine("bf16")
     modes = [int(m) for m in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2, 4, 3, 6, 7]
-    kernels = ("k_bigconv",) if "bigconv" in sys.argv else ("k_resconv", "k_bigconv")
+    kernels = ("k_bigconv",) if "bigconv" in sys.argv else ("conv1d_igemm_kernel",) if "igemm" in sys.argv \
+        else ("k_resconv", "k_bigconv")
     res = {m: run(eng, args, m) for m in modes}
     print(f"{'i':>3} {'C':>3} {'k':>2} {'d':>1} {'ra':>2} " + " ".join(f"{'dbg' + str(m):>7}" for m in modes))
     tot = {m: 0.0 for m in modes}
