@@ -100,6 +100,53 @@ long long stts_mel_workspace_bytes(void);
 int stts_wave_preprocess(const float* wave, int B, long long L, long long wave_ld, float* mel, void* workspace,
                          long long ws_bytes, void* stream);
 
+/* ---- Duration / text path, fp32, stateless (weights are the
+ * state-dict tensors themselves).  Activations are frames [B][T][C] unless strides say otherwise;
+ * `lengths` is a DEVICE int32 [B] (NULL = every row has length T), the lengths the reference
+ * hands to pack_padded_sequence / length_to_mask. */
+
+/* y[b][t][n] = bias[n] + bias2[n] + sum_{k<K, c<Cin} w[b*ws_b + n*ws_n + c*ws_c + k*ws_k] *
+ *              x[b*xs_b + (t+k-pad)*xs_t + c*xs_c]      (x rows outside [0, Tin) read as 0)
+ * for t < Tout.  Serves  Conv1d  <- models.py:245 (TextEncoder cnn, weight-norm folded),
+ *                        Linear  <- models.py:430 duration_proj (LinearNorm, models.py:152-162),
+ *                        en = d^T @ aln <- models.py:432 / inference.py:266, asr = t_en @ aln <- inference.py:268. */
+int stts_frames_gemm(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int Tin, int Cin,
+                     const float* w, long long ws_b, long long ws_n, long long ws_c, long long ws_k, int N, int K,
+                     int pad, const float* bias, const float* bias2, float* y, long long ys_b, long long ys_t,
+                     long long ys_n, int Tout, void* stream);
+
+/* Bidirectional single-layer nn.LSTM(batch_first=True) with pack_padded_sequence semantics
+ * <- models.py:267-279 (TextEncoder.lstm), :420-430 (ProsodyPredictor.lstm), :449 (shared),
+ *    :510-518 (DurationEncoder.lstms).  x(b, t, c) = x[b*xs_b + t*xs_t + c*xs_c], params = the 8
+ * state-dict tensors {weight_ih_l0, weight_hh_l0, bias_ih_l0, bias_hh_l0, and the *_reverse four},
+ * H = hidden_size (16 | H, H <= 256).  y [B][T][2H] (forward half first, rows t >= len zero);
+ * h_n, c_n [2][B][H] or NULL.  Workspace >= stts_bilstm_workspace_bytes(B, T, H). */
+long long stts_bilstm_workspace_bytes(int B, int T, int H);
+int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
+                    const int* lengths, const float* const* params, int H, float* y, float* h_n, float* c_n,
+                    void* workspace, long long ws_bytes, void* stream);
+
+/* Channel norm of frames rows, fused with LeakyReLU, masking and a style concat:
+ *   mode 0 LayerNorm(gamma[C], beta[C])       <- models.py:229-240 (TextEncoder cnn)
+ *   mode 1 AdaLayerNorm: (1 + gb[b][c]) xhat + gb[b][C + c], gb = gamma, row stride gb_sb
+ *                                             <- models.py:383-392, 503-507 (DurationEncoder)
+ *   mode 2 no norm (copy)                     <- models.py:499-501 (the DurationEncoder input concat)
+ * x(b, t, c) = x[b*xs_b + t*xs_t + c*xs_c];
+ * y[b][t][0..C) = norm (LeakyReLU(slope) if lrelu), y[b][t][C..C+E) = extra[b][..]; rows t >= len = 0. */
+int stts_row_norm(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int C, int mode,
+                  const float* gamma, const float* beta, long long gb_sb, float eps, int lrelu, float slope,
+                  const int* lengths, const float* extra, int E, float* y, long long ys_b, long long ys_t,
+                  void* stream);
+
+/* nn.Embedding + masked_fill_ <- models.py:257-260: tokens int64 [B][T] -> y [B][T][C]; an id outside
+ * [0, n_symbols) writes zeros and sets *err_flag |= 1 (device int, may be NULL). */
+int stts_embedding(const long long* tokens, int B, int T, const float* table, int n_symbols, int C,
+                   const int* lengths, float* y, int* err_flag, void* stream);
+
+/* weight_norm fold w = g * v / ||v|| (norm over all dims but 0) <- torch.nn.utils.weight_norm as used
+ * at models.py:245; v, w [d0][inner], g [d0] (NULL = plain normalisation). */
+int stts_weight_norm(const float* g, const float* v, int d0, int inner, float* w, void* stream);
+
 const char* stts_error_string(int code);
 
 /* Engine options (process-wide, take effect on the next launch):

@@ -399,3 +399,85 @@ def get_style(audio, sd, sr=24000, split_dur=3, prefix=""):
             count += 1
         return ref / count
     return enc(audio)
+
+
+# ----------------------------------------------------------------------------------
+# Duration / text path: TextEncoder, DurationEncoder,
+# ProsodyPredictor.forward.  Stock torch-CPU ops in the reference's op order.
+# ----------------------------------------------------------------------------------
+
+def bilstm(x, sd, p, lengths=None):
+    """nn.LSTM(bidirectional, batch_first) `p` on x [B, T, C]; with `lengths`, the reference's
+    pack_padded_sequence -> LSTM -> pad_packed_sequence -> zero pad to T (models.py:267-285,
+    510-523, 420-430)."""
+    H = _t(sd, p + "weight_hh_l0").shape[1]
+    C = _t(sd, p + "weight_ih_l0").shape[1]
+    lstm = torch.nn.LSTM(C, H, 1, batch_first=True, bidirectional=True)
+    lstm.load_state_dict({k[len(p):]: _t(sd, k) for k in sd if k.startswith(p) and "_l0" in k})
+    with torch.no_grad():
+        if lengths is None:
+            y, _ = lstm(x)
+            return y
+        ln = torch.as_tensor(lengths).cpu()
+        pk = torch.nn.utils.rnn.pack_padded_sequence(x, ln, batch_first=True, enforce_sorted=False)
+        y, _ = lstm(pk)
+        y, _ = torch.nn.utils.rnn.pad_packed_sequence(y, batch_first=True)
+    out = torch.zeros(x.shape[0], x.shape[1], y.shape[-1])
+    out[:, :y.shape[1]] = y
+    return out
+
+
+def length_to_mask(lengths, T=None):
+    """reference models.py:463-466 / inference.py:58-62: True where t >= length."""
+    ln = torch.as_tensor(lengths)
+    T = int(ln.max()) if T is None else T
+    return torch.arange(T).unsqueeze(0).expand(ln.shape[0], -1) + 1 > ln.unsqueeze(1)
+
+
+def text_encoder(tokens, lengths, sd, prefix="", depth=3, slope=0.2):
+    """reference models.py:256-285 (TextEncoder.forward, eval): -> [B, C, T]."""
+    tokens = torch.as_tensor(tokens)
+    m = length_to_mask(lengths, tokens.shape[1]).unsqueeze(1)
+    x = F.embedding(tokens, _t(sd, prefix + "embedding.weight")).transpose(1, 2)
+    x = x.masked_fill(m, 0.0)
+    for i in range(depth):
+        p = f"{prefix}cnn.{i}."
+        w = wn(sd, p + "0")
+        x = F.conv1d(x, w, _t(sd, p + "0.bias"), padding=(w.shape[-1] - 1) // 2)
+        C = x.shape[1]
+        x = F.layer_norm(x.transpose(1, -1), (C,), _t(sd, p + "1.gamma"), _t(sd, p + "1.beta"), 1e-5).transpose(1, -1)
+        x = F.leaky_relu(x, slope)
+        x = x.masked_fill(m, 0.0)
+    x = bilstm(x.transpose(1, 2), sd, prefix + "lstm.", lengths).transpose(1, 2)
+    return x.masked_fill(m, 0.0)
+
+
+def ada_layer_norm(x, s, sd, p, eps=1e-5):
+    """reference models.py:383-392 on x [B, T, C]."""
+    h = F.linear(s, _t(sd, p + "fc.weight"), _t(sd, p + "fc.bias"))
+    C = x.shape[-1]
+    gamma, beta = h[:, :C].unsqueeze(1), h[:, C:].unsqueeze(1)
+    return (1 + gamma) * F.layer_norm(x, (C,), eps=eps) + beta
+
+
+def duration_encoder(x, style, lengths, sd, prefix="", nlayers=3):
+    """reference models.py:497-523 (DurationEncoder.forward, eval): x [B, C, T] -> [B, T, C + sty]."""
+    B, C, T = x.shape
+    m = length_to_mask(lengths, T).unsqueeze(-1)  # [B, T, 1]
+    s = style.unsqueeze(1).expand(B, T, style.shape[-1])
+    h = torch.cat([x.transpose(1, 2), s], -1).masked_fill(m, 0.0)
+    for i in range(nlayers):
+        h = bilstm(h, sd, f"{prefix}lstms.{2 * i}.", lengths)
+        h = ada_layer_norm(h, style, sd, f"{prefix}lstms.{2 * i + 1}.")
+        h = torch.cat([h, s], -1).masked_fill(m, 0.0)
+    return h
+
+
+def predictor_forward(texts, style, lengths, alignment, sd, prefix=""):
+    """reference models.py:417-446 (ProsodyPredictor.forward, eval) -> (duration, en)."""
+    d = duration_encoder(texts, style, lengths, sd, prefix + "text_encoder.")
+    x = bilstm(d, sd, prefix + "lstm.", lengths)
+    duration = F.linear(x, _t(sd, prefix + "duration_proj.linear_layer.weight"),
+                        _t(sd, prefix + "duration_proj.linear_layer.bias"))
+    en = d.transpose(-1, -2) @ alignment
+    return duration.squeeze(-1), en

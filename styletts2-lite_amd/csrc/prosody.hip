@@ -1,0 +1,324 @@
+// Duration / text path of StyleTTS2-lite on gfx950, fp32.
+//
+// Reference computations replaced (thewh1teagle/StyleTTS2-lite @ 2025-06-14):
+//   * nn.LSTM(bidirectional, batch_first) + pack_padded_sequence / pad_packed_sequence:
+//       TextEncoder.lstm            models.py:267-279
+//       DurationEncoder.lstms[2i]   models.py:510-518
+//       ProsodyPredictor.lstm       models.py:420-430, inference.py:246
+//       ProsodyPredictor.shared     models.py:449
+//   * TextEncoder CNN  (weight-norm Conv1d k5 -> LayerNorm(gamma, beta) -> LeakyReLU 0.2 -> mask)
+//                                   models.py:243-262
+//   * AdaLayerNorm + style concat + mask (DurationEncoder)  models.py:372-392, 503-507
+//   * embedding + mask (TextEncoder) models.py:257-260; duration_proj (LinearNorm) models.py:430;
+//     the alignment products en = d^T @ aln / asr = t_en @ aln   models.py:432, inference.py:266-269
+//
+// All activations are "frames" [B][T][C] (channel fastest), the layout the reference's
+// batch_first LSTMs use.  Everything here is latency-bound at text lengths (T <= a few
+// hundred tokens): the kernels aim at few launches and no host round trips, not at MFMA.
+#include "common.h"
+#include "stts2.h"
+
+// ---------------------------------------------------------------------------------------
+// Strided batched "frames GEMM": a 1-D convolution over the T axis as an implicit GEMM
+//   y[b][t][n] = bias[n] + bias2[n] + sum_{k<K} sum_{c<Cin} w(b, n, c, k) * x(b, t + k - pad, c)
+// with every operand addressed by explicit strides, so one kernel serves Conv1d (K taps),
+// Linear / LSTM input projections (K = 1) and batched matrix products (w strided per batch).
+// 64 x 64 output tile per 256-thread workgroup, 4 x 4 per lane, K staged through LDS in 16s.
+// ---------------------------------------------------------------------------------------
+struct GemmArgs {
+  const float* x;
+  long long xs_b, xs_t, xs_c;
+  int Tin, Cin;
+  const float* w;
+  long long ws_b, ws_n, ws_c, ws_k;
+  int N, K, pad;
+  const float* bias;
+  const float* bias2;
+  float* y;
+  long long ys_b, ys_t, ys_n;
+  int Tout;
+};
+
+__global__ void __launch_bounds__(256) k_frames_gemm(GemmArgs a) {
+  __shared__ float As[16][68];  // [k][t]
+  __shared__ float Bs[16][68];  // [k][n]
+  const int b = blockIdx.z, t0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int Ktot = a.Cin * a.K;
+  const float* xb = a.x + (size_t)b * a.xs_b;
+  const float* wb = a.w + (size_t)b * a.ws_b;
+  float acc[4][4] = {};
+  for (int kk = 0; kk < Ktot; kk += 16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + e * 256, kl = idx & 15, rl = idx >> 4;
+      const int kg = kk + kl;
+      float va = 0.f, vb = 0.f;
+      if (kg < Ktot) {
+        const int tap = kg / a.Cin, c = kg - tap * a.Cin;
+        const int t = t0 + rl, ti = t + tap - a.pad;
+        if (t < a.Tout && ti >= 0 && ti < a.Tin) va = xb[(size_t)ti * a.xs_t + (size_t)c * a.xs_c];
+        const int n = n0 + rl;
+        if (n < a.N) vb = wb[(size_t)n * a.ws_n + (size_t)c * a.ws_c + (size_t)tap * a.ws_k];
+      }
+      As[kl][rl] = va;
+      Bs[kl][rl] = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float4 av = *reinterpret_cast<const float4*>(&As[k][ty * 4]);
+      const float4 bv = *reinterpret_cast<const float4*>(&Bs[k][tx * 4]);
+      const float ar[4] = {av.x, av.y, av.z, av.w}, br[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(ar[i], br[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + tx * 4 + j;
+    if (n >= a.N) continue;
+    const float bs = (a.bias ? a.bias[n] : 0.f) + (a.bias2 ? a.bias2[n] : 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + ty * 4 + i;
+      if (t < a.Tout) a.y[(size_t)b * a.ys_b + (size_t)t * a.ys_t + (size_t)n * a.ys_n] = acc[i][j] + bs;
+    }
+  }
+}
+
+static int launch_gemm(const GemmArgs& a, int B, hipStream_t s) {
+  if (B <= 0 || a.Tout <= 0 || a.N <= 0) return 0;
+  if (a.Cin <= 0 || a.K <= 0 || !a.x || !a.w || !a.y) return ST_EINVAL;
+  dim3 grid((a.Tout + 63) / 64, (a.N + 63) / 64, B);
+  hipLaunchKernelGGL(k_frames_gemm, grid, dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// BiLSTM recurrence (torch gate order i, f, g, o; c' = f c + i g; h' = o tanh(c')).
+// G = x W_ih^T + b_ih + b_hh for every (direction, utterance, step) comes precomputed from
+// k_frames_gemm.  One workgroup per (utterance, direction) with 4H lanes: lane j owns gate
+// row j and streams column j of W_hh^T (coalesced over j, L2-resident across steps) against
+// h_{t-1} broadcast from LDS.  pack_padded_sequence semantics: the forward direction runs
+// t = 0 .. len-1, the reverse t = len-1 .. 0, both from zero state; rows t >= len are 0.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+__global__ void __launch_bounds__(1024) k_bilstm_rec(const float* __restrict__ G, const float* __restrict__ WT,
+                                                     const int* __restrict__ lengths, int B, int T, int H,
+                                                     float* __restrict__ y, float* __restrict__ hn,
+                                                     float* __restrict__ cn) {
+  __shared__ float hs[256];
+  __shared__ float gs[1024];
+  const int b = blockIdx.x, d = blockIdx.y, j = threadIdx.x, H4 = 4 * H;
+  int len = lengths ? lengths[b] : T;
+  len = len < 0 ? 0 : (len > T ? T : len);
+  float* yb = y + (size_t)b * T * 2 * H + (size_t)d * H;
+  if (j < H) {
+    for (int t = len; t < T; ++t) yb[(size_t)t * 2 * H + j] = 0.f;
+    hs[j] = 0.f;
+  }
+  float c = 0.f, h = 0.f;
+  __syncthreads();
+  const float* W = WT + (size_t)d * H * H4 + j;
+  const float* g = G + ((size_t)d * B + b) * T * H4 + j;
+  for (int s = 0; s < len; ++s) {
+    const int t = d == 0 ? s : len - 1 - s;
+    float a0 = g[(size_t)t * H4], a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int k = 0; k < H; k += 4) {
+      const float4 hv = *reinterpret_cast<const float4*>(&hs[k]);
+      a0 = fmaf(W[(size_t)(k + 0) * H4], hv.x, a0);
+      a1 = fmaf(W[(size_t)(k + 1) * H4], hv.y, a1);
+      a2 = fmaf(W[(size_t)(k + 2) * H4], hv.z, a2);
+      a3 = fmaf(W[(size_t)(k + 3) * H4], hv.w, a3);
+    }
+    gs[j] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (j < H) {
+      const float ig = sigm(gs[j]), fg = sigm(gs[H + j]), gg = tanhf(gs[2 * H + j]), og = sigm(gs[3 * H + j]);
+      c = fg * c + ig * gg;
+      h = og * tanhf(c);
+      hs[j] = h;
+      yb[(size_t)t * 2 * H + j] = h;
+    }
+    __syncthreads();
+  }
+  if (j < H) {
+    if (hn) hn[((size_t)d * B + b) * H + j] = h;
+    if (cn) cn[((size_t)d * B + b) * H + j] = c;
+  }
+}
+
+// W_hh [4H][H] (torch) -> WT [H][4H], both directions.
+__global__ void k_lstm_wt(const float* __restrict__ w0, const float* __restrict__ w1, int H, float* __restrict__ wt) {
+  const int H4 = 4 * H;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)2 * H * H4) return;
+  const int d = (int)(i / ((size_t)H * H4));
+  const int r = (int)(i % ((size_t)H * H4));
+  const int k = r / H4, jj = r % H4;
+  const float* w = d ? w1 : w0;
+  wt[i] = w[(size_t)jj * H + k];
+}
+
+// ---------------------------------------------------------------------------------------
+// Row norm over channels of frames rows, fused with what follows it in the reference:
+//   mode 0 (LayerNorm, models.py:229-240):  v = xhat * gamma[c] + beta[c]
+//   mode 1 (AdaLayerNorm, models.py:383-392): v = (1 + gb[b][c]) * xhat + gb[b][C + c]
+//   mode 2 (no norm, the input concat of models.py:499-501): v = x
+// then optional LeakyReLU(slope), then the row is zeroed for t >= len (masked_fill_), and
+// `extra` [B][E] (the style vector) is appended as channels C .. C+E (the concat of
+// models.py:505).  xhat = (x - mean) / sqrt(biased var + eps).  One wave64 per row.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_row_norm(const float* __restrict__ x, long long xs_b, long long xs_t,
+                                                  long long xs_c, int B,
+                                                  int T, int C, int mode, const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, long long gb_sb, float eps,
+                                                  int lrelu, float slope, const int* __restrict__ lengths,
+                                                  const float* __restrict__ extra, int E, float* __restrict__ y,
+                                                  long long ys_b, long long ys_t) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long long)B * T) return;
+  const int b = (int)(row / T), t = (int)(row % T);
+  const bool valid = !lengths || t < lengths[b];
+  float* yr = y + (size_t)b * ys_b + (size_t)t * ys_t;
+  if (!valid) {
+    for (int c = lane; c < C + E; c += 64) yr[c] = 0.f;
+    return;
+  }
+  const float* xr = x + (size_t)b * xs_b + (size_t)t * xs_t;
+  if (mode == 2) {
+    for (int c = lane; c < C; c += 64) yr[c] = xr[(size_t)c * xs_c];
+    for (int e = lane; e < E; e += 64) yr[C + e] = extra[(size_t)b * E + e];
+    return;
+  }
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += xr[(size_t)c * xs_c];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / (float)C;
+  float v2 = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float dlt = xr[(size_t)c * xs_c] - mean;
+    v2 += dlt * dlt;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v2 += __shfl_xor(v2, o);
+  const float rstd = 1.0f / sqrtf(v2 / (float)C + eps);
+  for (int c = lane; c < C; c += 64) {
+    const float xh = (xr[(size_t)c * xs_c] - mean) * rstd;
+    float v;
+    if (mode == 0) {
+      v = xh * gamma[c] + beta[c];
+    } else {
+      const float* gb = gamma + (size_t)b * gb_sb;
+      v = (1.0f + gb[c]) * xh + gb[C + c];
+    }
+    if (lrelu) v = v > 0.f ? v : v * slope;
+    yr[c] = v;
+  }
+  for (int e = lane; e < E; e += 64) yr[C + e] = extra[(size_t)b * E + e];
+}
+
+// Embedding gather + mask: y[b][t][:] = table[tokens[b][t]][:] for t < len, else 0.
+__global__ void __launch_bounds__(256) k_embedding(const long long* __restrict__ tok, int B, int T,
+                                                   const float* __restrict__ table, int n_symbols, int C,
+                                                   const int* __restrict__ lengths, float* __restrict__ y,
+                                                   int* __restrict__ err) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= (long long)B * T) return;
+  const int b = (int)(row / T), t = (int)(row % T);
+  const long long id = tok[row];
+  const bool valid = (!lengths || t < lengths[b]);
+  const bool in_range = id >= 0 && id < n_symbols;
+  if (!in_range && lane == 0 && err) atomicOr(err, 1);
+  float* yr = y + (size_t)row * C;
+  for (int c = lane; c < C; c += 64) yr[c] = (valid && in_range) ? table[(size_t)id * C + c] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------------------
+extern "C" {
+
+int stts_frames_gemm(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int Tin, int Cin,
+                     const float* w, long long ws_b, long long ws_n, long long ws_c, long long ws_k, int N, int K,
+                     int pad, const float* bias, const float* bias2, float* y, long long ys_b, long long ys_t,
+                     long long ys_n, int Tout, void* stream) {
+  if (B < 0 || Tin < 0 || Tout < 0 || Cin < 0 || N < 0 || K <= 0 || pad < 0) return ST_EINVAL;
+  GemmArgs a{x, xs_b, xs_t, xs_c, Tin, Cin, w, ws_b, ws_n, ws_c, ws_k, N, K, pad, bias, bias2, y, ys_b, ys_t, ys_n, Tout};
+  return launch_gemm(a, B, (hipStream_t)stream);
+}
+
+long long stts_bilstm_workspace_bytes(int B, int T, int H) {
+  if (B < 0 || T < 0 || H <= 0) return -1;
+  return ((long long)2 * B * T * 4 * H + (long long)2 * H * 4 * H) * (long long)sizeof(float);
+}
+
+int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
+                    const int* lengths, const float* const* params, int H, float* y, float* h_n, float* c_n,
+                    void* workspace, long long ws_bytes, void* stream) {
+  if (B < 0 || T < 0 || Cin <= 0 || !params || !y) return ST_EINVAL;
+  if (H <= 0 || H > 256 || (H & 15)) return ST_EINVAL;  // 4H lanes per workgroup, float4 LDS reads
+  for (int i = 0; i < 8; ++i)
+    if (!params[i]) return ST_EPARAMS;
+  if (ws_bytes < stts_bilstm_workspace_bytes(B, T, H)) return ST_EWORKSPACE;
+  if (B == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  float* G = (float*)workspace;
+  float* WT = G + (size_t)2 * B * T * 4 * H;
+  const int H4 = 4 * H;
+  {
+    const size_t n = (size_t)2 * H * H4;
+    hipLaunchKernelGGL(k_lstm_wt, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, params[1], params[5], H, WT);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  if (T > 0) {
+    for (int d = 0; d < 2; ++d) {
+      const float* const* p = params + 4 * d;
+      GemmArgs a{x, xs_b, xs_t, xs_c, T, Cin, p[0], 0, Cin, 1, 0, H4, 1, 0, p[2], p[3],
+                 G + (size_t)d * B * T * H4, (long long)T * H4, H4, 1, T};
+      ST_CHECK(launch_gemm(a, B, s));
+    }
+  }
+  hipLaunchKernelGGL(k_bilstm_rec, dim3(B, 2), dim3(H4), 0, s, G, WT, lengths, B, T, H, y, h_n, c_n);
+  return (int)hipGetLastError();
+}
+
+int stts_row_norm(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int C, int mode,
+                  const float* gamma, const float* beta, long long gb_sb, float eps, int lrelu, float slope,
+                  const int* lengths, const float* extra, int E, float* y, long long ys_b, long long ys_t,
+                  void* stream) {
+  if (B < 0 || T < 0 || C <= 0 || E < 0 || (E > 0 && !extra) || !x || !y) return ST_EINVAL;
+  if (mode < 0 || mode > 2 || (mode != 2 && !gamma) || (mode == 0 && !beta)) return ST_EINVAL;
+  const long long rows = (long long)B * T;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(k_row_norm, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, xs_b, xs_t,
+                     xs_c, B, T, C, mode, gamma, beta, gb_sb, eps, lrelu, slope, lengths, extra, E, y, ys_b, ys_t);
+  return (int)hipGetLastError();
+}
+
+int stts_embedding(const long long* tokens, int B, int T, const float* table, int n_symbols, int C,
+                   const int* lengths, float* y, int* err_flag, void* stream) {
+  if (B < 0 || T < 0 || C <= 0 || n_symbols <= 0 || !tokens || !table || !y) return ST_EINVAL;
+  const long long rows = (long long)B * T;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(k_embedding, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, tokens, B, T,
+                     table, n_symbols, C, lengths, y, err_flag);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"
+
+int st_wn_fold(const float* v, const float* g, int d0, int inner, float* wout, hipStream_t s);
+
+extern "C" int stts_weight_norm(const float* g, const float* v, int d0, int inner, float* w, void* stream) {
+  if (d0 <= 0 || inner <= 0 || !v || !w) return ST_EINVAL;
+  return st_wn_fold(v, g, d0, inner, w, (hipStream_t)stream);
+}

@@ -4,9 +4,11 @@ Same constructor signatures and state-dict keys as the reference
 (ProsodyPredictor models.py:394-466, StyleEncoder models.py:125-150), so checkpoints
 load unchanged (reference inference.py:120-122, 158-168).
 
-* `ProsodyPredictor.F0Ntrain(en, s)` (models.py:448-461): the shared BiLSTM stays on
-  PyTorch/MIOpen, the F0 / N AdainResBlk1d conv stacks and the
-  1x1 projections run as HIP kernels through the C-ABI.
+* `ProsodyPredictor.F0Ntrain(en, s)` (models.py:448-461): the shared BiLSTM (HIP recurrence,
+  prosody.py), the F0 / N AdainResBlk1d conv stacks and the 1x1 projections run as HIP kernels
+  through the C-ABI.
+* `ProsodyPredictor.forward(texts, style, text_lengths, alignment, m)` (models.py:417-446) and
+  `TextEncoder` (models.py:241-295): the duration path, prosody.py.
 * `StyleEncoder.forward(mel)` (models.py:145-150): the whole 2-D ResNet runs as HIP kernels.
 """
 from __future__ import annotations
@@ -15,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from .params import AdainResBlk1d, Conv1d, Conv2d, Linear
+from .prosody import LSTM, AdaLayerNorm, DurationEncoder, TextEncoder, linear_frames, matmul  # noqa: F401
 
 
 class LinearNorm(nn.Module):
@@ -28,29 +31,6 @@ class LinearNorm(nn.Module):
         return self.linear_layer(x)
 
 
-class AdaLayerNorm(nn.Module):
-    """reference models.py:372-392 parameter layout (fc)."""
-
-    def __init__(self, style_dim, channels, eps=1e-5):
-        super().__init__()
-        self.channels, self.eps = channels, eps
-        self.fc = nn.Linear(style_dim, channels * 2)
-
-
-class DurationEncoder(nn.Module):
-    """reference models.py:468-533 parameter layout (lstms = [LSTM, AdaLayerNorm] x nlayers).
-    Out of the hot-path scope; parameters only."""
-
-    def __init__(self, sty_dim, d_model, nlayers, dropout=0.1):
-        super().__init__()
-        self.lstms = nn.ModuleList()
-        for _ in range(nlayers):
-            self.lstms.append(nn.LSTM(d_model + sty_dim, d_model // 2, num_layers=1, batch_first=True,
-                                      bidirectional=True))
-            self.lstms.append(AdaLayerNorm(sty_dim, d_model))
-        self.dropout, self.d_model, self.sty_dim = dropout, d_model, sty_dim
-
-
 class ProsodyPredictor(nn.Module):
     """reference models.py:394-466."""
 
@@ -58,9 +38,9 @@ class ProsodyPredictor(nn.Module):
         super().__init__()
         self.style_dim, self.d_hid = int(style_dim), int(d_hid)
         self.text_encoder = DurationEncoder(sty_dim=style_dim, d_model=d_hid, nlayers=nlayers, dropout=dropout)
-        self.lstm = nn.LSTM(d_hid + style_dim, d_hid // 2, 1, batch_first=True, bidirectional=True)
+        self.lstm = LSTM(d_hid + style_dim, d_hid // 2, 1, batch_first=True, bidirectional=True)
         self.duration_proj = LinearNorm(d_hid, max_dur)
-        self.shared = nn.LSTM(d_hid + style_dim, d_hid // 2, 1, batch_first=True, bidirectional=True)
+        self.shared = LSTM(d_hid + style_dim, d_hid // 2, 1, batch_first=True, bidirectional=True)
         self.F0 = nn.ModuleList([
             AdainResBlk1d(d_hid, d_hid, style_dim, dropout_p=dropout),
             AdainResBlk1d(d_hid, d_hid // 2, style_dim, upsample=True, dropout_p=dropout),
@@ -79,12 +59,27 @@ class ProsodyPredictor(nn.Module):
             self._engine = F0NEngine(self, dtype=dtype)
         return self._engine
 
+    def forward(self, texts, style, text_lengths, alignment, m=None):
+        """reference models.py:417-446: texts = TextEncoder output [B, d_hid, T], style [B, style_dim],
+        alignment [B, T, F] -> (duration logits [B, T, max_dur], en [B, d_hid + style_dim, F])."""
+        dev = self.F0_proj.weight.device
+        texts, style, alignment = (t.to(dev, torch.float32) for t in (texts, style, alignment))
+        with torch.no_grad():
+            d = self.text_encoder(texts, style, text_lengths, m)  # [B, T, d_hid + style_dim]
+            x, _ = self.lstm(d, lengths=text_lengths)  # pack -> LSTM -> pad (models.py:421-430)
+            lin = self.duration_proj.linear_layer
+            duration = linear_frames(x, lin.weight.detach(), lin.bias.detach())  # dropout: eval identity
+            en = matmul(d.transpose(-1, -2), alignment)
+        return duration.squeeze(-1), en
+
     def F0Ntrain(self, x, s, dtype="fp32"):
         """x = en [B, d_hid+style_dim, T], s [B, style_dim] -> (F0 [B,2T], N [B,2T])."""
+        dev = self.F0_proj.weight.device
+        in_dev = x.device
         with torch.no_grad():
-            self.shared.flatten_parameters() if x.is_cuda else None
-            h, _ = self.shared(x.transpose(-1, -2))  # [B, T, d_hid] == NLC, consumed as-is
-        return self.f0n_engine(dtype).forward_nlc(h.contiguous(), s)
+            h, _ = self.shared(x.to(dev, torch.float32).transpose(-1, -2))  # [B, T, d_hid] frames, HIP BiLSTM
+        F0, N = self.f0n_engine(dtype).forward_nlc(h, s)
+        return (F0, N) if in_dev.type == "cuda" else (F0.to(in_dev), N.to(in_dev))
 
 
 class LearnedDownSample(nn.Module):

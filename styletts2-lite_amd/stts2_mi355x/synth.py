@@ -96,6 +96,8 @@ def synth_param(key: str, shape) -> np.ndarray:
         return uniform(key, shape, -1.0, 1.0) * np.float32(1.0 / np.sqrt(hidden))
     if "bias_ih" in key or "bias_hh" in key:
         return uniform(key, shape, -0.1, 0.1)
+    if key.endswith("embedding.weight"):  # nn.Embedding default init N(0, 1)
+        return normal(key, shape)
     if key.endswith(".weight") and len(shape) >= 2:  # plain conv / linear (no weight norm)
         fan_in = int(np.prod(shape[1:]))
         gain = 1.0

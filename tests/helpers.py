@@ -62,3 +62,34 @@ def speech_like(name, L, sr=24000):
     x = sum(0.3 / h * np.sin(h * ph) for h in range(1, 9))
     env = 0.5 + 0.5 * np.sin(2 * np.pi * 3.1 * t) ** 2
     return (x * env + 0.01 * synth.normal(name, (L,)).astype(np.float64)).astype(np.float32)
+
+
+DURATION_CASES = ((24, (24, 19, 13)), (60, (60,)))  # (T tokens, lengths per utterance)
+
+
+def duration_inputs(T, lengths):
+    """Duration-path case (tests/golden/make_golden_duration.py): tokens [B,T] int64 (0 past the
+    length), lengths [B], style [B,128], alignment [B,T,F] (1-4 frames per token, 0 past the length)."""
+    B = len(lengths)
+    tok = np.zeros((B, T), np.int64)
+    dur = np.zeros((B, T), np.int64)
+    for b, n in enumerate(lengths):
+        tok[b, :n] = (synth.hash_u01(f"dur:tok:{b}:{T}", n) * 178).astype(np.int64)
+        dur[b, :n] = 1 + (synth.hash_u01(f"dur:dur:{b}:{T}", n) * 4).astype(np.int64)
+    F = int(dur.sum(1).max())
+    aln = np.zeros((B, T, F), np.float32)
+    for b in range(B):
+        c = 0
+        for t in range(T):
+            aln[b, t, c:c + dur[b, t]] = 1.0
+            c += dur[b, t]
+    s = np.stack([synth.normal(f"dur:s:{b}", (128,)) for b in range(B)]).astype(np.float32)
+    return tok, np.asarray(lengths, np.int64), s, aln
+
+
+def make_duration_modules():
+    """Drop-in TextEncoder + ProsodyPredictor with the fixtures' formula weights (prefixes te. / pp.)."""
+    from stts2_mi355x.models import ProsodyPredictor, TextEncoder
+    te = fill_module(TextEncoder(channels=512, kernel_size=5, depth=3, n_symbols=178), "te.").eval()
+    pp = fill_module(ProsodyPredictor(style_dim=128, d_hid=512, nlayers=3, max_dur=50, dropout=0.2), "pp.").eval()
+    return te, pp

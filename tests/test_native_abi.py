@@ -115,3 +115,36 @@ def test_style_plan_names_match_state_dict():
     assert L.stts_workspace_bytes(h, 0, 1, 241) > 0
     assert L.stts_workspace_bytes(h, 0, 1, 48) < 0  # 5x5 valid conv needs T >= 65 (reference raises too)
     L.stts_model_destroy(h)
+
+
+def test_duration_path_argument_checks():
+    """The duration-path entry points validate shapes before touching the device (include/stts2.h)."""
+    from stts2_mi355x import prosody
+    L = prosody._L()
+    assert L.stts_bilstm_workspace_bytes(2, 10, 256) == (2 * 2 * 10 * 1024 + 2 * 256 * 1024) * 4
+    params = (ctypes.c_void_p * 8)(*([1] * 8))
+    # H must be a multiple of 16 and <= 256
+    assert L.stts_bilstm_fwd(1, 0, 0, 0, 1, 4, 8, None, params, 300, 1, None, None, 1, 1 << 30, None) == -1
+    assert L.stts_bilstm_fwd(1, 0, 0, 0, 1, 4, 8, None, params, 24, 1, None, None, 1, 1 << 30, None) == -1
+    # workspace too small
+    assert L.stts_bilstm_fwd(1, 0, 0, 0, 1, 4, 8, None, params, 32, 1, None, None, 1, 16, None) == -4
+    assert L.stts_row_norm(1, 0, 0, 0, 1, 1, 8, 3, 1, 1, 0, 1e-5, 0, 0.0, None, None, 0, 1, 0, 0, None) == -1
+    assert L.stts_frames_gemm(1, 0, 0, 0, 1, 1, 1, 1, 0, 0, 0, 0, 1, 0, 0, None, None, 1, 0, 0, 0, 1, None) == -1
+
+
+def test_duration_modules_keep_reference_keys():
+    """TextEncoder / ProsodyPredictor expose the reference's state-dict names (models.py:241-466)."""
+    from stts2_mi355x.models import ProsodyPredictor, TextEncoder
+    te = TextEncoder(channels=512, kernel_size=5, depth=3, n_symbols=178)
+    keys = set(te.state_dict())
+    for k in ("embedding.weight", "cnn.2.0.weight_g", "cnn.2.0.weight_v", "cnn.2.0.bias", "cnn.2.1.gamma",
+              "cnn.2.1.beta", "lstm.weight_hh_l0_reverse", "lstm.bias_ih_l0"):
+        assert k in keys, k
+    assert len(keys) == 1 + 3 * 5 + 8
+    pp = ProsodyPredictor(style_dim=128, d_hid=512, nlayers=3, max_dur=50, dropout=0.2)
+    pk = set(pp.state_dict())
+    for k in ("text_encoder.lstms.0.weight_ih_l0", "text_encoder.lstms.5.fc.weight", "lstm.bias_hh_l0_reverse",
+              "duration_proj.linear_layer.weight", "shared.weight_hh_l0"):
+        assert k in pk, k
+    with pytest.raises(RuntimeError):
+        te(torch.zeros(1, 4, dtype=torch.long), torch.tensor([4]))
