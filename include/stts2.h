@@ -143,6 +143,25 @@ int stts_row_norm(const float* x, long long xs_b, long long xs_t, long long xs_c
 int stts_embedding(const long long* tokens, int B, int T, const float* table, int n_symbols, int C,
                    const int* lengths, float* y, int* err_flag, void* stream);
 
+/* Durations -> integer frame counts <- inference.py:247-258 (StyleTTS2.__inference): per utterance
+ * (its first lengths[b] <= T <= 1024 tokens), dur = sum_k sigmoid(logits[t][k]) over K logits
+ * (logits(b, t, k) = logits[b*ls_b + t*ls_t + k]); stats = (prev_mean != 0 ? prev_mean : mean(dur)) +
+ * std(dur) * z[b][t] (z = the standard-normal draw of :249-252, NULL = 0); dur = dur (1 - mix) + stats mix;
+ * z-score outlier clamp of dur[1:-2] (threshold 3, factor 0.95, :134-148); dur /= speed;
+ * pred = max(round_half_even(dur), 1).  Outputs dur [B][T], pred int32 [B][T] (0 past the length),
+ * total int32 [B] = sum pred (the alignment width), dur_mean [B] (may be NULL) = the `duration.mean()`
+ * the reference returns. */
+int stts_durations(const float* logits, long long ls_b, long long ls_t, int B, int T, int K, const int* lengths,
+                   const float* z, float mix, float prev_mean, float speed, float* dur, int* pred, int* total,
+                   float* dur_mean, void* stream);
+
+/* The alignment products of inference.py:259-268 / models.py:432 without the one-hot matrix: with
+ * aln[b][t][f] = 1 for the pred[b][t] frames of token t (tokens in order, pred from stts_durations),
+ * y[b][c][f] = sum_t src(b, t, c) aln[b][t][f] = src(b, token of f, c) exactly, 0 past the utterance's
+ * total.  src(b, t, c) = src[b*ss_b + t*ss_t + c*ss_c]; y [B][C][Fmax]; frame_tok int32 [B][Fmax] scratch. */
+int stts_expand_frames(const float* src, long long ss_b, long long ss_t, long long ss_c, int B, int T, int C,
+                       const int* pred, int Fmax, int* frame_tok, float* y, void* stream);
+
 /* weight_norm fold w = g * v / ||v|| (norm over all dims but 0) <- torch.nn.utils.weight_norm as used
  * at models.py:245; v, w [d0][inner], g [d0] (NULL = plain normalisation). */
 int stts_weight_norm(const float* g, const float* v, int d0, int inner, float* w, void* stream);

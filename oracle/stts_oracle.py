@@ -481,3 +481,57 @@ def predictor_forward(texts, style, lengths, alignment, sd, prefix=""):
                         _t(sd, prefix + "duration_proj.linear_layer.bias"))
     en = d.transpose(-1, -2) @ alignment
     return duration.squeeze(-1), en
+
+
+def replace_outliers_zscore(x, threshold=3.0, factor=0.95):
+    """reference inference.py:134-148."""
+    mean, std = x.mean(), x.std()
+    z = (x - mean) / std
+    mask = torch.abs(z) > threshold
+    rep = mean + torch.sign(x - mean) * (threshold * std * factor)
+    out = x.clone()
+    out[mask] = rep[mask]
+    return out
+
+
+def durations(logits, z, mix=0.1, prev_mean=0.0, speed=1.0):
+    """reference inference.py:247-258 for one utterance: logits [1, T, max_dur], z [1, T] = the
+    standard-normal draw of dur_stats (normal_(mean, std) = mean + std * z) -> (duration, pred_dur)."""
+    speed = min(max(speed, 0.0001), 2)
+    duration = torch.sigmoid(logits).sum(axis=-1)
+    mu = prev_mean if prev_mean != 0 else duration.mean()
+    dur_stats = mu + duration.std() * z
+    duration = duration * (1 - mix) + dur_stats * mix
+    duration[:, 1:-2] = replace_outliers_zscore(duration[:, 1:-2])
+    duration = duration / speed
+    pred_dur = torch.round(duration.squeeze()).clamp(min=1)
+    return duration, pred_dur
+
+
+def alignment_matrix(pred_dur):
+    """reference inference.py:259-263."""
+    aln = torch.zeros(pred_dur.shape[0], int(pred_dur.sum()))
+    c = 0
+    for i in range(aln.shape[0]):
+        aln[i, c:c + int(pred_dur[i])] = 1
+        c += int(pred_dur[i])
+    return aln.unsqueeze(0)
+
+
+def inference_chain(tokens, s, te_sd, pp_sd, dec_sd, dec_cfg, z, noise_fn, mix=0.1, prev_mean=0.0, speed=1.0):
+    """reference inference.py:225-272 (StyleTTS2.__inference) from the cleaner's token ids on, with the
+    HiFi-GAN decoder: -> (audio [600 F], duration.mean(), pred_dur).  noise_fn(F) -> [1, 600F, 9]."""
+    ids = [0] + [int(i) for i in tokens] + [0]
+    tok = torch.tensor(ids).unsqueeze(0)
+    ln = torch.tensor([len(ids)])
+    t_en = text_encoder(tok, ln, te_sd)
+    d = duration_encoder(t_en, s, ln, pp_sd, "text_encoder.")
+    x = bilstm(d, pp_sd, "lstm.")
+    logits = F.linear(x, _t(pp_sd, "duration_proj.linear_layer.weight"), _t(pp_sd, "duration_proj.linear_layer.bias"))
+    duration, pred = durations(logits, z, mix, prev_mean, speed)
+    aln = alignment_matrix(pred)
+    en = d.transpose(-1, -2) @ aln
+    F0, N = f0ntrain(en, s, pp_sd)
+    asr = t_en @ aln
+    out = decoder_hifigan(asr, F0, N, s, dec_sd, dec_cfg, noise_fn(aln.shape[-1]))
+    return out.squeeze(), duration.mean(), pred

@@ -243,6 +243,139 @@ __global__ void __launch_bounds__(256) k_embedding(const long long* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------
+// Durations -> frame map (reference inference.py:247-263, StyleTTS2.__inference), one workgroup
+// per utterance over its first len tokens:
+//   dur   = sum_k sigmoid(logits[t][k])                                   (:247)
+//   stats = (prev_mean != 0 ? prev_mean : mean(dur)) + std(dur) * z[t]    (:249-252, std unbiased)
+//   dur   = dur * (1 - mix) + stats * mix                                 (:253)
+//   dur[1:-2] = z-score outlier clamp (threshold 3, factor 0.95)          (:254, :134-148)
+//   dur  /= speed; pred = max(round_half_even(dur), 1)                    (:256-258)
+// and the frame -> token map of the alignment matrix (:259-263): frame_tok[b][f] = t for the
+// pred[t] frames of token t, -1 past the utterance's total.  Sums are fixed-order tree reductions.
+// ---------------------------------------------------------------------------------------
+#define DUR_MAX_T 1024
+
+__device__ float block_sum_1024(float v, float* red) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  const float r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(1024) k_durations(const float* __restrict__ logits, long long ls_b, long long ls_t,
+                                                    int T, int K, const int* __restrict__ lengths,
+                                                    const float* __restrict__ z, float mix, float prev_mean,
+                                                    float speed, float* __restrict__ dur_out,
+                                                    int* __restrict__ pred, int* __restrict__ total,
+                                                    float* __restrict__ dur_mean) {
+  __shared__ float red[1024];
+  __shared__ int cum[DUR_MAX_T];
+  const int b = blockIdx.x, t = threadIdx.x;
+  int len = lengths ? lengths[b] : T;
+  len = len < 0 ? 0 : (len > T ? T : len);
+  const bool on = t < len;
+  float d = 0.f;
+  if (on) {
+    const float* lr = logits + (size_t)b * ls_b + (size_t)t * ls_t;
+    for (int k = 0; k < K; ++k) d += 1.0f / (1.0f + expf(-lr[k]));
+  }
+  // mean / unbiased std over the utterance's tokens (duration.mean(), duration.std())
+  const float n = (float)len;
+  float mean = block_sum_1024(on ? d : 0.f, red) / n;
+  float dv = on ? (d - mean) : 0.f;
+  float sd = sqrtf(block_sum_1024(dv * dv, red) / (n - 1.0f));
+  {
+    const float mu = prev_mean != 0.f ? prev_mean : mean;
+    const float st = mu + sd * (z && on ? z[(size_t)b * T + t] : 0.f);
+    if (on) d = d * (1.0f - mix) + st * mix;
+  }
+  // outliers over the slice [1, len-2)
+  const int lo = 1, hi = len - 2;
+  const bool in_sl = t >= lo && t < hi;
+  const float ns = (float)(hi - lo);
+  if (hi - lo > 0) {
+    const float m2 = block_sum_1024(in_sl ? d : 0.f, red) / ns;
+    const float dd = in_sl ? d - m2 : 0.f;
+    const float s2 = sqrtf(block_sum_1024(dd * dd, red) / (ns - 1.0f));
+    if (in_sl) {
+      const float zz = (d - m2) / s2;
+      if (fabsf(zz) > 3.0f) {
+        const float sg = d > m2 ? 1.0f : (d < m2 ? -1.0f : 0.0f);
+        d = m2 + sg * (3.0f * s2 * 0.95f);
+      }
+    }
+  }
+  d = d / speed;
+  int p = 0;
+  if (on) {
+    p = (int)rintf(d);
+    p = p < 1 ? 1 : p;
+  }
+  const float mfin = block_sum_1024(on ? d : 0.f, red) / n;
+  if (on) {
+    dur_out[(size_t)b * T + t] = d;
+    pred[(size_t)b * T + t] = p;
+  } else if (t < T) {
+    dur_out[(size_t)b * T + t] = 0.f;
+    pred[(size_t)b * T + t] = 0;
+  }
+  // inclusive scan of pred over tokens (Hillis-Steele in LDS)
+  if (t < DUR_MAX_T) cum[t] = p;
+  __syncthreads();
+  for (int off = 1; off < DUR_MAX_T; off <<= 1) {
+    const int v = (t < DUR_MAX_T && t >= off) ? cum[t - off] : 0;
+    __syncthreads();
+    if (t < DUR_MAX_T) cum[t] += v;
+    __syncthreads();
+  }
+  if (t == 0) {
+    total[b] = len > 0 ? cum[len - 1] : 0;
+    if (dur_mean) dur_mean[b] = mfin;
+  }
+}
+
+// frame_tok[b][f] for f < Fmax: the token whose run covers frame f (pred from k_durations), -1 past
+// the utterance's total.  One workgroup per utterance; each token writes its own run.
+__global__ void __launch_bounds__(1024) k_frame_map(const int* __restrict__ pred, int T, int Fmax,
+                                                    int* __restrict__ frame_tok) {
+  __shared__ int cum[DUR_MAX_T];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int p = t < T ? pred[(size_t)b * T + t] : 0;
+  cum[t] = p;
+  __syncthreads();
+  for (int off = 1; off < DUR_MAX_T; off <<= 1) {
+    const int v = t >= off ? cum[t - off] : 0;
+    __syncthreads();
+    cum[t] += v;
+    __syncthreads();
+  }
+  const int end = cum[t], start = end - p;
+  int* fr = frame_tok + (size_t)b * Fmax;
+  for (int f = start; f < end && f < Fmax; ++f) fr[f] = t;
+  const int tot = cum[DUR_MAX_T - 1];
+  for (int f = tot + t; f < Fmax; f += DUR_MAX_T) fr[f] = -1;
+}
+
+// Alignment product as a gather (exact: a one-hot column picks one token):
+//   y[b][c][f] = src(b, frame_tok[b][f], c), 0 where frame_tok = -1
+// = (t_en @ aln)[b][c][f] (inference.py:268) or (d^T @ aln)[b][c][f] (models.py:432, inference.py:266).
+__global__ void __launch_bounds__(256) k_expand_frames(const float* __restrict__ src, long long ss_b, long long ss_t,
+                                                       long long ss_c, int C, const int* __restrict__ frame_tok,
+                                                       int Fmax, float* __restrict__ y) {
+  const int b = blockIdx.z, c = blockIdx.y;
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= Fmax) return;
+  const int t = frame_tok[(size_t)b * Fmax + f];
+  y[((size_t)b * C + c) * Fmax + f] = t < 0 ? 0.f : src[(size_t)b * ss_b + (size_t)t * ss_t + (size_t)c * ss_c];
+}
+
+// ---------------------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------------------
 extern "C" {
@@ -311,6 +444,29 @@ int stts_embedding(const long long* tokens, int B, int T, const float* table, in
   if (rows == 0) return 0;
   hipLaunchKernelGGL(k_embedding, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, tokens, B, T,
                      table, n_symbols, C, lengths, y, err_flag);
+  return (int)hipGetLastError();
+}
+
+int stts_durations(const float* logits, long long ls_b, long long ls_t, int B, int T, int K, const int* lengths,
+                   const float* z, float mix, float prev_mean, float speed, float* dur, int* pred, int* total,
+                   float* dur_mean, void* stream) {
+  if (B < 0 || T < 0 || T > DUR_MAX_T || K <= 0 || !logits || !dur || !pred || !total || !(speed > 0.f))
+    return ST_EINVAL;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(k_durations, dim3(B), dim3(1024), 0, (hipStream_t)stream, logits, ls_b, ls_t, T, K, lengths, z,
+                     mix, prev_mean, speed, dur, pred, total, dur_mean);
+  return (int)hipGetLastError();
+}
+
+int stts_expand_frames(const float* src, long long ss_b, long long ss_t, long long ss_c, int B, int T, int C,
+                       const int* pred, int Fmax, int* frame_tok, float* y, void* stream) {
+  if (B < 0 || T < 0 || T > DUR_MAX_T || C <= 0 || Fmax < 0 || !src || !pred || !frame_tok || !y) return ST_EINVAL;
+  if (B == 0 || Fmax == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_frame_map, dim3(B), dim3(DUR_MAX_T), 0, s, pred, T, Fmax, frame_tok);
+  ST_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_expand_frames, dim3((Fmax + 255) / 256, C, B), dim3(256), 0, s, src, ss_b, ss_t, ss_c, C,
+                     frame_tok, Fmax, y);
   return (int)hipGetLastError();
 }
 

@@ -3,9 +3,13 @@
 (inference.py:195-217), with the log-mel computed by the HIP kernel behind
 `stts_wave_preprocess` (include/stts2.h) and the style by the HIP StyleEncoder.
 
+`Synthesizer.inference` is StyleTTS2.__inference (inference.py:219-272) from the token ids on:
+text encoder, duration path, durations -> alignment, F0Ntrain and the decoder, all on the HIP
+device with one host read (the alignment width, as the reference's `int(pred_dur.sum())`).
+
 Out of scope here: text normalisation and phonemisation, audio loading
 (librosa) and the optional noisereduce denoise step -- `get_style` takes the loaded, already
-denoised waveform.
+denoised waveform, `Synthesizer.inference` the token ids of `TextCleaner`.
 """
 from __future__ import annotations
 
@@ -13,6 +17,7 @@ import numpy as np
 import torch
 
 from .engine import wave_preprocess_batch
+from .prosody import durations, expand_frames, linear_frames
 
 
 class Preprocess:
@@ -59,3 +64,49 @@ def get_style(style_encoder, audio, sr=24000, split_dur=3, dtype="fp32"):
             count += 1
         return ref / count
     return enc([audio])
+
+
+class Synthesizer:
+    """The model half of reference inference.py StyleTTS2 (:64-272) over drop-in modules:
+    text_encoder (models.TextEncoder), predictor (models.ProsodyPredictor), decoder
+    (hifigan / istftnet Decoder), all on the HIP device."""
+
+    def __init__(self, text_encoder, predictor, decoder, decoder_dtype="fp32"):
+        self.text_encoder, self.predictor, self.decoder = text_encoder, predictor, decoder
+        self.decoder_dtype = decoder_dtype
+
+    def alignment(self, tokens, ref_s, speed=1, prev_d_mean=0, t=0.1, z=None):
+        """inference.py:225-263: token ids (TextCleaner output, without the 0 pads) -> intermediate
+        tensors {t_en [1,C,T], d [1,T,C+S], logits, dur, pred [1,T], frames F, dur_mean}.
+        `z` [T] = the standard-normal draw behind dur_stats (:249-252); None draws it on the device."""
+        dev = self.predictor.F0_proj.weight.device
+        speed = min(max(speed, 0.0001), 2)
+        ids = [0] + [int(i) for i in tokens] + [0]  # tokens.insert(0, 0); tokens.append(0)  (:228-229)
+        tok = torch.tensor(ids, dtype=torch.int64, device=dev).unsqueeze(0)
+        T = tok.shape[1]
+        s = torch.as_tensor(ref_s).to(dev, torch.float32).reshape(1, -1)
+        with torch.no_grad():
+            t_en = self.text_encoder(tok, None)
+            d = self.predictor.text_encoder(t_en, s, None)
+            x, _ = self.predictor.lstm(d)
+            lin = self.predictor.duration_proj.linear_layer
+            logits = linear_frames(x, lin.weight.detach(), lin.bias.detach())
+            if z is None:
+                z = torch.randn(1, T, device=dev)
+            z = torch.as_tensor(z).to(dev, torch.float32).reshape(1, T)
+            dur, pred, total, dmean = durations(logits, None, z, mix=t, prev_mean=prev_d_mean, speed=speed)
+        return {"t_en": t_en, "d": d, "s": s, "logits": logits, "dur": dur, "pred": pred,
+                "frames": int(total[0].item()), "dur_mean": dmean[0]}
+
+    def inference(self, tokens, ref_s, speed=1, prev_d_mean=0, t=0.1, z=None, noise=None, seed=0):
+        """-> (audio [600 F] float32 on the device, duration.mean()) as inference.py:272 returns
+        (the reference moves the audio to a numpy array)."""
+        a = self.alignment(tokens, ref_s, speed, prev_d_mean, t, z)
+        F, s = a["frames"], a["s"]
+        with torch.no_grad():
+            en = expand_frames(a["d"], a["pred"], F)  # d^T @ aln          (:266)
+            F0, N = self.predictor.F0Ntrain(en, s)  # (:267)
+            t_en = a["t_en"]
+            asr = expand_frames(t_en.transpose(1, 2), a["pred"], F)  # t_en @ aln  (:268)
+            out = self.decoder(asr, F0, N, s, noise=noise, seed=seed, dtype=self.decoder_dtype)
+        return out.squeeze(), a["dur_mean"]

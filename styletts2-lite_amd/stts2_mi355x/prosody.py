@@ -46,6 +46,11 @@ def _L():
         L.stts_embedding.restype = c_int
         L.stts_weight_norm.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]
         L.stts_weight_norm.restype = c_int
+        L.stts_durations.argtypes = [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_float, c_float, c_float,
+                                     c_vp, c_vp, c_vp, c_vp, c_vp]
+        L.stts_durations.restype = c_int
+        L.stts_expand_frames.argtypes = [c_vp, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp]
+        L.stts_expand_frames.restype = c_int
         _BOUND = True
     return L
 
@@ -114,6 +119,40 @@ def weight_norm_fold(g: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
     d0 = v.shape[0]
     check(_L().stts_weight_norm(_ptr(g), _ptr(v), d0, v.numel() // d0, _ptr(w), _stream()), "stts_weight_norm")
     return w
+
+
+def durations(logits, lengths=None, z=None, mix=0.0, prev_mean=0.0, speed=1.0):
+    """stts_durations (inference.py:247-258): logits [B, T, K] (last axis contiguous) ->
+    (dur [B,T] float32, pred [B,T] int32, total [B] int32, dur_mean [B] float32)."""
+    _on_device(logits, "durations")
+    B, T, K = logits.shape
+    if logits.stride(2) != 1:
+        logits = logits.contiguous()
+    dev = logits.device
+    ln = _lengths(lengths, B, T, dev)
+    if z is not None:
+        z = _on_device(z.reshape(B, T).contiguous(), "durations z")
+    dur = torch.empty(B, T, dtype=torch.float32, device=dev)
+    pred = torch.empty(B, T, dtype=torch.int32, device=dev)
+    total = torch.empty(B, dtype=torch.int32, device=dev)
+    dmean = torch.empty(B, dtype=torch.float32, device=dev)
+    check(_L().stts_durations(_ptr(logits), logits.stride(0), logits.stride(1), B, T, K, _ptr(ln), _ptr(z),
+                              float(mix), float(prev_mean), float(speed), _ptr(dur), _ptr(pred), _ptr(total),
+                              _ptr(dmean), _stream()), "stts_durations")
+    return dur, pred, total, dmean
+
+
+def expand_frames(src_btc: torch.Tensor, pred: torch.Tensor, Fmax: int) -> torch.Tensor:
+    """stts_expand_frames: src viewed as (b, t, c) (any strides) -> [B, C, Fmax] = src^T @ aln, the
+    one-hot alignment of `pred` frames per token (inference.py:259-268) applied as an exact gather."""
+    _on_device(src_btc, "expand_frames")
+    B, T, C = src_btc.shape
+    pred = pred.to(torch.int32).contiguous()
+    y = torch.empty(B, C, Fmax, dtype=torch.float32, device=src_btc.device)
+    ftok = torch.empty(B, max(Fmax, 1), dtype=torch.int32, device=src_btc.device)
+    check(_L().stts_expand_frames(_ptr(src_btc), *src_btc.stride(), B, T, C, _ptr(pred), Fmax, _ptr(ftok), _ptr(y),
+                                  _stream()), "stts_expand_frames")
+    return y
 
 
 class LSTM(nn.LSTM):

@@ -39,3 +39,24 @@ def test_padding_rows_are_zero():
     g = golden("duration_T24_B3")
     for b, n in enumerate(g["lengths"]):
         assert np.all(g["t_en"][b, :, n:] == 0) and np.all(g["d"][b, n:] == 0)
+
+
+def test_oracle_durations_known_answers():
+    """inference.py:134-148, 247-258 restated; known answers (inference.py cannot be imported here: it
+    downloads nltk data at import, SURVEY §8(c), so this step is pinned by hand-computed cases)."""
+    x = torch.tensor([[1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 40.0, 1.0]])
+    out = orc.replace_outliers_zscore(x)
+    mean, std = x.mean(), x.std()
+    assert abs(float(out[0, 12]) - float(mean + 3 * std * 0.95)) < 1e-5
+    assert torch.equal(out[0, :12], x[0, :12])
+    # logits of +-inf-like magnitude: sigmoid sums are exact integers
+    logits = torch.full((1, 6, 50), -30.0)
+    logits[0, :, :3] = 30.0  # 3 frames per token
+    dur, pred = orc.durations(logits, torch.zeros(1, 6), mix=0.0, speed=1.0)
+    assert torch.equal(pred, torch.full((6,), 3.0))
+    dur, pred = orc.durations(logits, torch.zeros(1, 6), mix=0.0, speed=2.0)  # 1.5 rounds half to even
+    assert torch.equal(pred, torch.full((6,), 2.0))
+    dur, pred = orc.durations(torch.full((1, 6, 50), -30.0), torch.zeros(1, 6), mix=0.0)
+    assert torch.equal(pred, torch.ones(6))  # clamp(min=1)
+    aln = orc.alignment_matrix(torch.tensor([2.0, 1.0, 3.0]))
+    assert aln.shape == (1, 3, 6) and aln.sum() == 6 and aln[0, 2, 3:].sum() == 3

@@ -142,3 +142,62 @@ def test_cpu_tensors_refused(mods):
     with pytest.raises(RuntimeError):
         pp.lstm.cpu()(torch.randn(1, 4, 640))
     pp.lstm.cuda()
+
+
+@pytest.mark.parametrize("mix,prev,speed", [(0.0, 0.0, 1.0), (0.1, 0.0, 1.0), (0.3, 2.5, 0.8), (0.1, 0.0, 1.7)])
+def test_durations_vs_oracle(mix, prev, speed):
+    from stts2_mi355x.prosody import durations
+    torch.manual_seed(int(mix * 100 + speed * 10))
+    T = 57
+    logits = torch.randn(1, T, 50) * 2.0
+    logits[0, 20] += 25.0  # a long token -> exercises the z-score outlier clamp
+    z = torch.randn(1, T)
+    want_dur, want_pred = orc.durations(logits.clone(), z, mix, prev, speed)
+    dur, pred, total, dmean = durations(logits.cuda(), None, z.cuda(), mix, prev, speed)
+    assert _err(dur, want_dur.numpy()) < 1e-4
+    assert torch.equal(pred.cpu().reshape(-1).float(), want_pred)
+    assert int(total[0]) == int(want_pred.sum())
+    assert abs(float(dmean[0]) - float(want_dur.mean())) < 1e-4
+
+
+def test_expand_frames_is_the_alignment_product():
+    from stts2_mi355x.prosody import expand_frames
+    torch.manual_seed(9)
+    pred = torch.tensor([[2, 1, 4, 1, 3], [1, 1, 2, 0, 0]], dtype=torch.int32)
+    F = 11
+    src = torch.randn(2, 5, 7)  # (b, t, c)
+    aln = torch.zeros(2, 5, F)
+    for b in range(2):
+        c = 0
+        for t in range(5):
+            aln[b, t, c:c + int(pred[b, t])] = 1
+            c += int(pred[b, t])
+    want = src.transpose(1, 2) @ aln
+    got = expand_frames(src.cuda(), pred.cuda(), F)
+    assert torch.equal(got.cpu(), want)
+    got = expand_frames(src.transpose(1, 2).contiguous().cuda().transpose(1, 2), pred.cuda(), F)  # strided
+    assert torch.equal(got.cpu(), want)
+
+
+def test_synthesizer_chain_vs_oracle(mods):
+    """inference.py:225-272 from the token ids to the waveform: HIP chain vs the oracle chain, fp32."""
+    from helpers import make_decoder
+    from stts2_mi355x.inference import Synthesizer
+    te, pp = mods
+    dec, cfg = make_decoder("hifigan")
+    tokens = [int(v) for v in (synth.hash_u01("chain:tok", 22) * 177 + 1)]
+    s = torch.from_numpy(synth.normal("chain:s", (1, 128)))
+    z = torch.from_numpy(synth.normal("chain:z", (1, len(tokens) + 2)))
+    noise_fn = lambda F: torch.from_numpy(synth.source_noise(1, 600 * F, tag="chain"))  # noqa: E731
+    cpu = lambda m: {k: v.cpu() for k, v in m.state_dict().items()}  # noqa: E731
+    want, want_mean, want_pred = orc.inference_chain(tokens, s, cpu(te), cpu(pp),
+                                                     {k: v.cpu() for k, v in dec.state_dict().items()}, cfg, z,
+                                                     noise_fn, mix=0.1)
+    syn = Synthesizer(te, pp, dec.cuda())
+    a = syn.alignment(tokens, s.cuda(), t=0.1, z=z.cuda())
+    assert torch.equal(a["pred"].cpu().reshape(-1).float(), want_pred)
+    F = a["frames"]
+    out, dmean = syn.inference(tokens, s.cuda(), t=0.1, z=z.cuda(), noise=noise_fn(F).cuda())
+    assert out.shape[-1] == 600 * F == want.shape[-1]
+    assert _err(out, want.numpy()) < 1e-3  # north-star waveform tolerance
+    assert abs(float(dmean) - float(want_mean)) < 1e-4
