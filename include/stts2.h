@@ -119,9 +119,13 @@ int stts_frames_gemm(const float* x, long long xs_b, long long xs_t, long long x
  * <- models.py:267-279 (TextEncoder.lstm), :420-430 (ProsodyPredictor.lstm), :449 (shared),
  *    :510-518 (DurationEncoder.lstms).  x(b, t, c) = x[b*xs_b + t*xs_t + c*xs_c], params = the 8
  * state-dict tensors {weight_ih_l0, weight_hh_l0, bias_ih_l0, bias_hh_l0, and the *_reverse four},
- * H = hidden_size (16 | H, H <= 256).  y [B][T][2H] (forward half first, rows t >= len zero);
+ * H = hidden_size (32 | H, H <= 256).  y [B][T][2H] (forward half first, rows t >= len zero);
  * h_n, c_n [2][B][H] or NULL.  Workspace >= stts_bilstm_workspace_bytes(B, T, H). */
 long long stts_bilstm_workspace_bytes(int B, int T, int H);
+/* Recurrence kernel choice: 0 = automatic (default: the cooperative kernel, W_hh split over 8 workgroups,
+ * for H = 256 and B <= 4, else one workgroup per utterance and direction), -1 = cooperative whenever
+ * H = 256, 1 / 2 / 4 = utterances per workgroup of the per-workgroup kernel (A/B testing). */
+int stts_set_lstm_group(int bg);
 int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
                     const int* lengths, const float* const* params, int H, float* y, float* h_n, float* c_n,
                     void* workspace, long long ws_bytes, void* stream);

@@ -106,61 +106,252 @@ static int launch_gemm(const GemmArgs& a, int B, hipStream_t s) {
 // h_{t-1} broadcast from LDS.  pack_padded_sequence semantics: the forward direction runs
 // t = 0 .. len-1, the reverse t = len-1 .. 0, both from zero state; rows t >= len are 0.
 // ---------------------------------------------------------------------------------------
+static int g_lstm_bg = 0;  // 0 = automatic, -1 = cooperative, 1/2/4 = per-workgroup (stts_set_lstm_group)
+
 __device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v)); }
 
-__global__ void __launch_bounds__(1024) k_bilstm_rec(const float* __restrict__ G, const float* __restrict__ WT,
+// BG utterances of one direction per workgroup: every W_hh element loaded from L2 feeds BG FMAs.
+// Each step is a chain the workgroup cannot overlap with the next, so its cost is the latency of
+// streaming the lane's 4H x H / 4H = H recurrent weights: W_hh is stored k-quad interleaved
+// (WT4[q][j] = W_hh[j][4q .. 4q+3], one float4 per lane, 1 KB coalesced per wave) and streamed in
+// chunks of 4 float4 with the next chunk in flight while the current one is consumed (measured:
+// one dword per lane per load and a 4-deep loop spent ~8 us a step on L2 round trips).
+// h_{t-1} sits in LDS as [q][BG][4] so one ds_read_b128 broadcasts 4 k of one utterance.
+template <int BG>
+__global__ void __launch_bounds__(1024) k_bilstm_rec(const float* __restrict__ G, const float4* __restrict__ WT4,
                                                      const int* __restrict__ lengths, int B, int T, int H,
                                                      float* __restrict__ y, float* __restrict__ hn,
                                                      float* __restrict__ cn) {
-  __shared__ float hs[256];
-  __shared__ float gs[1024];
-  const int b = blockIdx.x, d = blockIdx.y, j = threadIdx.x, H4 = 4 * H;
-  int len = lengths ? lengths[b] : T;
-  len = len < 0 ? 0 : (len > T ? T : len);
-  float* yb = y + (size_t)b * T * 2 * H + (size_t)d * H;
-  if (j < H) {
-    for (int t = len; t < T; ++t) yb[(size_t)t * 2 * H + j] = 0.f;
-    hs[j] = 0.f;
-  }
-  float c = 0.f, h = 0.f;
-  __syncthreads();
-  const float* W = WT + (size_t)d * H * H4 + j;
-  const float* g = G + ((size_t)d * B + b) * T * H4 + j;
-  for (int s = 0; s < len; ++s) {
-    const int t = d == 0 ? s : len - 1 - s;
-    float a0 = g[(size_t)t * H4], a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int k = 0; k < H; k += 4) {
-      const float4 hv = *reinterpret_cast<const float4*>(&hs[k]);
-      a0 = fmaf(W[(size_t)(k + 0) * H4], hv.x, a0);
-      a1 = fmaf(W[(size_t)(k + 1) * H4], hv.y, a1);
-      a2 = fmaf(W[(size_t)(k + 2) * H4], hv.z, a2);
-      a3 = fmaf(W[(size_t)(k + 3) * H4], hv.w, a3);
+  __shared__ float4 hs4[64 * BG];
+  __shared__ float gs[BG][1024];
+  float* hs = reinterpret_cast<float*>(hs4);
+  const int b0 = blockIdx.x * BG, d = blockIdx.y, j = threadIdx.x, H4 = 4 * H;
+  const int nch = H >> 4;  // chunks of 4 k-quads
+  int len[BG], maxlen = 0;
+#pragma unroll
+  for (int i = 0; i < BG; ++i) {
+    int l = 0;
+    if (b0 + i < B) {
+      l = lengths ? lengths[b0 + i] : T;
+      l = l < 0 ? 0 : (l > T ? T : l);
     }
-    gs[j] = (a0 + a1) + (a2 + a3);
+    len[i] = l;
+    maxlen = l > maxlen ? l : maxlen;
+  }
+  if (j < H) {
+#pragma unroll
+    for (int i = 0; i < BG; ++i) {
+      hs[((j >> 2) * BG + i) * 4 + (j & 3)] = 0.f;
+      if (b0 + i >= B) continue;
+      float* yb = y + (size_t)(b0 + i) * T * 2 * H + (size_t)d * H;
+      for (int t = len[i]; t < T; ++t) yb[(size_t)t * 2 * H + j] = 0.f;
+    }
+  }
+  float c[BG], h[BG];
+#pragma unroll
+  for (int i = 0; i < BG; ++i) c[i] = h[i] = 0.f;
+  __syncthreads();
+  const float4* W = WT4 + (size_t)d * (H >> 2) * H4 + j;
+  for (int s = 0; s < maxlen; ++s) {
+    float acc[BG][4];
+#pragma unroll
+    for (int i = 0; i < BG; ++i) {
+      const int t = d == 0 ? s : len[i] - 1 - s;
+      acc[i][0] = s < len[i] ? G[(((size_t)d * B + b0 + i) * T + t) * H4 + j] : 0.f;
+      acc[i][1] = acc[i][2] = acc[i][3] = 0.f;
+    }
+    auto consume = [&](const float4 (&w)[4], int ch) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = ch * 4 + u;
+#pragma unroll
+        for (int i = 0; i < BG; ++i) {
+          const float4 hv = hs4[q * BG + i];
+          acc[i][0] = fmaf(w[u].x, hv.x, acc[i][0]);
+          acc[i][1] = fmaf(w[u].y, hv.y, acc[i][1]);
+          acc[i][2] = fmaf(w[u].z, hv.z, acc[i][2]);
+          acc[i][3] = fmaf(w[u].w, hv.w, acc[i][3]);
+        }
+      }
+    };
+    float4 wa[4], wb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wa[u] = W[(size_t)u * H4];
+#pragma unroll 1
+    for (int ch = 0; ch < nch; ch += 2) {
+      if (ch + 1 < nch) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wb[u] = W[(size_t)((ch + 1) * 4 + u) * H4];
+      }
+      consume(wa, ch);
+      if (ch + 1 < nch) {
+        if (ch + 2 < nch) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) wa[u] = W[(size_t)((ch + 2) * 4 + u) * H4];
+        }
+        consume(wb, ch + 1);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BG; ++i) gs[i][j] = (acc[i][0] + acc[i][1]) + (acc[i][2] + acc[i][3]);
     __syncthreads();
     if (j < H) {
-      const float ig = sigm(gs[j]), fg = sigm(gs[H + j]), gg = tanhf(gs[2 * H + j]), og = sigm(gs[3 * H + j]);
-      c = fg * c + ig * gg;
-      h = og * tanhf(c);
-      hs[j] = h;
-      yb[(size_t)t * 2 * H + j] = h;
+#pragma unroll
+      for (int i = 0; i < BG; ++i) {
+        if (s >= len[i]) continue;
+        const int t = d == 0 ? s : len[i] - 1 - s;
+        const float ig = sigm(gs[i][j]), fg = sigm(gs[i][H + j]), gg = tanhf(gs[i][2 * H + j]);
+        const float og = sigm(gs[i][3 * H + j]);
+        c[i] = fg * c[i] + ig * gg;
+        h[i] = og * tanhf(c[i]);
+        hs[((j >> 2) * BG + i) * 4 + (j & 3)] = h[i];
+        y[((size_t)(b0 + i) * T + t) * 2 * H + (size_t)d * H + j] = h[i];
+      }
     }
     __syncthreads();
   }
   if (j < H) {
-    if (hn) hn[((size_t)d * B + b) * H + j] = h;
-    if (cn) cn[((size_t)d * B + b) * H + j] = c;
+#pragma unroll
+    for (int i = 0; i < BG; ++i) {
+      if (b0 + i >= B) continue;
+      if (hn) hn[((size_t)d * B + b0 + i) * H + j] = h[i];
+      if (cn) cn[((size_t)d * B + b0 + i) * H + j] = c[i];
+    }
   }
 }
 
-// W_hh [4H][H] (torch) -> WT [H][4H], both directions.
+// ---------------------------------------------------------------------------------------
+// Cooperative recurrence for H = 256 (the reference's every LSTM): the per-step floor of
+// k_bilstm_rec is one CU streaming the whole 1 MB W_hh through its 64 B/clk L1 (~7 us a step).
+// Here a direction's W_hh is split over COOP_NW = 8 workgroups, each holding the 4 gate rows of
+// 32 hidden units resident in LDS (128 rows x 256, padded rows: 133 KB), so a step reads no weights
+// from L2 at all.  Per step each workgroup computes its 128 gate rows (512 lanes: row = lane / 4,
+// a quarter of k per lane, shuffle-reduced), updates its 32 (c, h), publishes h to an exchange
+// buffer (double-buffered by step parity) and meets the other 7 at an arrival counter (agent-scope
+// atomics).  Groups = (direction, utterance slot) run persistently over the utterances; the launch
+// is cooperative (co-residency guaranteed or the launch fails -> k_bilstm_rec), and every spin is
+// bounded (a timed-out wait sets *err and the outputs are poisoned with NaN, never a hang).
+// ---------------------------------------------------------------------------------------
+#define COOP_H 256
+#define COOP_NW 8
+#define COOP_U (COOP_H / COOP_NW)  // hidden units per workgroup (32)
+#define COOP_ROWS (4 * COOP_U)     // gate rows per workgroup (128)
+#define COOP_LD 260                // padded LDS row stride (floats)
+#define COOP_SPIN_LIMIT (1u << 22)
+
+struct CoopArgs {
+  const float* G;     // [2][B][T][4H] input projections (+ both biases)
+  const float* whh0;  // W_hh forward  [4H][H] (torch layout)
+  const float* whh1;  // W_hh reverse
+  const int* lengths;
+  int B, T, groups;   // groups: even, group g -> direction g & 1, utterances g>>1, g>>1 + groups/2, ...
+  float* y;           // [B][T][2H]
+  float* hn;
+  float* cn;
+  float* xh;          // exchange [groups][2][H]
+  unsigned* counter;  // [groups], zeroed before launch
+  int* err;
+};
+
+__global__ void __launch_bounds__(512) k_bilstm_coop(CoopArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Ws = lds;                           // [COOP_ROWS][COOP_LD]
+  float* hb = lds + COOP_ROWS * COOP_LD;     // [H]
+  float* gl = hb + COOP_H;                   // [COOP_ROWS]
+  const int H = COOP_H, H4 = 4 * COOP_H;
+  const int grp = blockIdx.x / COOP_NW, w = blockIdx.x % COOP_NW, tid = threadIdx.x;
+  const int d = grp & 1, slot = grp >> 1, nslots = a.groups >> 1;
+  const int r = tid >> 2, part = tid & 3;
+  const int gate = r / COOP_U, unit = r % COOP_U;
+  const int grow = gate * H + w * COOP_U + unit;  // global gate row of lane row r
+  {  // resident W_hh slice: local row rr = (gate, unit) <- W_hh[gate * H + w * 32 + unit][:]
+    const float* W = d ? a.whh1 : a.whh0;
+    for (int i = tid; i < COOP_ROWS * (COOP_H / 4); i += 512) {
+      const int rr = i / (COOP_H / 4), q = i % (COOP_H / 4);
+      const int gr = (rr / COOP_U) * H + w * COOP_U + (rr % COOP_U);
+      *reinterpret_cast<float4*>(&Ws[rr * COOP_LD + 4 * q]) = *reinterpret_cast<const float4*>(&W[(size_t)gr * H + 4 * q]);
+    }
+  }
+  __shared__ int poisoned;  // a timed-out wait: stop waiting, poison the outputs
+  if (tid == 0) poisoned = 0;
+  unsigned arrivals = 0;
+  float* xh = a.xh + (size_t)grp * 2 * H;
+  for (int b = slot; b < a.B; b += nslots) {
+    int len = a.lengths ? a.lengths[b] : a.T;
+    len = len < 0 ? 0 : (len > a.T ? a.T : len);
+    float* yb = a.y + (size_t)b * a.T * 2 * H + (size_t)d * H + w * COOP_U;
+    if (tid < COOP_U)
+      for (int t = len; t < a.T; ++t) yb[(size_t)t * 2 * H + tid] = 0.f;
+    if (tid < H) hb[tid] = 0.f;
+    float c = 0.f, h = 0.f;
+    __syncthreads();
+    const float* Gb = a.G + ((size_t)d * a.B + b) * a.T * H4;
+    for (int s = 0; s < len; ++s) {
+      const int t = d == 0 ? s : len - 1 - s;
+      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+      const float* wr = Ws + r * COOP_LD + part * (COOP_H / 4);
+      const float* hr = hb + part * (COOP_H / 4);
+#pragma unroll
+      for (int m = 0; m < COOP_H / 16; ++m) {
+        const float4 wv = *reinterpret_cast<const float4*>(wr + 4 * m);
+        const float4 hv = *reinterpret_cast<const float4*>(hr + 4 * m);
+        acc0 = fmaf(wv.x, hv.x, acc0);
+        acc1 = fmaf(wv.y, hv.y, acc1);
+        acc2 = fmaf(wv.z, hv.z, acc2);
+        acc3 = fmaf(wv.w, hv.w, acc3);
+      }
+      float v = (acc0 + acc1) + (acc2 + acc3);
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      if (part == 0) gl[r] = v + Gb[(size_t)t * H4 + grow];
+      __syncthreads();
+      float* xo = xh + (size_t)(s & 1) * H;
+      if (tid < COOP_U) {
+        const float ig = sigm(gl[tid]), fg = sigm(gl[COOP_U + tid]), gg = tanhf(gl[2 * COOP_U + tid]);
+        const float og = sigm(gl[3 * COOP_U + tid]);
+        c = fg * c + ig * gg;
+        h = og * tanhf(c);
+        __hip_atomic_store(&xo[w * COOP_U + tid], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        yb[(size_t)t * 2 * H + tid] = poisoned ? __builtin_nanf("") : h;
+      }
+      __syncthreads();
+      ++arrivals;
+      if (tid == 0) {  // wave 0 also made the h stores above: the release orders them before the arrival
+        __hip_atomic_fetch_add(&a.counter[grp], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = arrivals * COOP_NW;
+        unsigned spins = 0;
+        while (!poisoned &&
+               __hip_atomic_load(&a.counter[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          if (++spins > COOP_SPIN_LIMIT) {
+            atomicOr(a.err, 1);
+            poisoned = 1;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (tid < H) hb[tid] = __hip_atomic_load(&xo[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+    }
+    if (tid < COOP_U) {
+      if (a.hn) a.hn[((size_t)d * a.B + b) * H + w * COOP_U + tid] = h;
+      if (a.cn) a.cn[((size_t)d * a.B + b) * H + w * COOP_U + tid] = c;
+    }
+    __syncthreads();
+  }
+}
+
+static int g_coop_groups_cap = -1;  // co-resident groups this device allows (-1 = not probed)
+#define COOP_LDS_BYTES ((COOP_ROWS * COOP_LD + COOP_H + COOP_ROWS) * (int)sizeof(float))
+
+// W_hh [4H][H] (torch) -> WT4 [H/4][4H][4] (k-quad interleaved), both directions.
 __global__ void k_lstm_wt(const float* __restrict__ w0, const float* __restrict__ w1, int H, float* __restrict__ wt) {
   const int H4 = 4 * H;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (size_t)2 * H * H4) return;
   const int d = (int)(i / ((size_t)H * H4));
   const int r = (int)(i % ((size_t)H * H4));
-  const int k = r / H4, jj = r % H4;
+  const int q = r / (H4 * 4), jj = (r >> 2) % H4, k = 4 * q + (r & 3);
   const float* w = d ? w1 : w0;
   wt[i] = w[(size_t)jj * H + k];
 }
@@ -391,14 +582,16 @@ int stts_frames_gemm(const float* x, long long xs_b, long long xs_t, long long x
 
 long long stts_bilstm_workspace_bytes(int B, int T, int H) {
   if (B < 0 || T < 0 || H <= 0) return -1;
-  return ((long long)2 * B * T * 4 * H + (long long)2 * H * 4 * H) * (long long)sizeof(float);
+  // G + W_hh^T, then the cooperative kernel's exchange buffers (<= 2B groups x 2 x H), counters, flag
+  return ((long long)2 * B * T * 4 * H + (long long)2 * H * 4 * H + (long long)2 * B * 2 * H) * (long long)sizeof(float) +
+         (long long)(2 * B + 1) * 4;
 }
 
 int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
                     const int* lengths, const float* const* params, int H, float* y, float* h_n, float* c_n,
                     void* workspace, long long ws_bytes, void* stream) {
   if (B < 0 || T < 0 || Cin <= 0 || !params || !y) return ST_EINVAL;
-  if (H <= 0 || H > 256 || (H & 15)) return ST_EINVAL;  // 4H lanes per workgroup, float4 LDS reads
+  if (H <= 0 || H > 256 || (H & 31)) return ST_EINVAL;  // 4H lanes per workgroup, chunks of 8 k-quads
   for (int i = 0; i < 8; ++i)
     if (!params[i]) return ST_EPARAMS;
   if (ws_bytes < stts_bilstm_workspace_bytes(B, T, H)) return ST_EWORKSPACE;
@@ -420,7 +613,44 @@ int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs
       ST_CHECK(launch_gemm(a, B, s));
     }
   }
-  hipLaunchKernelGGL(k_bilstm_rec, dim3(B, 2), dim3(H4), 0, s, G, WT, lengths, B, T, H, y, h_n, c_n);
+  // utterances per workgroup: 1 (measured fastest at every B from 1 to 64, tools/lstm_sweep.py);
+  // 2 / 4 share each W_hh load between utterances (A/B knob stts_set_lstm_group)
+  // cooperative path: B <= 4 by default (measured, tools/lstm_sweep.py: 4.75 vs 8.4 us a step at B = 1,
+  // 6.6 vs 8.5 at B = 4, slower from B = 8 as the groups' arrival counters contend); -1 forces it
+  if (H == COOP_H && (g_lstm_bg == -1 || (g_lstm_bg == 0 && B <= 4)) && B > 0 && T > 0) {
+    if (g_coop_groups_cap < 0) {
+      g_coop_groups_cap = 0;
+      int dev = 0, ncu = 0, coop = 0, occ = 0;
+      if (hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && coop &&
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+          hipFuncSetAttribute((const void*)k_bilstm_coop, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              COOP_LDS_BYTES) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bilstm_coop, 512, COOP_LDS_BYTES) == hipSuccess)
+        g_coop_groups_cap = ((occ * ncu) / COOP_NW) & ~1;
+    }
+    int groups = 2 * B < g_coop_groups_cap ? 2 * B : g_coop_groups_cap;
+    if (groups >= 2) {
+      char* extra = (char*)(WT + (size_t)2 * H * H4);
+      float* xh = (float*)extra;
+      unsigned* counter = (unsigned*)(xh + (size_t)groups * 2 * H);
+      int* err = (int*)(counter + groups);
+      ST_CHECK_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned) * groups + sizeof(int), s));
+      CoopArgs ca{G, params[1], params[5], lengths, B, T, groups, y, h_n, c_n, xh, counter, err};
+      void* args[] = {&ca};
+      hipError_t e = hipLaunchCooperativeKernel((const void*)k_bilstm_coop, dim3(groups * COOP_NW), dim3(512), args,
+                                                COOP_LDS_BYTES, s);
+      if (e == hipSuccess) return 0;
+      (void)hipGetLastError();  // not co-resident on this device / stream: the per-workgroup kernel below
+    }
+  }
+  const int bg = g_lstm_bg > 0 ? g_lstm_bg : 1;  // (-1 with no co-residency: 1)
+  if (bg == 4)
+    hipLaunchKernelGGL(k_bilstm_rec<4>, dim3((B + 3) / 4, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n);
+  else if (bg == 2)
+    hipLaunchKernelGGL(k_bilstm_rec<2>, dim3((B + 1) / 2, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n);
+  else
+    hipLaunchKernelGGL(k_bilstm_rec<1>, dim3(B, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n);
   return (int)hipGetLastError();
 }
 
@@ -477,4 +707,10 @@ int st_wn_fold(const float* v, const float* g, int d0, int inner, float* wout, h
 extern "C" int stts_weight_norm(const float* g, const float* v, int d0, int inner, float* w, void* stream) {
   if (d0 <= 0 || inner <= 0 || !v || !w) return ST_EINVAL;
   return st_wn_fold(v, g, d0, inner, w, (hipStream_t)stream);
+}
+
+extern "C" int stts_set_lstm_group(int bg) {
+  if (bg != -1 && bg != 0 && bg != 1 && bg != 2 && bg != 4) return ST_EINVAL;
+  g_lstm_bg = bg;
+  return 0;
 }

@@ -39,6 +39,8 @@ def _L():
         L.stts_bilstm_fwd.argtypes = [c_vp, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp, ctypes.POINTER(c_vp), c_int,
                                       c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]
         L.stts_bilstm_fwd.restype = c_int
+        L.stts_set_lstm_group.argtypes = [c_int]
+        L.stts_set_lstm_group.restype = c_int
         L.stts_row_norm.argtypes = [c_vp, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_float,
                                     c_int, c_float, c_vp, c_vp, c_int, c_vp, c_ll, c_ll, c_vp]
         L.stts_row_norm.restype = c_int
@@ -53,6 +55,12 @@ def _L():
         L.stts_expand_frames.restype = c_int
         _BOUND = True
     return L
+
+
+def set_lstm_group(bg: int) -> None:
+    """BiLSTM recurrence kernel: 0 = automatic, -1 = cooperative (H = 256), 1 / 2 / 4 = utterances per
+    workgroup of the per-workgroup kernel (A/B testing)."""
+    check(_L().stts_set_lstm_group(int(bg)), "stts_set_lstm_group")
 
 
 def _on_device(t: torch.Tensor, what: str) -> torch.Tensor:

@@ -65,7 +65,7 @@ def test_shared_lstm_vs_reference_tap():
     assert _err(h.transpose(1, 2), g["tap_lstm"]) < TOL
 
 
-@pytest.mark.parametrize("H,Cin,T,lengths", [(16, 8, 5, (5, 1, 3)), (64, 40, 33, (33, 17)), (256, 640, 130, None),
+@pytest.mark.parametrize("H,Cin,T,lengths", [(32, 8, 5, (5, 1, 3)), (64, 40, 33, (33, 17)), (256, 640, 130, None),
                                              (128, 96, 7, (0, 7))])
 def test_lstm_vs_torch(H, Cin, T, lengths):
     torch.manual_seed(H + T)
@@ -201,3 +201,61 @@ def test_synthesizer_chain_vs_oracle(mods):
     assert out.shape[-1] == 600 * F == want.shape[-1]
     assert _err(out, want.numpy()) < 1e-3  # north-star waveform tolerance
     assert abs(float(dmean) - float(want_mean)) < 1e-4
+
+
+def test_lstm_groupings_bit_identical():
+    """The recurrence's utterances-per-workgroup choice (1 / 2 / 4) changes no bit of the output."""
+    from stts2_mi355x.prosody import set_lstm_group
+    torch.manual_seed(11)
+    lstm = LSTM(64, 256, 1, batch_first=True, bidirectional=True).cuda()
+    x = torch.randn(7, 29, 64).cuda()
+    ln = torch.tensor([29, 3, 17, 29, 1, 8, 22])
+    outs = []
+    try:
+        for bg in (1, 2, 4):
+            set_lstm_group(bg)
+            outs.append(lstm(x, lengths=ln)[0])
+    finally:
+        set_lstm_group(0)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    ref = torch.nn.LSTM(64, 256, 1, batch_first=True, bidirectional=True)
+    ref.load_state_dict({k: v.cpu() for k, v in lstm.state_dict().items()})
+    with torch.no_grad():
+        y, _ = ref(torch.nn.utils.rnn.pack_padded_sequence(x.cpu(), ln, batch_first=True, enforce_sorted=False))
+    y, _ = torch.nn.utils.rnn.pad_packed_sequence(y, batch_first=True, total_length=29)
+    assert _err(outs[2], y.numpy()) < TOL
+
+
+def test_lstm_cooperative_many_utterances():
+    """H = 256 runs the cooperative recurrence (W_hh split over 8 workgroups, persistent over the
+    utterances): ragged batch larger than the co-resident group count, zero-length rows included."""
+    from stts2_mi355x.prosody import set_lstm_group
+    torch.manual_seed(12)
+    lstm = LSTM(40, 256, 1, batch_first=True, bidirectional=True)
+    ref = torch.nn.LSTM(40, 256, 1, batch_first=True, bidirectional=True)
+    ref.load_state_dict(lstm.state_dict())
+    lstm = lstm.cuda()
+    B, T = 40, 23
+    ln = torch.randint(1, T + 1, (B,))
+    ln[5], ln[0] = 0, T
+    x = torch.randn(B, T, 40)
+    set_lstm_group(-1)
+    try:
+        got, (hn, cn) = lstm(x.cuda(), lengths=ln)
+    finally:
+        set_lstm_group(0)
+    keep = ln > 0
+    with torch.no_grad():
+        y, (rh, rc) = ref(torch.nn.utils.rnn.pack_padded_sequence(x[keep], ln[keep], batch_first=True,
+                                                                   enforce_sorted=False))
+    y, _ = torch.nn.utils.rnn.pad_packed_sequence(y, batch_first=True, total_length=T)
+    want = torch.zeros(B, T, 512)
+    want[keep] = y
+    assert _err(got, want.numpy()) < TOL
+    assert _err(hn[:, keep], rh.numpy()) < TOL and _err(cn[:, keep], rc.numpy()) < TOL
+    set_lstm_group(1)
+    try:
+        alt, _ = lstm(x.cuda(), lengths=ln)
+    finally:
+        set_lstm_group(0)
+    assert _err(got, alt.cpu().numpy()) < 1e-5

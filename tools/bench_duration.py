@@ -9,7 +9,7 @@ Workloads (synthetic formula weights, inputs resident in HBM, fp32):
     for B utterances of `tokens` tokens (130 tokens ~ a 10-s utterance at ~3 frames a token);
   * the F0Ntrain shared BiLSTM at B x `frames` (400 frames = 10 s), the largest recurrence of the path;
   * one utterance end to end (Synthesizer.inference: tokens -> waveform, HiFi-GAN decoder fp32 and
-    bf16), the reference's own inference.py unit.
+    bf16), the reference's own inference.py unit (B = 1: the cooperative BiLSTM recurrence runs).
 Timing: torch.cuda.Event pairs on the current stream (the library launches on it).
 
 The BiLSTM recurrence is a chain of `len` dependent steps: its bound is per-step latency, not HBM or
@@ -57,6 +57,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the one-utterance end-to-end leg")
+    ap.add_argument("--e2e-tokens", type=int, default=14,
+                    help="tokens of the end-to-end utterance (formula weights give ~25 frames a token: "
+                         "14 (+2 pads) ~ 400 frames = 10 s)")
     args = ap.parse_args()
 
     from helpers import make_decoder, make_duration_modules
@@ -91,15 +95,15 @@ def main():
     # one utterance end to end (inference.py unit), fp32 and bf16 decoders
     dec, _ = make_decoder("hifigan")
     dec = dec.to(dev)
-    tokens1 = [int(v) for v in (synth.hash_u01("bench:e2e:tok", T - 2) * 177 + 1)]
+    tokens1 = [int(v) for v in (synth.hash_u01("bench:e2e:tok", args.e2e_tokens) * 177 + 1)]
     s1 = s[:1]
     e2e = {}
-    for dt in ("fp32", "bf16"):
+    for dt in (() if args.no_e2e else ("fp32", "bf16")):
         syn = Synthesizer(te, pp, dec, decoder_dtype=dt)
-        z1 = torch.zeros(1, T, device=dev)
+        z1 = torch.zeros(1, args.e2e_tokens + 2, device=dev)
         frames = syn.alignment(tokens1, s1, t=0.1, z=z1)["frames"]
         ms = timed(lambda: syn.inference(tokens1, s1, t=0.1, z=z1), max(2, args.steps // 2), 1)
-        e2e[dt] = {"ms": ms, "frames": frames, "samples": 600 * frames,
+        e2e[dt] = {"ms": ms, "tokens": args.e2e_tokens + 2, "frames": frames, "samples": 600 * frames,
                    "x_realtime": (600 * frames / 24000) / (ms / 1e3)}
 
     H = 256
