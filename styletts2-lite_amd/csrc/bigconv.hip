@@ -241,7 +241,7 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
             q += __shfl_xor(q, o);
           }
           if (l32 == 0) {
-            double* d = p.stats + ((size_t)b * p.stats_ld + (wn * NTL + ni) * 32 + hi * 16 + r) * 2;
+            double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + (wn * NTL + ni) * 32 + hi * 16 + r) * 2;
             atomicAdd(d, (double)a);
             atomicAdd(d + 1, (double)q);
           }
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   // per-tile path: LDS accumulators -> global (after a barrier), when the block leaves utterance b
   auto flush_lds = [&](int b) __attribute__((always_inline)) {
     for (int ci = tid; ci < C; ci += NT) {
-      double* d = p.stats + ((size_t)b * p.stats_ld + ci) * 2;
+      double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ci) * 2;
       atomicAdd(d, (double)st_lds[2 * ci]);
       atomicAdd(d + 1, (double)st_lds[2 * ci + 1]);
       st_lds[2 * ci] = st_lds[2 * ci + 1] = 0.f;

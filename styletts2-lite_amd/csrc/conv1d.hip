@@ -148,8 +148,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       const int n = nt * BN + (wn * WN + ni) * 32 + l32;
       if (hi == 0 && n < p.N) {
         const int co = n % p.Cout;
-        atomicAdd(p.stats + ((size_t)b * p.stats_ld + co) * 2 + 0, (double)a);
-        atomicAdd(p.stats + ((size_t)b * p.stats_ld + co) * 2 + 1, (double)q);
+        double* sb = stats_slot(p, blockIdx.x);
+        atomicAdd(sb + ((size_t)b * p.stats_ld + co) * 2 + 0, (double)a);
+        atomicAdd(sb + ((size_t)b * p.stats_ld + co) * 2 + 1, (double)q);
       }
       st_s[ni] = st_q[ni] = 0.f;
     }

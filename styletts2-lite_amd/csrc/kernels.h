@@ -37,6 +37,11 @@ struct ConvParams {
   int epi_tanh, reflect_front;
   double* stats;  // [B][stats_ld][2] accumulated statistics of the stored output
   int stats_ld;
+  // small-batch atomic spreading: workgroup g accumulates into slot g % stats_slots, the slot
+  // buffers lying stats_slot_bs doubles apart after `stats` (slot 0 = stats itself); the caller
+  // folds slots 1.. into slot 0 after the launch (st_stats_fold).  0 / 1 = direct atomics.
+  int stats_slots;
+  long long stats_slot_bs;
   // 2-D taps on a zero-padded, row-flattened image (style encoder): tap t reads input row
   // q*stride + (t / kw) * row_off + (t % kw) * dil - pad.  1-D convs: kw = KS, row_off = 0.
   int kw, row_off;
@@ -50,6 +55,12 @@ struct ConvParams {
 };
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);
+// slot base of workgroup `g` (see ConvParams::stats_slots)
+__device__ __forceinline__ double* stats_slot(const ConvParams& p, int g) {
+  return p.stats_slots > 1 ? p.stats + (size_t)(g % p.stats_slots) * p.stats_slot_bs : p.stats;
+}
+// stats[b][c] += sum of slots 1..S-1, and those slots are zeroed, for b < B, c < C
+int st_stats_fold(double* stats, int B, int ld, int C, int slots, long long slot_bs, hipStream_t s);
 // which engine st_conv1d routes p to (profiling records; bench.py names the dominant kernel)
 enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2, ST_ENGINE_RESFUSED = 3 };
 int st_conv1d_engine(const ConvParams& p, int dtype);
@@ -88,6 +99,8 @@ struct ResFusedParams {
   float acc_div;
   double* stats;
   int stats_ld;
+  int stats_slots;  // as ConvParams::stats_slots
+  long long stats_slot_bs;
 };
 extern int g_opt_resfused;
 bool st_resfused_eligible(int C, int K, int dil, int dtype);

@@ -24,6 +24,25 @@ namespace {
     }                                              \
   } while (0)
 
+// slots 1..S-1 of a spread statistics buffer folded into slot 0 and cleared (ConvParams::stats_slots)
+__global__ void __launch_bounds__(256) k_stats_fold(double* __restrict__ st, int B, int ld, int C, int S,
+                                                    long long slot_bs) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i % C;
+  double* d = st + ((size_t)b * ld + c) * 2;
+  double a = 0.0, q = 0.0;
+  for (int k = 1; k < S; ++k) {
+    double* e = d + (size_t)k * slot_bs;
+    a += e[0];
+    q += e[1];
+    e[0] = 0.0;
+    e[1] = 0.0;
+  }
+  d[0] += a;
+  d[1] += q;
+}
+
 __device__ __forceinline__ void atomic_stats(double* st, double a, double q) {
   atomicAdd(st, a);
   atomicAdd(st + 1, q);
@@ -767,6 +786,12 @@ int st_istft(const void* post, int B, int F, int ld, int n_fft, int hop, const f
   dim3 grid((L + 255) / 256, B);
   DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_istft<T>, grid, dim3(256), 0, s, reinterpret_cast<const T*>(post), F,
                                               ld, n_fft, hop, br, bi, out, L));
+  return (int)hipGetLastError();
+}
+
+int st_stats_fold(double* stats, int B, int ld, int C, int slots, long long slot_bs, hipStream_t s) {
+  if (slots <= 1 || B * C == 0) return 0;
+  hipLaunchKernelGGL(k_stats_fold, dim3((B * C + 255) / 256), dim3(256), 0, s, stats, B, ld, C, slots, slot_bs);
   return (int)hipGetLastError();
 }
 

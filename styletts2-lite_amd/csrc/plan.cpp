@@ -382,6 +382,8 @@ struct Buf {
   void* at(int c0, size_t esz) const { return p + (size_t)c0 * esz; }
 };
 
+static int g_opt_stats_slots = 0;  // STTS_OPT_STATS_SLOTS (0 = automatic)
+
 struct Ctx {
   Model* m;
   int dtype;
@@ -392,6 +394,10 @@ struct Ctx {
   char* ws;
   size_t off = 0;
   size_t stats_begin = 0, stats_off = 0;
+  // small batches: conv statistics spread over `slots` copies so that the persistent grids' fp64
+  // atomics do not all land on the same few (utterance, channel) addresses (B = 1: ~200-450 us a
+  // launch measured, tools/phase_profile.py with PHASE_B=1), folded after each producing launch
+  int slots = 1;
   float* H = nullptr;
   const char* packed;
   char* aux;
@@ -411,7 +417,7 @@ struct Ctx {
   }
   double* stat(int C) {
     double* p = dry ? nullptr : reinterpret_cast<double*>(ws + stats_off);
-    stats_off += rup((size_t)B * C * 2 * sizeof(double), ALIGN);
+    stats_off += rup((size_t)slots * B * C * 2 * sizeof(double), ALIGN);
     return p;
   }
   const void* wpk(const WConv& c) const { return packed + c.off[dtype]; }
@@ -507,8 +513,11 @@ int conv_run(Ctx& c, ConvParams& p) {
   if (c.dry) return 0;
   const bool prof = g_prof.on;
   if (prof) ST_CHECK(prof_begin(c));
+  p.stats_slots = p.stats ? c.slots : 1;
+  p.stats_slot_bs = (long long)c.B * p.stats_ld * 2;
   int r = st_conv1d(p, c.dtype, c.s);
   if (r) return r;
+  if (p.stats && c.slots > 1) ST_CHECK(st_stats_fold(p.stats, c.B, p.stats_ld, p.Cout, c.slots, p.stats_slot_bs, c.s));
   if (prof) {
     // algorithmic work: a (transposed) conv is 2 * rows * N * Cin * taps flops on its GEMM view;
     // bytes = one read of the input, residual and running sum, one write of the output (none for a
@@ -523,11 +532,14 @@ int conv_run(Ctx& c, ConvParams& p) {
   return 0;
 }
 
-int resfused_run(Ctx& c, const ResFusedParams& p) {
+int resfused_run(Ctx& c, ResFusedParams& p) {
   if (c.dry) return 0;
   const bool prof = g_prof.on;
   if (prof) ST_CHECK(prof_begin(c));
+  p.stats_slots = p.stats ? c.slots : 1;
+  p.stats_slot_bs = (long long)c.B * p.stats_ld * 2;
   ST_CHECK(st_resfused(p, c.s));
+  if (p.stats && c.slots > 1) ST_CHECK(st_stats_fold(p.stats, c.B, p.stats_ld, p.C, c.slots, p.stats_slot_bs, c.s));
   if (prof) {
     // algorithmic work of the two convs; bytes = x once (window + residual), running sum, y
     const double fl = 2.0 * 2.0 * p.B * (double)p.L * p.C * p.C * p.K;
@@ -1134,6 +1146,7 @@ template <typename F>
 int with_ctx(Model* m, int dtype, int B, void* ws, long long ws_bytes, void* stream, F&& body, size_t* need) {
   if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
   Ctx c{m, dtype, (size_t)(dtype == ST_FP32 ? 4 : 2), B, (hipStream_t)stream, true, nullptr};
+  c.slots = g_opt_stats_slots > 0 ? g_opt_stats_slots : (B <= 4 ? 16 : 1);
   c.packed = m->packed[dtype];
   c.aux = m->packed[dtype] ? const_cast<char*>(m->packed[dtype]) + m->aux_off[dtype] : nullptr;
   ST_CHECK(body(c));  // dry run: layout
@@ -1146,6 +1159,7 @@ int with_ctx(Model* m, int dtype, int B, void* ws, long long ws_bytes, void* str
   if ((long long)total > ws_bytes || !ws) return ST_EWORKSPACE;
   const size_t stats_begin = c.stats_begin;
   Ctx r{m, dtype, c.esz, B, (hipStream_t)stream, false, reinterpret_cast<char*>(ws)};
+  r.slots = c.slots;
   r.packed = c.packed;
   r.aux = c.aux;
   if (total > stats_begin) ST_CHECK_HIP(hipMemsetAsync(r.ws + stats_begin, 0, total - stats_begin, r.s));
@@ -1288,6 +1302,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_GRID_CAP: g_opt_grid_cap = value > 0 ? value : 0; return 0;
     case STTS_OPT_RESFUSED: g_opt_resfused = value != 0; return 0;
     case STTS_OPT_DEBUG: g_opt_debug = value; return 0;
+    case STTS_OPT_STATS_SLOTS: g_opt_stats_slots = value > 0 ? value : 0; return 0;
     default: return ST_EINVAL;
   }
 }

@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
             q += __shfl_xor(q, o);
           }
           if (l32 == 0) {
-            double* d = p.stats + ((size_t)b * p.stats_ld + (wn * NTL + ni) * 32 + hi * 16 + r) * 2;
+            double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + (wn * NTL + ni) * 32 + hi * 16 + r) * 2;
             atomicAdd(d, (double)a);
             atomicAdd(d + 1, (double)q);
           }

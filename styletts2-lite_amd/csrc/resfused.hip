@@ -211,7 +211,8 @@ __global__ void __launch_bounds__(512, 1) k_resfused(const ResFusedParams p) {
           q += __shfl_xor(q, o);
         }
         if (l32 == 0) {
-          double* d = p.stats + ((size_t)b * p.stats_ld + co0 + r) * 2;
+          double* d = (p.stats_slots > 1 ? p.stats + (size_t)(blockIdx.x % p.stats_slots) * p.stats_slot_bs : p.stats) +
+                      ((size_t)b * p.stats_ld + co0 + r) * 2;
           atomicAdd(d, (double)a);
           atomicAdd(d + 1, (double)q);
         }
