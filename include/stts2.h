@@ -188,7 +188,7 @@ const char* stts_error_string(int code);
  *                     4 epilogue) for timing experiments; outputs are WRONG while set.  0 = off. */
 #define STTS_OPT_DEBUG 4
 /*   STTS_OPT_STATS_SLOTS n > 0: copies of every conv-statistics buffer the persistent grids spread their
- *                     fp64 atomics over (folded after each launch); 0 (default) = 16 for B <= 4, else 1. */
+ *                     fp64 atomics over (folded after each launch); 0 (default) = 16 for B <= 4, 4 for B <= 16, else 1. */
 #define STTS_OPT_STATS_SLOTS 5
 int stts_set_option(int key, int value);
 

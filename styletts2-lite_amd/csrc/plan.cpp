@@ -1146,7 +1146,7 @@ template <typename F>
 int with_ctx(Model* m, int dtype, int B, void* ws, long long ws_bytes, void* stream, F&& body, size_t* need) {
   if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
   Ctx c{m, dtype, (size_t)(dtype == ST_FP32 ? 4 : 2), B, (hipStream_t)stream, true, nullptr};
-  c.slots = g_opt_stats_slots > 0 ? g_opt_stats_slots : (B <= 4 ? 16 : 1);
+  c.slots = g_opt_stats_slots > 0 ? g_opt_stats_slots : (B <= 4 ? 16 : (B <= 16 ? 4 : 1));  // tools/slots_sweep.py
   c.packed = m->packed[dtype];
   c.aux = m->packed[dtype] ? const_cast<char*>(m->packed[dtype]) + m->aux_off[dtype] : nullptr;
   ST_CHECK(body(c));  // dry run: layout

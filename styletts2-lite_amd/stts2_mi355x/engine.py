@@ -83,6 +83,7 @@ OPT_RESCONV = 1
 OPT_GRID_CAP = 2
 OPT_RESFUSED = 3
 OPT_DEBUG = 4
+OPT_STATS_SLOTS = 5
 
 
 def set_option(key: int, value: int) -> None:

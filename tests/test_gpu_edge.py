@@ -98,3 +98,28 @@ def test_shape_validation():
             d(asr, f0, n, s, noise=noise[:, :-1])          # noise must be [B, 600T, 9]
         with pytest.raises(ValueError):                    # one frame: the reference's
             d(asr[..., :1], f0[:, :2], n[:, :2], s)        # InstanceNorm1d raises too
+
+
+@pytest.mark.parametrize("dtype,B", [("fp32", 1), ("bf16", 1), ("bf16", 3)])
+def test_stats_slots_do_not_change_results(dtype, B):
+    """Small-batch statistics spreading (STTS_OPT_STATS_SLOTS, slots folded after each launch) only
+    reorders fp64 sums: outputs with 1, 16 and 64 slots agree (fp32 to 1e-5; bf16 to 1e-2, the
+    rounding of a bf16 activation may flip) and fp32 still matches the oracle."""
+    from stts2_mi355x import engine as E
+    d, sd, cfg = dec("hifigan")
+    asr, f0, n, s, noise = decoder_case(B, 7)
+    outs = []
+    try:
+        for slots in (1, 16, 64):
+            E.set_option(E.OPT_STATS_SLOTS, slots)
+            with torch.no_grad():
+                outs.append(d(asr.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=noise.cuda(), dtype=dtype).cpu())
+    finally:
+        E.set_option(E.OPT_STATS_SLOTS, 0)
+    tol = 1e-5 if dtype == "fp32" else 1e-2
+    assert (outs[0] - outs[1]).abs().max().item() < tol
+    assert (outs[0] - outs[2]).abs().max().item() < tol
+    if dtype == "fp32":
+        with torch.no_grad():
+            ref = orc.decoder_hifigan(asr, f0, n, s, sd, cfg, noise)
+        assert (outs[1] - ref).abs().max().item() < 1e-3
