@@ -110,3 +110,63 @@ class Synthesizer:
             asr = expand_frames(t_en.transpose(1, 2), a["pred"], F)  # t_en @ aln  (:268)
             out = self.decoder(asr, F0, N, s, noise=noise, seed=seed, dtype=self.decoder_dtype)
         return out.squeeze(), a["dur_mean"]
+
+
+def symbol_table(config):
+    """inference.py:70-86: the token table from config['symbol'] -> ({symbol: id}, n_token)."""
+    sym = config["symbol"]
+    symbols = (list(sym["pad"]) + list(sym["punctuation"]) + list(sym["letters"]) + list(sym["letters_ipa"])
+               + list(sym["extend"]))
+    table = {s: i for i, s in enumerate(symbols)}
+    return table, len(table) + 1
+
+
+def build_models(config):
+    """inference.py:88-122 with the drop-in classes: the parsed config.yaml (a dict) ->
+    {'decoder', 'predictor', 'text_encoder', 'style_encoder'} modules (parameters on the CPU,
+    move them with .to('cuda'))."""
+    from . import hifigan, istftnet
+    from .models import ProsodyPredictor, StyleEncoder, TextEncoder
+    args = config["model_params"]
+    _, n_token = symbol_table(config)
+    dec = args["decoder"]
+    common = dict(dim_in=args["hidden_dim"], style_dim=args["style_dim"], dim_out=args["n_mels"],
+                  resblock_kernel_sizes=dec["resblock_kernel_sizes"], upsample_rates=dec["upsample_rates"],
+                  upsample_initial_channel=dec["upsample_initial_channel"],
+                  resblock_dilation_sizes=dec["resblock_dilation_sizes"],
+                  upsample_kernel_sizes=dec["upsample_kernel_sizes"])
+    if dec["type"] == "istftnet":
+        decoder = istftnet.Decoder(**common, gen_istft_n_fft=dec["gen_istft_n_fft"],
+                                   gen_istft_hop_size=dec["gen_istft_hop_size"])
+    elif dec["type"] == "hifigan":
+        decoder = hifigan.Decoder(**common)
+    else:  # the reference also accepts 'vocos' (Modules/vocos.py): out of scope here (DESIGN.md §7)
+        raise NotImplementedError(f"decoder type {dec['type']!r}: only hifigan / istftnet run on the HIP path")
+    return {
+        "decoder": decoder,
+        "predictor": ProsodyPredictor(style_dim=args["style_dim"], d_hid=args["hidden_dim"], nlayers=args["n_layer"],
+                                      max_dur=args["max_dur"], dropout=args["dropout"]),
+        "text_encoder": TextEncoder(channels=args["hidden_dim"], kernel_size=5, depth=args["n_layer"],
+                                    n_symbols=n_token),
+        "style_encoder": StyleEncoder(dim_in=args["dim_in"], style_dim=args["style_dim"],
+                                      max_conv_dim=args["hidden_dim"]),
+    }
+
+
+def load_models(model, models_path):
+    """inference.py:150-174 (StyleTTS2.__load_models): checkpoint['net'][key] -> model[key], retrying
+    with the 7-character 'module.' prefix stripped and strict=False as the reference does.  Loaded with
+    torch.load(weights_only=True): a checkpoint that needs unpickling of code is refused.
+    Returns {key: parameter count}."""
+    from collections import OrderedDict
+    params = torch.load(models_path, map_location="cpu", weights_only=True)["net"]
+    params = {k: v for k, v in params.items() if k in model}
+    counts = {}
+    for key in model:
+        try:
+            model[key].load_state_dict(params[key])
+        except Exception:
+            sd = OrderedDict((k[7:], v) for k, v in params[key].items())
+            model[key].load_state_dict(sd, strict=False)
+        counts[key] = sum(p.numel() for p in model[key].parameters())
+    return counts
