@@ -190,6 +190,9 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_STATS_SLOTS n > 0: copies of every conv-statistics buffer the persistent grids spread their
  *                     fp64 atomics over (folded after each launch); 0 (default) = 16 for B <= 4, 4 for B <= 16, else 1. */
 #define STTS_OPT_STATS_SLOTS 5
+/*   STTS_OPT_SMALL_TILES 1 (default) = implicit-GEMM launches that would make fewer than half as many
+ *                     256 x 128 tiles as there are CUs use 64 x 128 tiles; 0 = off (A/B). */
+#define STTS_OPT_SMALL_TILES 6
 int stts_set_option(int key, int value);
 
 /* Optional per-launch timing of the conv engines (conv1d_igemm, resconv, bigconv) with hipEvents

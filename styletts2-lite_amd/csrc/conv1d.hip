@@ -30,6 +30,7 @@
 #include "conv_common.h"
 #include "kernels.h"
 
+
 namespace {
 
 constexpr int BK = 32;
@@ -761,6 +762,13 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
   }
   if (p.epi_tanh) return ST_EINVAL;  // tanh only on narrow heads
   if (p.stride > 1) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);  // BM 64 x BN 128 (short window)
+  if (p.N > 64 && g_opt_small_tiles) {
+    // few tiles (small batches: the 400-frame front-end at B = 1 makes 16 tiles of 256 x 128 for 256
+    // CUs): BM 64 x BN 128 tiles, 4x the workgroups
+    const long long big = (long long)((p.N + 127) / 128) * ((p.Lq + 255) / 256) * p.B;
+    const int ncu = g_num_cu ? g_num_cu : 256;
+    if (big < ncu / 2) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);
+  }
   if (p.N <= 32) return launch_cfg<T, MT, 4, 1, 2, 1>(p, stream);     // BM 256 x BN 32, 4 waves
   if constexpr (!ConvCfg<T, MT, 1, 1, 1, 1>::BF) {
     // fp32 (parity mode): 4-wave tiles, so a wave may hold its fp32 windows and weight slices in
@@ -778,6 +786,7 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
 }  // namespace
 
 int g_opt_resconv = 1;
+int g_opt_small_tiles = 1;
 int g_opt_resfused = 0;
 int g_opt_grid_cap = 0;
 int g_opt_debug = 0;

@@ -69,6 +69,7 @@ int st_conv1d_engine(const ConvParams& p, int dtype);
 bool st_resconv_eligible(const ConvParams& p, int dtype);
 int st_resconv(const ConvParams& p, hipStream_t stream);
 extern int g_opt_resconv;
+extern int g_opt_small_tiles;  // few-tile igemm launches use 64 x 128 tiles (STTS_OPT_SMALL_TILES)
 extern int g_opt_grid_cap;  // > 0: cap persistent conv grids (tests: many tiles per block)
 extern int g_opt_debug;     // resconv phase-skipping knob (timing experiments only)
 // wide-stage resblock conv engine (bigconv.hip): bf16, C = 128 / 256, same contract

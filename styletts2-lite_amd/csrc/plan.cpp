@@ -1303,6 +1303,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_RESFUSED: g_opt_resfused = value != 0; return 0;
     case STTS_OPT_DEBUG: g_opt_debug = value; return 0;
     case STTS_OPT_STATS_SLOTS: g_opt_stats_slots = value > 0 ? value : 0; return 0;
+    case STTS_OPT_SMALL_TILES: g_opt_small_tiles = value != 0; return 0;
     default: return ST_EINVAL;
   }
 }
