@@ -123,3 +123,20 @@ def test_stats_slots_do_not_change_results(dtype, B):
         with torch.no_grad():
             ref = orc.decoder_hifigan(asr, f0, n, s, sd, cfg, noise)
         assert (outs[1] - ref).abs().max().item() < 1e-3
+
+
+def test_small_tiles_do_not_change_results():
+    """STTS_OPT_SMALL_TILES (64 x 128 implicit-GEMM tiles for few-tile launches) vs the 128 x 128 fp32
+    tiles: same sums per output, so the fp32 decoder output agrees to 1e-5."""
+    from stts2_mi355x import engine as E
+    d, sd, cfg = dec("istftnet")
+    asr, f0, n, s, noise = decoder_case(1, 9)
+    outs = []
+    try:
+        for on in (1, 0):
+            E.set_option(6, on)
+            with torch.no_grad():
+                outs.append(d(asr.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=noise.cuda(), dtype="fp32").cpu())
+    finally:
+        E.set_option(6, 1)
+    assert (outs[0] - outs[1]).abs().max().item() < 1e-5
