@@ -227,8 +227,8 @@ __global__ void __launch_bounds__(1024) k_bilstm_rec(const float* __restrict__ G
 // 32 hidden units resident in LDS (128 rows x 256, padded rows: 133 KB), so a step reads no weights
 // from L2 at all.  Per step each workgroup computes its 128 gate rows (512 lanes: row = lane / 4,
 // a quarter of k per lane, shuffle-reduced), updates its 32 (c, h), publishes h to an exchange
-// buffer (double-buffered by step parity) and meets the other 7 at an arrival counter (agent-scope
-// atomics).  Groups = (direction, utterance slot) run persistently over the utterances; the launch
+// buffer as (step tag, h) 64-bit words (double-buffered by step parity) and polls the 256 words of
+// the step (agent-scope acquire loads): the data is its own arrival flag, one round trip a step.  Groups = (direction, utterance slot) run persistently over the utterances; the launch
 // is cooperative (co-residency guaranteed or the launch fails -> k_bilstm_rec), and every spin is
 // bounded (a timed-out wait sets *err and the outputs are poisoned with NaN, never a hang).
 // ---------------------------------------------------------------------------------------
@@ -248,8 +248,7 @@ struct CoopArgs {
   float* y;           // [B][T][2H]
   float* hn;
   float* cn;
-  float* xh;          // exchange [groups][2][H]
-  unsigned* counter;  // [groups], zeroed before launch
+  unsigned long long* xe;  // exchange [groups][2][H] of (step tag << 32 | h bits), zeroed before launch
   int* err;
 };
 
@@ -274,8 +273,8 @@ __global__ void __launch_bounds__(512) k_bilstm_coop(CoopArgs a) {
   }
   __shared__ int poisoned;  // a timed-out wait: stop waiting, poison the outputs
   if (tid == 0) poisoned = 0;
-  unsigned arrivals = 0;
-  float* xh = a.xh + (size_t)grp * 2 * H;
+  unsigned gstep = 1;  // step tag, unique over the group's whole job sequence (words start zeroed)
+  unsigned long long* xe = a.xe + (size_t)grp * 2 * H;
   for (int b = slot; b < a.B; b += nslots) {
     int len = a.lengths ? a.lengths[b] : a.T;
     len = len < 0 ? 0 : (len > a.T ? a.T : len);
@@ -286,8 +285,13 @@ __global__ void __launch_bounds__(512) k_bilstm_coop(CoopArgs a) {
     float c = 0.f, h = 0.f;
     __syncthreads();
     const float* Gb = a.G + ((size_t)d * a.B + b) * a.T * H4;
+    // the input projection of step s + 1 is loaded while step s computes (its HBM / L2 latency was
+    // exposed once a step)
+    float gnext = (part == 0 && len > 0) ? Gb[(size_t)(d == 0 ? 0 : len - 1) * H4 + grow] : 0.f;
     for (int s = 0; s < len; ++s) {
       const int t = d == 0 ? s : len - 1 - s;
+      const float gcur = gnext;
+      if (part == 0 && s + 1 < len) gnext = Gb[(size_t)(d == 0 ? s + 1 : len - 2 - s) * H4 + grow];
       float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
       const float* wr = Ws + r * COOP_LD + part * (COOP_H / 4);
       const float* hr = hb + part * (COOP_H / 4);
@@ -303,34 +307,35 @@ __global__ void __launch_bounds__(512) k_bilstm_coop(CoopArgs a) {
       float v = (acc0 + acc1) + (acc2 + acc3);
       v += __shfl_xor(v, 1);
       v += __shfl_xor(v, 2);
-      if (part == 0) gl[r] = v + Gb[(size_t)t * H4 + grow];
+      if (part == 0) gl[r] = v + gcur;
       __syncthreads();
-      float* xo = xh + (size_t)(s & 1) * H;
+      // publish (h, step tag) as one 64-bit word; every lane k < H then polls word k of this step
+      unsigned long long* xo = xe + (size_t)(gstep & 1) * H;
       if (tid < COOP_U) {
         const float ig = sigm(gl[tid]), fg = sigm(gl[COOP_U + tid]), gg = tanhf(gl[2 * COOP_U + tid]);
         const float og = sigm(gl[3 * COOP_U + tid]);
         c = fg * c + ig * gg;
         h = og * tanhf(c);
-        __hip_atomic_store(&xo[w * COOP_U + tid], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long word = ((unsigned long long)gstep << 32) | (unsigned long long)__float_as_uint(h);
+        __hip_atomic_store(&xo[w * COOP_U + tid], word, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         yb[(size_t)t * 2 * H + tid] = poisoned ? __builtin_nanf("") : h;
       }
-      __syncthreads();
-      ++arrivals;
-      if (tid == 0) {  // wave 0 also made the h stores above: the release orders them before the arrival
-        __hip_atomic_fetch_add(&a.counter[grp], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned target = arrivals * COOP_NW;
+      if (tid < H) {  // hb is free: every lane finished this step's dot products (barrier above)
+        unsigned long long v = 0;
         unsigned spins = 0;
-        while (!poisoned &&
-               __hip_atomic_load(&a.counter[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-          if (++spins > COOP_SPIN_LIMIT) {
-            atomicOr(a.err, 1);
+        while (true) {
+          v = __hip_atomic_load(&xo[tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(v >> 32) == gstep) break;
+          if (poisoned || ++spins > COOP_SPIN_LIMIT) {
+            if (!poisoned) atomicOr(a.err, 1);
             poisoned = 1;
+            break;
           }
           __builtin_amdgcn_s_sleep(1);
         }
+        hb[tid] = __uint_as_float((unsigned)v);
       }
-      __syncthreads();
-      if (tid < H) hb[tid] = __hip_atomic_load(&xo[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ++gstep;
       __syncthreads();
     }
     if (tid < COOP_U) {
@@ -582,9 +587,9 @@ int stts_frames_gemm(const float* x, long long xs_b, long long xs_t, long long x
 
 long long stts_bilstm_workspace_bytes(int B, int T, int H) {
   if (B < 0 || T < 0 || H <= 0) return -1;
-  // G + W_hh^T, then the cooperative kernel's exchange buffers (<= 2B groups x 2 x H), counters, flag
-  return ((long long)2 * B * T * 4 * H + (long long)2 * H * 4 * H + (long long)2 * B * 2 * H) * (long long)sizeof(float) +
-         (long long)(2 * B + 1) * 4;
+  // G + W_hh^T (fp32), then the cooperative kernel's exchange words (<= 2B groups x 2 x H) and flag
+  return ((long long)2 * B * T * 4 * H + (long long)2 * H * 4 * H) * (long long)sizeof(float) +
+         (long long)2 * B * 2 * H * 8 + 8;
 }
 
 int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
@@ -615,8 +620,7 @@ int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs
   }
   // utterances per workgroup: 1 (measured fastest at every B from 1 to 64, tools/lstm_sweep.py);
   // 2 / 4 share each W_hh load between utterances (A/B knob stts_set_lstm_group)
-  // cooperative path: B <= 4 by default (measured, tools/lstm_sweep.py: 4.75 vs 8.4 us a step at B = 1,
-  // 6.6 vs 8.5 at B = 4, slower from B = 8 as the groups' arrival counters contend); -1 forces it
+  // cooperative path: B <= 4 by default (tools/lstm_sweep.py); -1 forces it
   if (H == COOP_H && (g_lstm_bg == -1 || (g_lstm_bg == 0 && B <= 4)) && B > 0 && T > 0) {
     if (g_coop_groups_cap < 0) {
       g_coop_groups_cap = 0;
@@ -632,11 +636,10 @@ int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs
     int groups = 2 * B < g_coop_groups_cap ? 2 * B : g_coop_groups_cap;
     if (groups >= 2) {
       char* extra = (char*)(WT + (size_t)2 * H * H4);
-      float* xh = (float*)extra;
-      unsigned* counter = (unsigned*)(xh + (size_t)groups * 2 * H);
-      int* err = (int*)(counter + groups);
-      ST_CHECK_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned) * groups + sizeof(int), s));
-      CoopArgs ca{G, params[1], params[5], lengths, B, T, groups, y, h_n, c_n, xh, counter, err};
+      unsigned long long* xe = (unsigned long long*)extra;
+      int* err = (int*)(xe + (size_t)groups * 2 * H);
+      ST_CHECK_HIP(hipMemsetAsync(xe, 0, sizeof(unsigned long long) * groups * 2 * H + sizeof(int), s));
+      CoopArgs ca{G, params[1], params[5], lengths, B, T, groups, y, h_n, c_n, xe, err};
       void* args[] = {&ca};
       hipError_t e = hipLaunchCooperativeKernel((const void*)k_bilstm_coop, dim3(groups * COOP_NW), dim3(512), args,
                                                 COOP_LDS_BYTES, s);
