@@ -114,6 +114,13 @@ int stts_frames_gemm(const float* x, long long xs_b, long long xs_t, long long x
                      const float* w, long long ws_b, long long ws_n, long long ws_c, long long ws_k, int N, int K,
                      int pad, const float* bias, const float* bias2, float* y, long long ys_b, long long ys_t,
                      long long ys_n, int Tout, void* stream);
+/* Same, with a scratch workspace: when the output has few 64 x 64 tiles (text-length rows) K is split
+ * over up to 16 workgroups per tile, partial sums go to the workspace (splits x B x Tout x N floats,
+ * fewer splits if it is smaller) and a fixed-order reduction adds them (deterministic). */
+int stts_frames_gemm_ws(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int Tin, int Cin,
+                        const float* w, long long ws_b, long long ws_n, long long ws_c, long long ws_k, int N, int K,
+                        int pad, const float* bias, const float* bias2, float* y, long long ys_b, long long ys_t,
+                        long long ys_n, int Tout, void* workspace, long long ws_bytes, void* stream);
 
 /* Bidirectional single-layer nn.LSTM(batch_first=True) with pack_padded_sequence semantics
  * <- models.py:267-279 (TextEncoder.lstm), :420-430 (ProsodyPredictor.lstm), :449 (shared),

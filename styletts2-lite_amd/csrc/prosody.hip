@@ -37,18 +37,27 @@ struct GemmArgs {
   float* y;
   long long ys_b, ys_t, ys_n;
   int Tout;
+  // split-K (few output tiles): blockIdx.z = b * splits + split; split k covers K rows
+  // [k * kper, (k + 1) * kper) and writes its partial sums to part[k][b][t][n] (no bias); a fixed-order
+  // reduction (k_splitk_reduce) then adds bias and stores y.  splits = 1: direct.
+  int splits, kper;
+  float* part;
 };
 
 __global__ void __launch_bounds__(256) k_frames_gemm(GemmArgs a) {
   __shared__ float As[16][68];  // [k][t]
   __shared__ float Bs[16][68];  // [k][n]
-  const int b = blockIdx.z, t0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int sp = a.splits > 1 ? (int)blockIdx.z % a.splits : 0;
+  const int b = a.splits > 1 ? (int)blockIdx.z / a.splits : (int)blockIdx.z;
+  const int t0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-  const int Ktot = a.Cin * a.K;
+  const int Kall = a.Cin * a.K;
+  const int kbeg = a.splits > 1 ? sp * a.kper : 0;
+  const int Ktot = a.splits > 1 ? (kbeg + a.kper < Kall ? kbeg + a.kper : Kall) : Kall;
   const float* xb = a.x + (size_t)b * a.xs_b;
   const float* wb = a.w + (size_t)b * a.ws_b;
   float acc[4][4] = {};
-  for (int kk = 0; kk < Ktot; kk += 16) {
+  for (int kk = kbeg; kk < Ktot; kk += 16) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int idx = tid + e * 256, kl = idx & 15, rl = idx >> 4;
@@ -77,6 +86,20 @@ __global__ void __launch_bounds__(256) k_frames_gemm(GemmArgs a) {
     }
     __syncthreads();
   }
+  if (a.splits > 1) {
+    float* pp = a.part + (((size_t)sp * gridDim.z / a.splits + b) * a.Tout) * a.N;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tx * 4 + j;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = t0 + ty * 4 + i;
+        if (t < a.Tout) pp[(size_t)t * a.N + n] = acc[i][j];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + tx * 4 + j;
@@ -90,12 +113,44 @@ __global__ void __launch_bounds__(256) k_frames_gemm(GemmArgs a) {
   }
 }
 
-static int launch_gemm(const GemmArgs& a, int B, hipStream_t s) {
-  if (B <= 0 || a.Tout <= 0 || a.N <= 0) return 0;
-  if (a.Cin <= 0 || a.K <= 0 || !a.x || !a.w || !a.y) return ST_EINVAL;
-  dim3 grid((a.Tout + 63) / 64, (a.N + 63) / 64, B);
+__global__ void __launch_bounds__(256) k_splitk_reduce(GemmArgs a, int B) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t per = (size_t)a.Tout * a.N;
+  if (i >= (size_t)B * per) return;
+  const int b = (int)(i / per), t = (int)((i % per) / a.N), n = (int)(i % a.N);
+  float v = 0.f;
+  for (int k = 0; k < a.splits; ++k) v += a.part[(size_t)k * B * per + i];  // fixed order
+  v += (a.bias ? a.bias[n] : 0.f) + (a.bias2 ? a.bias2[n] : 0.f);
+  a.y[(size_t)b * a.ys_b + (size_t)t * a.ys_t + (size_t)n * a.ys_n] = v;
+}
+
+// split count for a launch: enough workgroups for the chip when the output has few 64 x 64 tiles
+// (the text path: 16 - 130 token rows), K chunks of >= 128, at most 16 splits
+static int gemm_splits(int B, int Tout, int N, int Ktot) {
+  const long long tiles = (long long)((Tout + 63) / 64) * ((N + 63) / 64) * B;
+  int sp = 1;
+  while (sp < 16 && tiles * sp * 2 <= 256 && Ktot / (sp * 2) >= 128) sp *= 2;
+  return sp;
+}
+
+static int launch_gemm(const GemmArgs& a0, int B, hipStream_t s, float* part = nullptr, long long part_elems = 0) {
+  if (B <= 0 || a0.Tout <= 0 || a0.N <= 0) return 0;
+  if (a0.Cin <= 0 || a0.K <= 0 || !a0.x || !a0.w || !a0.y) return ST_EINVAL;
+  GemmArgs a = a0;
+  const int Kall = a.Cin * a.K;
+  a.splits = part ? gemm_splits(B, a.Tout, a.N, Kall) : 1;
+  while (a.splits > 1 && (long long)a.splits * B * a.Tout * a.N > part_elems) a.splits >>= 1;
+  a.kper = ((Kall + a.splits - 1) / a.splits + 15) & ~15;
+  a.part = part;
+  dim3 grid((a.Tout + 63) / 64, (a.N + 63) / 64, B * a.splits);
   hipLaunchKernelGGL(k_frames_gemm, grid, dim3(256), 0, s, a);
-  return (int)hipGetLastError();
+  ST_CHECK_HIP(hipGetLastError());
+  if (a.splits > 1) {
+    const size_t n = (size_t)B * a.Tout * a.N;
+    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, B);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  return 0;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -581,8 +636,19 @@ int stts_frames_gemm(const float* x, long long xs_b, long long xs_t, long long x
                      int pad, const float* bias, const float* bias2, float* y, long long ys_b, long long ys_t,
                      long long ys_n, int Tout, void* stream) {
   if (B < 0 || Tin < 0 || Tout < 0 || Cin < 0 || N < 0 || K <= 0 || pad < 0) return ST_EINVAL;
-  GemmArgs a{x, xs_b, xs_t, xs_c, Tin, Cin, w, ws_b, ws_n, ws_c, ws_k, N, K, pad, bias, bias2, y, ys_b, ys_t, ys_n, Tout};
+  GemmArgs a{x, xs_b, xs_t, xs_c, Tin, Cin, w, ws_b, ws_n, ws_c, ws_k, N, K, pad, bias, bias2, y, ys_b, ys_t, ys_n, Tout,
+             1, 0, nullptr};
   return launch_gemm(a, B, (hipStream_t)stream);
+}
+
+int stts_frames_gemm_ws(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int Tin, int Cin,
+                        const float* w, long long ws_b, long long ws_n, long long ws_c, long long ws_k, int N, int K,
+                        int pad, const float* bias, const float* bias2, float* y, long long ys_b, long long ys_t,
+                        long long ys_n, int Tout, void* workspace, long long ws_bytes, void* stream) {
+  if (B < 0 || Tin < 0 || Tout < 0 || Cin < 0 || N < 0 || K <= 0 || pad < 0 || ws_bytes < 0) return ST_EINVAL;
+  GemmArgs a{x, xs_b, xs_t, xs_c, Tin, Cin, w, ws_b, ws_n, ws_c, ws_k, N, K, pad, bias, bias2, y, ys_b, ys_t, ys_n, Tout,
+             1, 0, nullptr};
+  return launch_gemm(a, B, (hipStream_t)stream, (float*)workspace, workspace ? ws_bytes / (long long)sizeof(float) : 0);
 }
 
 long long stts_bilstm_workspace_bytes(int B, int T, int H) {
@@ -614,7 +680,7 @@ int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs
     for (int d = 0; d < 2; ++d) {
       const float* const* p = params + 4 * d;
       GemmArgs a{x, xs_b, xs_t, xs_c, T, Cin, p[0], 0, Cin, 1, 0, H4, 1, 0, p[2], p[3],
-                 G + (size_t)d * B * T * H4, (long long)T * H4, H4, 1, T};
+                 G + (size_t)d * B * T * H4, (long long)T * H4, H4, 1, T, 1, 0, nullptr};
       ST_CHECK(launch_gemm(a, B, s));
     }
   }

@@ -82,7 +82,7 @@ class Synthesizer:
         dev = self.predictor.F0_proj.weight.device
         speed = min(max(speed, 0.0001), 2)
         ids = [0] + [int(i) for i in tokens] + [0]  # tokens.insert(0, 0); tokens.append(0)  (:228-229)
-        tok = torch.tensor(ids, dtype=torch.int64, device=dev).unsqueeze(0)
+        tok = torch.tensor(ids, dtype=torch.int64).unsqueeze(0)  # host: ids checked there, no device sync
         T = tok.shape[1]
         s = torch.as_tensor(ref_s).to(dev, torch.float32).reshape(1, -1)
         with torch.no_grad():

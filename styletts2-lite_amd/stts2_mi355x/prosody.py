@@ -34,6 +34,10 @@ def _L():
         L.stts_frames_gemm.argtypes = [c_vp, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_ll, c_ll, c_ll, c_ll,
                                        c_int, c_int, c_int, c_vp, c_vp, c_vp, c_ll, c_ll, c_ll, c_int, c_vp]
         L.stts_frames_gemm.restype = c_int
+        L.stts_frames_gemm_ws.argtypes = [c_vp, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_ll, c_ll, c_ll, c_ll,
+                                          c_int, c_int, c_int, c_vp, c_vp, c_vp, c_ll, c_ll, c_ll, c_int, c_vp, c_ll,
+                                          c_vp]
+        L.stts_frames_gemm_ws.restype = c_int
         L.stts_bilstm_workspace_bytes.argtypes = [c_int, c_int, c_int]
         L.stts_bilstm_workspace_bytes.restype = c_ll
         L.stts_bilstm_fwd.argtypes = [c_vp, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_vp, ctypes.POINTER(c_vp), c_int,
@@ -81,9 +85,13 @@ def _lengths(lengths, B: int, T: int, device) -> torch.Tensor | None:
 
 
 def frames_gemm(x, xs, B, Tin, Cin, w, wst, N, K, pad, bias, bias2, y, ys, Tout):
-    """Raw stts_frames_gemm (include/stts2.h): xs = (b, t, c) strides, wst = (b, n, c, k), ys = (b, t, n)."""
-    check(_L().stts_frames_gemm(_ptr(x), *xs, B, Tin, Cin, _ptr(w), *wst, N, K, pad, _ptr(bias), _ptr(bias2),
-                                _ptr(y), *ys, Tout, _stream()), "stts_frames_gemm")
+    """Raw stts_frames_gemm_ws (include/stts2.h): xs = (b, t, c) strides, wst = (b, n, c, k), ys = (b, t, n).
+    Outputs with few 64 x 64 tiles (text-length rows) get a split-K scratch buffer."""
+    tiles = ((Tout + 63) // 64) * ((N + 63) // 64) * B
+    elems = 16 * B * Tout * N if tiles < 128 and Cin * K >= 256 else 0
+    ws = torch.empty(elems, dtype=torch.float32, device=y.device) if elems else None
+    check(_L().stts_frames_gemm_ws(_ptr(x), *xs, B, Tin, Cin, _ptr(w), *wst, N, K, pad, _ptr(bias), _ptr(bias2),
+                                   _ptr(y), *ys, Tout, _ptr(ws), elems * 4, _stream()), "stts_frames_gemm_ws")
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -246,12 +254,25 @@ class TextEncoder(nn.Module):
                                           nn.LeakyReLU(self.slope), nn.Dropout(0.2)))
         self.lstm = LSTM(channels, channels // 2, 1, batch_first=True, bidirectional=True)
 
+    def _folded(self, conv):
+        """weight_norm fold (stts_weight_norm), cached until the parameters change (load_state_dict,
+        optimizer steps bump their versions)."""
+        key = (conv.weight_g._version, conv.weight_v._version, conv.weight_g.data_ptr(), conv.weight_v.data_ptr())
+        cache = getattr(conv, "_stts_folded", None)
+        if cache is None or cache[0] != key:
+            cache = (key, weight_norm_fold(conv.weight_g.detach(), conv.weight_v.detach().contiguous()))
+            conv._stts_folded = cache
+        return cache[1]
+
     def forward(self, x, input_lengths, m=None):
         if x.dim() != 2:
             raise ValueError(f"tokens must be [B, T], got {tuple(x.shape)}")
         dev = self.embedding.weight.device
         if dev.type != "cuda":
             raise RuntimeError("TextEncoder: the HIP path needs the module on the HIP device; no CPU fallback")
+        host_checked = not x.is_cuda
+        if host_checked and x.numel() and (int(x.min()) < 0 or int(x.max()) >= self.n_symbols):
+            raise IndexError("TextEncoder: token id outside [0, n_symbols)")  # as nn.Embedding
         tok = x.to(device=dev, dtype=torch.int64).contiguous()
         B, T = tok.shape
         if m is not None and m.shape[-1] != T:
@@ -259,20 +280,20 @@ class TextEncoder(nn.Module):
         C = self.channels
         ln = _lengths(input_lengths, B, T, dev)
         h = torch.empty(B, T, C, dtype=torch.float32, device=dev)
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        err = None if host_checked else torch.zeros(1, dtype=torch.int32, device=dev)
         emb = _on_device(self.embedding.weight.detach(), "embedding").contiguous()
         check(_L().stts_embedding(_ptr(tok), B, T, _ptr(emb), self.n_symbols, C, _ptr(ln), _ptr(h), _ptr(err),
                                   _stream()), "stts_embedding")
         for blk in self.cnn:
             conv, ln_mod = blk[0], blk[1]
-            w = weight_norm_fold(conv.weight_g.detach(), conv.weight_v.detach().contiguous())
+            w = self._folded(conv)
             y = torch.empty(B, T, C, dtype=torch.float32, device=dev)
             frames_gemm(h, h.stride(), B, T, C, w, (0, w.stride(0), w.stride(1), w.stride(2)), C, conv.k,
                         conv.padding, conv.bias.detach(), None, y, y.stride(), T)
             h = row_norm(y, C, 0, gamma=ln_mod.gamma.detach(), beta=ln_mod.beta.detach(), eps=ln_mod.eps,
                          slope=self.slope, lengths=ln)
         out, _ = self.lstm(h, lengths=ln)
-        if int(err.item()) != 0:  # nn.Embedding raises IndexError on an out-of-range id
+        if err is not None and int(err.item()) != 0:  # device tokens: the kernel's flag (one sync)
             raise IndexError("TextEncoder: token id outside [0, n_symbols)")
         return out.transpose(1, 2)
 

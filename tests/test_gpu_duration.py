@@ -121,6 +121,28 @@ def test_lstm_strided_input_and_packed_sequence():
     assert _err(gy, wy.numpy()) < TOL
 
 
+@pytest.mark.parametrize("B,T,Cin,N,K", [(1, 16, 512, 512, 5), (2, 7, 640, 50, 1), (1, 3, 300, 70, 3)])
+def test_frames_gemm_split_k(B, T, Cin, N, K):
+    """Few-tile launches split K (deterministic fixed-order reduction): conv1d vs torch, and the
+    result does not depend on the workspace size (fewer splits)."""
+    from stts2_mi355x import prosody as P
+    torch.manual_seed(B * T + N)
+    x, w, bias = torch.randn(B, T, Cin), torch.randn(N, Cin, K) * 0.05, torch.randn(N)
+    want = torch.nn.functional.conv1d(x.transpose(1, 2), w, bias, padding=(K - 1) // 2).transpose(1, 2)
+    xd, wd, bd = x.cuda(), w.cuda(), bias.cuda()
+    outs = []
+    for elems in (16 * B * T * N, 2 * B * T * N, 0):
+        y = torch.empty(B, T, N, device="cuda")
+        ws = torch.empty(max(elems, 1), device="cuda")
+        P.check(P._L().stts_frames_gemm_ws(P._ptr(xd), *xd.stride(), B, T, Cin, P._ptr(wd), 0, wd.stride(0),
+                                           wd.stride(1), wd.stride(2), N, K, (K - 1) // 2, P._ptr(bd), None,
+                                           P._ptr(y), *y.stride(), T, P._ptr(ws) if elems else None, elems * 4,
+                                           P._stream()))
+        outs.append(y.cpu())
+    for o in outs:
+        assert _err(o, want.numpy()) < 1e-4
+
+
 def test_matmul_and_conv_shapes():
     torch.manual_seed(5)
     a, b = torch.randn(3, 70, 33), torch.randn(3, 33, 129)
@@ -134,7 +156,24 @@ def test_bad_token_raises(mods):
     te, _ = mods
     tok = torch.tensor([[1, 2, 500]]).cuda()
     with pytest.raises(IndexError):
-        te(tok, torch.tensor([3]).cuda())
+        te(tok, torch.tensor([3]).cuda())  # device tokens: the kernel's range flag
+    with pytest.raises(IndexError):
+        te(tok.cpu(), torch.tensor([3]))  # host tokens: checked before the upload
+    te(torch.tensor([[1, 2, 177]]), torch.tensor([3]))
+
+
+def test_text_encoder_fold_cache_follows_weights(mods):
+    """The cached weight-norm fold is recomputed after load_state_dict (parameter versions change)."""
+    te, _ = mods
+    tok = torch.tensor([[3, 4, 5, 6]])
+    a = te(tok, None).clone()
+    sd = {k: v.clone() for k, v in te.state_dict().items()}
+    g = sd["cnn.0.0.weight_g"]
+    te.load_state_dict({**sd, "cnn.0.0.weight_g": g * 1.5})
+    b = te(tok, None).clone()
+    te.load_state_dict(sd)
+    c = te(tok, None)
+    assert (a - b).abs().max().item() > 1e-3 and torch.equal(a, c)
 
 
 def test_cpu_tensors_refused(mods):
