@@ -651,11 +651,16 @@ int stts_frames_gemm_ws(const float* x, long long xs_b, long long xs_t, long lon
   return launch_gemm(a, B, (hipStream_t)stream, (float*)workspace, workspace ? ws_bytes / (long long)sizeof(float) : 0);
 }
 
+static long long lstm_part_elems(int B, int T, int H) {
+  return (long long)B * T <= 256 ? 16LL * B * T * 4 * H : 0;
+}
+
 long long stts_bilstm_workspace_bytes(int B, int T, int H) {
   if (B < 0 || T < 0 || H <= 0) return -1;
-  // G + W_hh^T (fp32), then the cooperative kernel's exchange words (<= 2B groups x 2 x H) and flag
+  // G + W_hh^T (fp32), the cooperative kernel's exchange words (<= 2B groups x 2 x H) and flag, then
+  // for text-length inputs (B T <= 256 rows) a split-K scratch for the input projections
   return ((long long)2 * B * T * 4 * H + (long long)2 * H * 4 * H) * (long long)sizeof(float) +
-         (long long)2 * B * 2 * H * 8 + 8;
+         (long long)2 * B * 2 * H * 8 + 8 + lstm_part_elems(B, T, H) * (long long)sizeof(float);
 }
 
 int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
@@ -681,7 +686,10 @@ int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs
       const float* const* p = params + 4 * d;
       GemmArgs a{x, xs_b, xs_t, xs_c, T, Cin, p[0], 0, Cin, 1, 0, H4, 1, 0, p[2], p[3],
                  G + (size_t)d * B * T * H4, (long long)T * H4, H4, 1, T, 1, 0, nullptr};
-      ST_CHECK(launch_gemm(a, B, s));
+      const long long pe = lstm_part_elems(B, T, H);
+      float* part = pe ? (float*)((char*)workspace + (stts_bilstm_workspace_bytes(B, T, H) - pe * (long long)sizeof(float)))
+                       : nullptr;
+      ST_CHECK(launch_gemm(a, B, s, part, pe));
     }
   }
   // utterances per workgroup: 1 (measured fastest at every B from 1 to 64, tools/lstm_sweep.py);

@@ -121,7 +121,9 @@ def test_duration_path_argument_checks():
     """The duration-path entry points validate shapes before touching the device (include/stts2.h)."""
     from stts2_mi355x import prosody
     L = prosody._L()
-    assert L.stts_bilstm_workspace_bytes(2, 10, 256) == (2 * 2 * 10 * 1024 + 2 * 256 * 1024) * 4 + 2 * 2 * 2 * 256 * 8 + 8
+    assert L.stts_bilstm_workspace_bytes(2, 10, 256) == ((2 * 2 * 10 * 1024 + 2 * 256 * 1024) * 4 + 2 * 2 * 2 * 256 * 8 + 8
+                                                          + 16 * 2 * 10 * 1024 * 4)  # split-K scratch (B T <= 256)
+    assert L.stts_bilstm_workspace_bytes(32, 400, 256) == (2 * 32 * 400 * 1024 + 2 * 256 * 1024) * 4 + 2 * 32 * 2 * 256 * 8 + 8
     params = (ctypes.c_void_p * 8)(*([1] * 8))
     # H must be a multiple of 32 and <= 256
     assert L.stts_bilstm_fwd(1, 0, 0, 0, 1, 4, 8, None, params, 300, 1, None, None, 1, 1 << 30, None) == -1
