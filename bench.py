@@ -10,16 +10,29 @@ checkpoint is download-only); inputs are synthetic with the SURVEY.md §8(d) dis
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--frames 400]
                     [--decoder hifigan|istftnet] [--dtype bf16|fp32] [--no-cpu-baseline]
+                    [--no-profile] [--no-parity-mode] [--no-e2e]
 
-N > 1 is launched by torch.distributed.run (one process per GPU, RCCL): utterances are
-sharded by rank (weak scaling, no data-path collective); timing is bracketed by a barrier
-and device syncs and the max over ranks is reported by rank 0 as ONE JSON line.
+N GPUs = N processes, one per GPU (config 4, BASELINE configs[3]): when WORLD_SIZE is not set
+and N > 1, this process spawns `torch.distributed.run --nproc-per-node N` as a child (it never
+touches the GPU itself) and exits with the child's status; under torch.distributed.run every rank
+reads RANK / LOCAL_RANK / WORLD_SIZE and refuses to run if WORLD_SIZE != --gpus.  Rank r decodes
+its contiguous shard of the N x B global utterances (stts2_mi355x.shard.shard_range) with the
+device noise keyed by GLOBAL utterance id, so the audio does not depend on N.  There is no
+collective on the audio path (weak scaling); the timed region is bracketed by a barrier and
+device syncs, and rank 0 prints ONE JSON line with the max over ranks.  A second timed figure
+adds the RCCL gather of every rank's audio to rank 0 (`with_gather`).
+
+--selftest-cpu (tests only): gloo on the CPU, the decoder replaced by a deterministic stand-in
+of the same output shape, so the spawn / shard / barrier / max / gather plumbing runs without a
+GPU (tests/test_bench_launcher.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,6 +50,11 @@ ISTFT_CFG = dict(resblock_kernel_sizes=[3, 7, 11], upsample_rates=[10, 6], upsam
                  gen_istft_n_fft=20, gen_istft_hop_size=5)
 PEAK_HBM = 8.0e12        # B/s, MI355X HBM3E (MI355X_MICROARCH.md chip table)
 PEAK_MFMA = {"bf16": 2.5e15, "fp32": 157.3e12}  # dense FLOP/s
+# algorithmic work per output sample (activation bytes: each conv reads its input
+# once and writes its output once, everything else fused)
+ALG = {"hifigan": {"flops": 2.913e6, "bytes": {"bf16": 9709.0, "fp32": 19417.0}},
+       "istftnet": {"flops": 2.163e6, "bytes": {"bf16": 3632.0, "fp32": 7265.0}}}
+METRIC = "24 kHz audio samples/sec/GPU + real-time factor, 10-s utterance batch"
 
 
 def build_decoder(kind):
@@ -78,9 +96,9 @@ def cpu_baseline(kind, dec, cfg, T, budget_s=12.0):
                       f"{'decoder_hifigan' if kind == 'hifigan' else 'decoder_istft'} fp32 on torch-CPU"}
 
 
-def roofline(recs, args, el, B, T):
+def roofline(recs, dtype, steps, step_ms, B, T, decoder):
     """Roofline of the dominant kernel (the conv engine with the most hipEvent-timed time in the
-    timed region).  achieved = its algorithmic work (SURVEY.md §8(d) byte / flop model, summed over
+    profiled steps).  achieved = its algorithmic work (SURVEY.md §8(d) byte / flop model, summed over
     its launches) / its measured time; bound = whichever of MFMA / HBM floors is larger for that
     work.  traffic = HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
     passes (tools/pmc_traffic.py -> profiles/*_traffic.json) when they were taken on this exact
@@ -94,9 +112,9 @@ def roofline(recs, args, el, B, T):
         f["launches"] += 1
     name, f = max(fam.items(), key=lambda kv: kv[1]["ms"])
     t_k = f["ms"] / 1e3
-    t_mfma, t_hbm = f["flops"] / PEAK_MFMA[args.dtype], f["bytes"] / PEAK_HBM
+    t_mfma, t_hbm = f["flops"] / PEAK_MFMA[dtype], f["bytes"] / PEAK_HBM
     if t_mfma >= t_hbm:
-        roof = {"bound": "mfma", "achieved": f["flops"] / t_k / 1e12, "peak": PEAK_MFMA[args.dtype] / 1e12,
+        roof = {"bound": "mfma", "achieved": f["flops"] / t_k / 1e12, "peak": PEAK_MFMA[dtype] / 1e12,
                 "unit": "TFLOP/s"}
     else:
         roof = {"bound": "hbm", "achieved": f["bytes"] / t_k / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s"}
@@ -107,18 +125,18 @@ def roofline(recs, args, el, B, T):
     roof["avg_launch_us"] = f["ms"] * 1e3 / f["launches"]
     roof["alg_flops_per_launch"] = f["flops"] / f["launches"]
     roof["alg_bytes_per_launch"] = f["bytes"] / f["launches"]
-    roof["kernel_share_of_step"] = f["ms"] / (el * 1e3)
-    roof["conv_engines"] = {k: {"ms_per_step": v["ms"] / args.steps, "launches_per_step": v["launches"] // args.steps,
+    roof["kernel_share_of_step"] = f["ms"] / steps / step_ms
+    roof["conv_engines"] = {k: {"ms_per_step": v["ms"] / steps, "launches_per_step": v["launches"] // steps,
                                 "tflops": v["flops"] / (v["ms"] / 1e3) / 1e12,
                                 "alg_GBps": v["bytes"] / (v["ms"] / 1e3) / 1e9} for k, v in sorted(fam.items())}
-    tr = _pmc_traffic(name, args, B, T)
+    tr = _pmc_traffic(name, dtype, B, T, decoder)
     if tr is not None:
         roof["traffic"] = tr["hbm_bytes_per_launch"]
         roof["traffic_source"] = tr["source"]
     return roof
 
 
-def _pmc_traffic(kernel, args, B, T):
+def _pmc_traffic(kernel, dtype, B, T, decoder):
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
         try:
@@ -126,10 +144,35 @@ def _pmc_traffic(kernel, args, B, T):
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        if (d.get("kernel") == kernel and d.get("decoder") == args.decoder and d.get("dtype") == args.dtype
+        if (d.get("kernel") == kernel and d.get("decoder") == decoder and d.get("dtype") == dtype
                 and d.get("batch") == B and d.get("frames") == T):
             return {"hbm_bytes_per_launch": d["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
     return None
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn(args_list, n):
+    """N ranks as children of this (GPU-untouched) process: torch.distributed.run, one per GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *args_list]
+    return subprocess.call(cmd)
+
+
+class Stand_in:
+    """--selftest-cpu: the decoder's output contract ([B,1,600T] float32, a pure function of the
+    GLOBAL utterance ids and the step seed) without a GPU."""
+
+    def forward(self, asr, f0, n, s, noise=None, seed=0, utt_offset=0, out=None):
+        B, T = asr.shape[0], asr.shape[2]
+        ids = torch.arange(utt_offset, utt_offset + B, dtype=torch.float64).reshape(B, 1, 1)
+        t = torch.arange(600 * T, dtype=torch.float64).reshape(1, 1, -1)
+        out.copy_(torch.sin(0.001 * t * (ids + 1) + float(seed % 1000)).float())
+        return out
 
 
 def main():
@@ -143,83 +186,168 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-parity-mode", action="store_true", help="skip the fp32 figure of the same workload")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-to-host (PCIe-inclusive) figure")
+    ap.add_argument("--selftest-cpu", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dump-checksum", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}")
+    cpu = args.selftest_cpu
+    dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        dist = None
+        if cpu:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL
+    elif not cpu:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
 
-    from stts2_mi355x import engine as E
-    from stts2_mi355x import synth
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
 
-    B, T = args.batch, args.frames
-    dec, cfg = build_decoder(args.decoder)
-    dec = dec.to(dev)
-    utt0 = rank * B  # global utterance ids of this shard
-    asr, f0, n, s = (torch.from_numpy(a).to(dev) for a in synth.decoder_inputs(B, T, utt0=utt0))
-    eng = dec.engine(args.dtype)
+    from stts2_mi355x import shard, synth
+    B_local, T = args.batch, args.frames
+    global_batch = world * B_local
+    utt0, B = shard.shard_range(global_batch, world, rank)
+    if cpu:
+        eng, dec, cfg = Stand_in(), None, None
+    else:
+        from stts2_mi355x import engine as E
+        dec, cfg = build_decoder(args.decoder)
+        dec = dec.to(dev)
+        eng = dec.engine(args.dtype)
+    host_in = synth.decoder_inputs(B, T, utt0=utt0)
+    asr, f0, n, s = (torch.from_numpy(a).to(dev) for a in host_in)
     out = torch.empty(B, 1, 600 * T, device=dev)
 
-    def step(i):
-        eng.forward(asr, f0, n, s, noise=None, seed=1234 + i, utt_offset=utt0, out=out)
+    def step(i, e=eng, o=out):
+        e.forward(asr, f0, n, s, noise=None, seed=1234 + i, utt_offset=utt0, out=o)
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
+    def timed(fn, k, w, gather=False):
+        """w untimed + k timed calls of fn(i) between barrier + device syncs: max over ranks of the
+        wall time, and the per-step device times (events) for the median."""
+        for i in range(w):
+            fn(i)
+        sync()
+        if dist:
+            dist.barrier()
+        sync()
+        evs = [] if cpu else [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)]
+        t0 = time.perf_counter()
+        if evs:
+            evs[0].record()
+        for i in range(k):
+            fn(w + i)
+            if gather:
+                shard.gather_to_rank0(out, world, rank)
+            if evs:
+                evs[i + 1].record()
+        sync()
+        el = time.perf_counter() - t0
+        per = [evs[i].elapsed_time(evs[i + 1]) for i in range(k)] if evs else [el * 1e3 / k] * k
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+            dist.barrier()
+        return el, per
+
+    el, per = timed(step, args.steps, args.warmup)
+    samples = global_batch * 600 * T * args.steps
+    value = samples / el
+    ms = el / args.steps * 1e3
+
+    # second figure: the same steps with every rank's audio gathered to rank 0 over RCCL
+    with_gather = None
     if dist:
-        dist.barrier()
-    if not args.no_profile:
+        elg, _ = timed(step, args.steps, 1, gather=True)
+        with_gather = {"value": samples / elg, "ms_per_step": elg / args.steps * 1e3,
+                       "gathered_bytes_per_step": global_batch * 600 * T * 4}
+    if args.dump_checksum is not None:  # tests: the audio of every utterance, gathered to rank 0
+        step(0)
+        full = shard.gather_to_rank0(out, world, rank) if dist else out
+        if rank == 0:
+            np.save(args.dump_checksum, full.cpu().numpy())
+
+    prof_recs = None
+    if not cpu and not args.no_profile:  # per-launch hipEvents: a separate pass, not the timed one
         E.profile_enable(True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    prof_recs = E.profile_launches() if not args.no_profile else None
-    E.profile_enable(False)
-    if dist:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = t.item()
-        dist.barrier()
+        for i in range(2):
+            step(100 + i)
+        sync()
+        prof_recs = E.profile_launches()
+        E.profile_enable(False)
+    parity = None
+    if not cpu and not args.no_parity_mode and args.dtype != "fp32":
+        # the north-star accuracy mode (fp32 storage + exact-fp32 MFMA, 10-s max-abs 2.7e-6 vs the
+        # reference) on the same workload
+        peng = dec.engine("fp32")
+        elp, perp = timed(lambda i: step(i, e=peng), 3, 1)
+        parity = {"dtype": "fp32", "steps": 3, "ms_per_step": elp / 3 * 1e3,
+                  "value": global_batch * 600 * T * 3 / elp,
+                  "hbm_fraction": ALG[args.decoder]["bytes"]["fp32"] * global_batch * 600 * T * 3 / elp / PEAK_HBM,
+                  "mfma_fraction": ALG[args.decoder]["flops"] * global_batch * 600 * T * 3 / elp / PEAK_MFMA["fp32"]}
+        dec.engine(args.dtype)
+    e2e = None
+    if not cpu and not args.no_e2e:
+        # host -> host: pinned host inputs copied in, decoded, audio copied back (PCIe included)
+        pins = [torch.from_numpy(a).pin_memory() for a in host_in]
+        hout = torch.empty(B, 1, 600 * T).pin_memory()
+
+        def h2h(i):
+            a, f, nn_, st = (p.to(dev, non_blocking=True) for p in pins)
+            eng.forward(a, f, nn_, st, noise=None, seed=1234 + i, utt_offset=utt0, out=out)
+            hout.copy_(out, non_blocking=True)
+        ele, _ = timed(h2h, 3, 1)
+        e2e = {"value": global_batch * 600 * T * 3 / ele, "ms_per_step": ele / 3 * 1e3,
+               "note": "inputs H2D from pinned host memory + decode + audio D2H, per step"}
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
-    samples = world * B * 600 * T * args.steps
-    value = samples / el
-    ms = el / args.steps * 1e3
-    roof = roofline(prof_recs, args, el, B, T) if prof_recs else None
+    a = ALG[args.decoder]
     line = {
-        "metric": "24 kHz audio samples/sec/GPU + real-time factor, 10-s utterance batch",
+        "metric": METRIC,
         "value": value,
         "unit": "samples/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms,
+        "ms_per_step_median": float(np.median(per)),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (formula weights + SURVEY §8(d) input distributions; device counter-RNG noise)",
-        "config": {"workload": f"{args.decoder} decoder, batch {B}/GPU x {T * 600 // 24000}-s utterances "
+        "data": "synthetic (formula weights + SURVEY §8(d) input distributions; device counter-RNG noise)"
+                + (" [SELFTEST: CPU stand-in decoder, not a measurement]" if cpu else ""),
+        "config": {"workload": f"{args.decoder} decoder, batch {B_local}/GPU x {T * 600 // 24000}-s utterances "
                                f"({T} asr frames, {600 * T} samples each)",
-                   "global_batch": world * B, "frames": T, "decoder": args.decoder,
+                   "global_batch": global_batch, "frames": T, "decoder": args.decoder,
                    "parallelism": f"dp{world} (utterance shards, no collective on the audio path)"},
         "x_realtime_per_gpu": value / world / 24000.0,
-        "roofline": roof,
+        "hbm_fraction": a["bytes"][args.dtype] * value / world / PEAK_HBM,
+        "mfma_fraction": a["flops"] * value / world / PEAK_MFMA[args.dtype],
+        "roofline": roofline(prof_recs, args.dtype, 2, ms, B, T, args.decoder) if prof_recs else None,
     }
-    if not args.no_cpu_baseline and world == 1:
+    if with_gather:
+        line["with_gather"] = with_gather
+    if parity:
+        line["parity_mode"] = parity
+    if e2e:
+        line["e2e_pcie"] = e2e
+    if not cpu and not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(args.decoder, dec.cpu(), cfg, T)
     print(json.dumps(line), flush=True)
     if dist:

@@ -136,6 +136,13 @@ int stts_set_lstm_group(int bg);
 int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
                     const int* lengths, const float* const* params, int H, float* y, float* h_n, float* c_n,
                     void* workspace, long long ws_bytes, void* stream);
+/* Byte offset in that workspace of a device int the forward zeroes and the cooperative recurrence sets
+ * to 1 when a wait for a peer workgroup timed out (y, h_n, c_n are then NaN from that step on): read it
+ * after the stream reaches the call (a host sync the caller already makes) and treat non-zero as an
+ * error.  Testing hook: stts_set_bilstm_debug(spin_limit (0 = default), drop) makes every wait give up
+ * after spin_limit polls and, with drop != 0, one workgroup of each group never publish. */
+long long stts_bilstm_error_offset(int B, int T, int H);
+int stts_set_bilstm_debug(int spin_limit, int drop);
 
 /* Channel norm of frames rows, fused with LeakyReLU, masking and a style concat:
  *   mode 0 LayerNorm(gamma[C], beta[C])       <- models.py:229-240 (TextEncoder cnn)
@@ -187,9 +194,9 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_GRID_CAP n > 0 caps the persistent conv grids at n workgroups (testing: forces many
  *                     tiles and utterance changes per workgroup); 0 (default) = one per CU. */
 #define STTS_OPT_GRID_CAP 2
-/*   STTS_OPT_RESFUSED 1 (default) = bf16 AdaINResBlock1 iterations at C = 32 (and C = 64, K = 3) run
- *                     as a statistics-only conv1 launch + one fused conv1 -> conv2 launch
- *                     (resfused.hip); 0 = two conv launches per iteration (A/B, cross-checking). */
+/*   STTS_OPT_RESFUSED 1 = bf16 AdaINResBlock1 iterations at C = 32 (and C = 64, K = 3) run as a
+ *                     statistics-only conv1 launch + one fused conv1 -> conv2 launch (resfused.hip);
+ *                     0 (default) = two conv launches per iteration (A/B, cross-checking). */
 #define STTS_OPT_RESFUSED 3
 /*   STTS_OPT_DEBUG    bit mask skipping phases of the resblock engine (1 prologue math, 2 MFMAs,
  *                     4 epilogue) for timing experiments; outputs are WRONG while set.  0 = off. */
@@ -201,6 +208,8 @@ const char* stts_error_string(int code);
  *                     256 x 128 tiles as there are CUs use 64 x 128 tiles; 0 = off (A/B). */
 #define STTS_OPT_SMALL_TILES 6
 int stts_set_option(int key, int value);
+/* Current value of an option (STTS_EINVAL for an unknown key). */
+int stts_get_option(int key);
 
 /* Optional per-launch timing of the conv engines (conv1d_igemm, resconv, bigconv) with hipEvents
  * recorded on `stream` around each launch: enable, run, then read totals (ms, launches). */

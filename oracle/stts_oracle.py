@@ -535,3 +535,18 @@ def inference_chain(tokens, s, te_sd, pp_sd, dec_sd, dec_cfg, z, noise_fn, mix=0
     asr = t_en @ aln
     out = decoder_hifigan(asr, F0, N, s, dec_sd, dec_cfg, noise_fn(aln.shape[-1]))
     return out.squeeze(), duration.mean(), pred
+
+
+def generate(sentences, s, te_sd, pp_sd, dec_sd, dec_cfg, zs, noise_fns, stabilize=True, speed=1.0):
+    """reference inference.py:303-319 (StyleTTS2.generate) over per-sentence token-id lists: each
+    sentence through inference_chain with t = 0.2 (stabilize) or 0 and prev_d_mean chained, its
+    audio trimmed by 4000 samples at both ends, concatenated, padded with 4000 zeros at both ends."""
+    smooth = 0.2 if stabilize else 0.0
+    prev = 0.0
+    wavs = []
+    for toks, z, nf in zip(sentences, zs, noise_fns):
+        wav, prev, _ = inference_chain(toks, s, te_sd, pp_sd, dec_sd, dec_cfg, z, nf, mix=smooth,
+                                       prev_mean=float(prev), speed=speed)
+        wavs.append(wav.numpy()[4000:-4000])
+    out = np.concatenate(wavs)
+    return np.concatenate([np.zeros([4000]), out, np.zeros([4000])], axis=0)

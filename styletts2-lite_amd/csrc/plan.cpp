@@ -1308,6 +1308,18 @@ int stts_set_option(int key, int value) {
   }
 }
 
+int stts_get_option(int key) {
+  switch (key) {
+    case STTS_OPT_RESCONV: return g_opt_resconv;
+    case STTS_OPT_GRID_CAP: return g_opt_grid_cap;
+    case STTS_OPT_RESFUSED: return g_opt_resfused;
+    case STTS_OPT_DEBUG: return g_opt_debug;
+    case STTS_OPT_STATS_SLOTS: return g_opt_stats_slots;
+    case STTS_OPT_SMALL_TILES: return g_opt_small_tiles;
+    default: return ST_EINVAL;
+  }
+}
+
 int stts_profile_enable(int on) {
   g_prof.on = on != 0;
   g_prof.used = 0;

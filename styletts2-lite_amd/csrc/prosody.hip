@@ -284,8 +284,10 @@ __global__ void __launch_bounds__(1024) k_bilstm_rec(const float* __restrict__ G
 // a quarter of k per lane, shuffle-reduced), updates its 32 (c, h), publishes h to an exchange
 // buffer as (step tag, h) 64-bit words (double-buffered by step parity) and polls the 256 words of
 // the step (agent-scope acquire loads): the data is its own arrival flag, one round trip a step.  Groups = (direction, utterance slot) run persistently over the utterances; the launch
-// is cooperative (co-residency guaranteed or the launch fails -> k_bilstm_rec), and every spin is
-// bounded (a timed-out wait sets *err and the outputs are poisoned with NaN, never a hang).
+// is a plain launch of at most 2B x 8 workgroups, admitted only when the occupancy query puts all of
+// them on the chip at once (else k_bilstm_rec), and every spin is bounded: a timed-out wait sets
+// *err (the host reads it: stts_bilstm_error_offset) and from then on the workgroup publishes NaN
+// as its h, so y, h_n and c_n are all poisoned, never a hang.
 // ---------------------------------------------------------------------------------------
 #define COOP_H 256
 #define COOP_NW 8
@@ -293,6 +295,8 @@ __global__ void __launch_bounds__(1024) k_bilstm_rec(const float* __restrict__ G
 #define COOP_ROWS (4 * COOP_U)     // gate rows per workgroup (128)
 #define COOP_LD 260                // padded LDS row stride (floats)
 #define COOP_SPIN_LIMIT (1u << 22)
+static unsigned g_coop_spin_limit = COOP_SPIN_LIMIT;  // stts_set_bilstm_debug (tests)
+static int g_coop_drop = 0;                          // debug: member 0 of every group never publishes
 
 struct CoopArgs {
   const float* G;     // [2][B][T][4H] input projections (+ both biases)
@@ -305,6 +309,8 @@ struct CoopArgs {
   float* cn;
   unsigned long long* xe;  // exchange [groups][2][H] of (step tag << 32 | h bits), zeroed before launch
   int* err;
+  unsigned spin_limit;
+  int drop;  // debug: workgroup member 0 never publishes (every wait of its group times out)
 };
 
 __global__ void __launch_bounds__(512) k_bilstm_coop(CoopArgs a) {
@@ -371,9 +377,10 @@ __global__ void __launch_bounds__(512) k_bilstm_coop(CoopArgs a) {
         const float og = sigm(gl[3 * COOP_U + tid]);
         c = fg * c + ig * gg;
         h = og * tanhf(c);
+        if (poisoned) c = h = __builtin_nanf("");  // a peer's h never arrived: everything after is NaN
         const unsigned long long word = ((unsigned long long)gstep << 32) | (unsigned long long)__float_as_uint(h);
-        __hip_atomic_store(&xo[w * COOP_U + tid], word, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        yb[(size_t)t * 2 * H + tid] = poisoned ? __builtin_nanf("") : h;
+        if (!(a.drop && w == 0)) __hip_atomic_store(&xo[w * COOP_U + tid], word, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        yb[(size_t)t * 2 * H + tid] = h;
       }
       if (tid < H) {  // hb is free: every lane finished this step's dot products (barrier above)
         unsigned long long v = 0;
@@ -381,14 +388,14 @@ __global__ void __launch_bounds__(512) k_bilstm_coop(CoopArgs a) {
         while (true) {
           v = __hip_atomic_load(&xo[tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
           if ((unsigned)(v >> 32) == gstep) break;
-          if (poisoned || ++spins > COOP_SPIN_LIMIT) {
+          if (poisoned || ++spins > a.spin_limit) {
             if (!poisoned) atomicOr(a.err, 1);
             poisoned = 1;
             break;
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        hb[tid] = __uint_as_float((unsigned)v);
+        hb[tid] = poisoned ? __builtin_nanf("") : __uint_as_float((unsigned)v);
       }
       ++gstep;
       __syncthreads();
@@ -651,6 +658,12 @@ int stts_frames_gemm_ws(const float* x, long long xs_b, long long xs_t, long lon
   return launch_gemm(a, B, (hipStream_t)stream, (float*)workspace, workspace ? ws_bytes / (long long)sizeof(float) : 0);
 }
 
+// byte offset of the int error word in the BiLSTM workspace (after G and W_hh^T); the exchange
+// words of the cooperative kernel follow it 8 bytes later
+static long long lstm_err_off(int B, int T, int H) {
+  return ((long long)2 * B * T * 4 * H + (long long)2 * H * 4 * H) * (long long)sizeof(float);
+}
+
 static long long lstm_part_elems(int B, int T, int H) {
   return (long long)B * T <= 256 ? 16LL * B * T * 4 * H : 0;
 }
@@ -659,8 +672,12 @@ long long stts_bilstm_workspace_bytes(int B, int T, int H) {
   if (B < 0 || T < 0 || H <= 0) return -1;
   // G + W_hh^T (fp32), the cooperative kernel's exchange words (<= 2B groups x 2 x H) and flag, then
   // for text-length inputs (B T <= 256 rows) a split-K scratch for the input projections
-  return ((long long)2 * B * T * 4 * H + (long long)2 * H * 4 * H) * (long long)sizeof(float) +
-         (long long)2 * B * 2 * H * 8 + 8 + lstm_part_elems(B, T, H) * (long long)sizeof(float);
+  return lstm_err_off(B, T, H) + 8 + (long long)2 * B * 2 * H * 8 + lstm_part_elems(B, T, H) * (long long)sizeof(float);
+}
+
+long long stts_bilstm_error_offset(int B, int T, int H) {
+  if (B < 0 || T < 0 || H <= 0) return -1;
+  return lstm_err_off(B, T, H);
 }
 
 int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
@@ -673,6 +690,8 @@ int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs
   if (ws_bytes < stts_bilstm_workspace_bytes(B, T, H)) return ST_EWORKSPACE;
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  int* err = (int*)((char*)workspace + lstm_err_off(B, T, H));
+  ST_CHECK_HIP(hipMemsetAsync(err, 0, sizeof(int), s));  // the host reads it (stts_bilstm_error_offset)
   float* G = (float*)workspace;
   float* WT = G + (size_t)2 * B * T * 4 * H;
   const int H4 = 4 * H;
@@ -709,16 +728,15 @@ int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs
     }
     int groups = 2 * B < g_coop_groups_cap ? 2 * B : g_coop_groups_cap;
     if (groups >= 2) {
-      char* extra = (char*)(WT + (size_t)2 * H * H4);
-      unsigned long long* xe = (unsigned long long*)extra;
-      int* err = (int*)(xe + (size_t)groups * 2 * H);
-      ST_CHECK_HIP(hipMemsetAsync(xe, 0, sizeof(unsigned long long) * groups * 2 * H + sizeof(int), s));
-      CoopArgs ca{G, params[1], params[5], lengths, B, T, groups, y, h_n, c_n, xe, err};
-      void* args[] = {&ca};
-      hipError_t e = hipLaunchCooperativeKernel((const void*)k_bilstm_coop, dim3(groups * COOP_NW), dim3(512), args,
-                                                COOP_LDS_BYTES, s);
-      if (e == hipSuccess) return 0;
-      (void)hipGetLastError();  // not co-resident on this device / stream: the per-workgroup kernel below
+      unsigned long long* xe = (unsigned long long*)((char*)err + 8);
+      ST_CHECK_HIP(hipMemsetAsync(xe, 0, sizeof(unsigned long long) * groups * 2 * H, s));
+      CoopArgs ca{G, params[1], params[5], lengths, B, T, groups, y, h_n, c_n, xe, err, g_coop_spin_limit, g_coop_drop};
+      // A plain launch: the grid (<= 2B x 8 = 64 workgroups, one per CU by LDS) was checked against the
+      // occupancy query above, which is all hipLaunchCooperativeKernel adds (MI355X_MICROARCH.md
+      // coop-launch: +15-19 us of host time per launch).  Under rocprofv3 the cooperative launch also
+      // ended the process with a segfault at exit (round 1); the plain launch does not.
+      hipLaunchKernelGGL(k_bilstm_coop, dim3(groups * COOP_NW), dim3(512), COOP_LDS_BYTES, s, ca);
+      return (int)hipGetLastError();
     }
   }
   const int bg = g_lstm_bg > 0 ? g_lstm_bg : 1;  // (-1 with no co-residency: 1)
@@ -784,6 +802,13 @@ int st_wn_fold(const float* v, const float* g, int d0, int inner, float* wout, h
 extern "C" int stts_weight_norm(const float* g, const float* v, int d0, int inner, float* w, void* stream) {
   if (d0 <= 0 || inner <= 0 || !v || !w) return ST_EINVAL;
   return st_wn_fold(v, g, d0, inner, w, (hipStream_t)stream);
+}
+
+extern "C" int stts_set_bilstm_debug(int spin_limit, int drop) {
+  if (spin_limit < 0) return ST_EINVAL;
+  g_coop_spin_limit = spin_limit ? (unsigned)spin_limit : COOP_SPIN_LIMIT;
+  g_coop_drop = drop != 0;
+  return 0;
 }
 
 extern "C" int stts_set_lstm_group(int bg) {

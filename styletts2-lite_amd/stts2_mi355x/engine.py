@@ -75,6 +75,8 @@ def lib():
     L.stts_profile_launch.restype = c_int
     L.stts_set_option.argtypes = [c_int, c_int]
     L.stts_set_option.restype = c_int
+    L.stts_get_option.argtypes = [c_int]
+    L.stts_get_option.restype = c_int
     _LIB = L
     return L
 
@@ -86,9 +88,30 @@ OPT_DEBUG = 4
 OPT_STATS_SLOTS = 5
 
 
+OPT_SMALL_TILES = 6
+# the production defaults of every STTS_OPT_* (include/stts2.h)
+OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
+                OPT_SMALL_TILES: 1}
+
+
 def set_option(key: int, value: int) -> None:
     """Process-wide engine option (include/stts2.h STTS_OPT_*)."""
     check(lib().stts_set_option(int(key), int(value)), "stts_set_option")
+
+
+def get_option(key: int) -> int:
+    return int(lib().stts_get_option(int(key)))
+
+
+def reset_options() -> None:
+    """Every engine option back to its production default (tests restore this after A/B runs)."""
+    if _LIB is None:
+        return
+    for k, v in OPT_DEFAULTS.items():
+        set_option(k, v)
+    from . import prosody
+    prosody.set_lstm_group(0)
+    prosody.set_bilstm_debug(0, False)
 
 
 def check(rc: int, what: str = "stts"):
@@ -128,14 +151,19 @@ class NativeModel:
         check(L.stts_model_create(kind, arr, len(cfg), ctypes.byref(h)), "stts_model_create")
         self.h = h
         self.device = torch.device("cuda", torch.cuda.current_device())
-        sd = module.state_dict()
+        sd = module.state_dict(keep_vars=True)
         n = L.stts_param_count(h)
         self.names, self._keep = [], []
+        # (tensor, _version, data_ptr) of every bound module tensor: an in-place update, a .to() or a
+        # load_state_dict makes the packed weights stale (_Engine.stale)
+        self.sources = []
         for i in range(n):
             name = L.stts_param_name(h, i).decode()
             if name not in sd:
                 raise KeyError(f"parameter {name} expected by the native plan is not in the module state dict")
-            t = _dev_f32(sd[name], self.device)
+            src = sd[name]
+            self.sources.append((src, src._version, src.data_ptr()))
+            t = _dev_f32(src.detach(), self.device)
             if t.numel() != L.stts_param_numel(h, i):
                 raise ValueError(f"{name}: numel {t.numel()} != plan {L.stts_param_numel(h, i)}")
             self._keep.append(t)
@@ -193,6 +221,12 @@ class _Engine:
         _watch(module)
 
     def stale(self, module):
+        """True when a bound parameter changed since packing: an in-place update (its _version moved),
+        a move or re-allocation (.to(), .cuda(), a new tensor: data_ptr moved).  Writes through
+        `param.data` bypass the version counter: call `module.invalidate()` after those."""
+        for src, ver, ptr in self.model.sources:
+            if src._version != ver or src.data_ptr() != ptr:
+                return True
         return False
 
 
@@ -214,8 +248,13 @@ class DecoderEngine(_Engine):
         self.model = NativeModel(kind, cfg, module)
         self.model.pack(dtype)
 
-    def forward(self, asr, F0_curve, N, s, noise=None, seed=0, utt_offset=0, out=None):
+    def forward(self, asr, F0_curve, N, s, noise=None, seed=None, utt_offset=0, out=None):
+        """seed None (and no noise): one draw from torch's default generator keys the device noise,
+        so torch.manual_seed governs it and successive calls differ, as the reference's
+        randn_like draws (hifigan.py:213) do."""
         dev = self.model.device
+        if noise is None and seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         in_dev = asr.device if isinstance(asr, torch.Tensor) else torch.device("cpu")
         asr, F0_curve, N, s = (_dev_f32(t, dev) for t in (asr, F0_curve, N, s))
         B, C, T = asr.shape

@@ -83,15 +83,21 @@ class Decoder(nn.Module):
         self._engine = None
 
     # -- HIP path ------------------------------------------------------------------
+    def invalidate(self):
+        """Drop the packed weights (after writes through `param.data`, which stale() cannot see)."""
+        self._engine = None
+
     def engine(self, dtype: str = "fp32"):
         from .engine import DecoderEngine
         if self._engine is None or self._engine.dtype != dtype or self._engine.stale(self):
             self._engine = DecoderEngine(self, dtype=dtype)
         return self._engine
 
-    def forward(self, asr, F0_curve, N, s, noise=None, seed: int = 0, utt_offset: int = 0, dtype: str = "fp32"):
+    def forward(self, asr, F0_curve, N, s, noise=None, seed=None, utt_offset: int = 0, dtype: str = "fp32"):
         """asr [B,512,T], F0_curve [B,2T], N [B,2T], s [B,style_dim] -> [B,1,600T] (float32).
 
         `noise` [B,600T,9] is the reference's randn_like(sine_waves) draw (hifigan.py:213);
-        None draws it on the device from a counter RNG keyed by (seed, utt_offset + b)."""
+        None draws it on the device from a counter RNG keyed by (seed, utt_offset + b, sample,
+        harmonic); seed None takes one draw from torch's default generator (torch.manual_seed
+        governs it and successive calls differ, as the reference's draws do)."""
         return self.engine(dtype).forward(asr, F0_curve, N, s, noise=noise, seed=seed, utt_offset=utt_offset)

@@ -111,11 +111,15 @@ class Decoder(nn.Module):
                                    gen_istft_hop_size)
         self._engine = None
 
+    def invalidate(self):
+        """Drop the packed weights (after writes through `param.data`, which stale() cannot see)."""
+        self._engine = None
+
     def engine(self, dtype: str = "fp32"):
         from .engine import DecoderEngine
         if self._engine is None or self._engine.dtype != dtype or self._engine.stale(self):
             self._engine = DecoderEngine(self, dtype=dtype)
         return self._engine
 
-    def forward(self, asr, F0_curve, N, s, noise=None, seed: int = 0, utt_offset: int = 0, dtype: str = "fp32"):
+    def forward(self, asr, F0_curve, N, s, noise=None, seed=None, utt_offset: int = 0, dtype: str = "fp32"):
         return self.engine(dtype).forward(asr, F0_curve, N, s, noise=noise, seed=seed, utt_offset=utt_offset)

@@ -53,6 +53,10 @@ class ProsodyPredictor(nn.Module):
         self.N_proj = Conv1d(d_hid // 2, 1, 1)
         self._engine = None
 
+    def invalidate(self):
+        """Drop the packed weights (after writes through `param.data`, which stale() cannot see)."""
+        self._engine = None
+
     def f0n_engine(self, dtype="fp32"):
         from .engine import F0NEngine
         if self._engine is None or self._engine.dtype != dtype or self._engine.stale(self):
@@ -121,6 +125,10 @@ class StyleEncoder(nn.Module):
         self.shared = nn.Sequential(*blocks)
         self.unshared = Linear(dim_out, style_dim)
         self.style_dim, self.dims = style_dim, dims
+        self._engine = None
+
+    def invalidate(self):
+        """Drop the packed weights (after writes through `param.data`, which stale() cannot see)."""
         self._engine = None
 
     def engine(self, dtype="fp32"):

@@ -45,6 +45,10 @@ def _L():
         L.stts_bilstm_fwd.restype = c_int
         L.stts_set_lstm_group.argtypes = [c_int]
         L.stts_set_lstm_group.restype = c_int
+        L.stts_bilstm_error_offset.argtypes = [c_int, c_int, c_int]
+        L.stts_bilstm_error_offset.restype = c_ll
+        L.stts_set_bilstm_debug.argtypes = [c_int, c_int]
+        L.stts_set_bilstm_debug.restype = c_int
         L.stts_row_norm.argtypes = [c_vp, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_float,
                                     c_int, c_float, c_vp, c_vp, c_int, c_vp, c_ll, c_ll, c_vp]
         L.stts_row_norm.restype = c_int
@@ -65,6 +69,31 @@ def set_lstm_group(bg: int) -> None:
     """BiLSTM recurrence kernel: 0 = automatic, -1 = cooperative (H = 256), 1 / 2 / 4 = utterances per
     workgroup of the per-workgroup kernel (A/B testing)."""
     check(_L().stts_set_lstm_group(int(bg)), "stts_set_lstm_group")
+
+
+def set_bilstm_debug(spin_limit: int = 0, drop: bool = False) -> None:
+    """Testing hook of the cooperative recurrence (stts_set_bilstm_debug): waits give up after
+    `spin_limit` polls (0 = the default bound) and, with `drop`, one workgroup never publishes."""
+    check(_L().stts_set_bilstm_debug(int(spin_limit), 1 if drop else 0), "stts_set_bilstm_debug")
+
+
+# device error words of BiLSTM launches not yet read by the host (stts_bilstm_error_offset)
+_PENDING: list = []
+
+
+def check_pending() -> None:
+    """Read the error words of every BiLSTM launch since the last check (one host sync) and raise
+    if a cooperative recurrence timed out (its outputs are then NaN).  Synthesizer calls this at the
+    host syncs the reference path already makes (the alignment width, the returned audio)."""
+    global _PENDING
+    if not _PENDING:
+        return
+    pend, _PENDING = _PENDING, []
+    flags = torch.cat([f for _, f in pend]).cpu()
+    bad = [name for (name, _), v in zip(pend, flags.tolist()) if v != 0]
+    if bad:
+        raise RuntimeError(f"stts_bilstm_fwd: the cooperative recurrence timed out waiting for a peer workgroup "
+                           f"({', '.join(bad)}); its outputs are NaN")
 
 
 def _on_device(t: torch.Tensor, what: str) -> torch.Tensor:
@@ -211,6 +240,12 @@ class LSTM(nn.LSTM):
         cn = torch.empty(2, B, H, dtype=torch.float32, device=x.device)
         check(L.stts_bilstm_fwd(_ptr(x), x.stride(0), x.stride(1), x.stride(2), B, T, Cin, _ptr(ln), arr, H, _ptr(y),
                                 _ptr(hn), _ptr(cn), _ptr(ws), nb, _stream()), "stts_bilstm_fwd")
+        off = int(L.stts_bilstm_error_offset(B, T, H))
+        if B > 0 and off >= 0:
+            if len(_PENDING) >= 64:  # bound the list for callers that never sync through check_pending
+                check_pending()
+            # a 4-byte device copy (async), so the workspace is not kept alive until the check
+            _PENDING.append((f"LSTM({self.input_size}, {H}) B={B} T={T}", ws[off:off + 4].view(torch.int32).clone()))
         return y, (hn, cn)
 
 

@@ -14,6 +14,16 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long CPU test")
 
 
+@pytest.fixture(autouse=True)
+def _production_options():
+    """Every test starts and ends on the production engine options (STTS_OPT_* defaults,
+    automatic BiLSTM kernel choice): an A/B test cannot leak its setting into later tests."""
+    from stts2_mi355x import engine
+    engine.reset_options()
+    yield
+    engine.reset_options()
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")

@@ -298,3 +298,67 @@ def test_lstm_cooperative_many_utterances():
     finally:
         set_lstm_group(0)
     assert _err(got, alt.cpu().numpy()) < 1e-5
+
+
+def test_generate_vs_oracle(mods):
+    """StyleTTS2.generate (inference.py:303-319) on the drop-ins: three sentences with prev_d_mean
+    chained from one to the next, each trimmed by 4000 samples at both ends, concatenated and padded,
+    against the oracle's restatement of the same loop (fp32, waveform tolerance 1e-3)."""
+    from helpers import make_decoder
+    from stts2_mi355x.inference import Synthesizer
+    te, pp = mods
+    dec, cfg = make_decoder("hifigan")
+    sents = [[int(v) for v in (synth.hash_u01(f"gen:tok:{i}", n) * 177 + 1)] for i, n in enumerate((18, 9, 26))]
+    s = torch.from_numpy(synth.normal("gen:s", (1, 128)))
+    zs = [torch.from_numpy(synth.normal(f"gen:z:{i}", (1, len(t) + 2))) for i, t in enumerate(sents)]
+    nfs = [(lambda F, i=i: torch.from_numpy(synth.source_noise(1, 600 * F, tag=f"gen{i}"))) for i in range(3)]
+    cpu = lambda m: {k: v.cpu() for k, v in m.state_dict().items()}  # noqa: E731
+    want = orc.generate(sents, s, cpu(te), cpu(pp), cpu(dec), cfg, zs, nfs, stabilize=True)
+    syn = Synthesizer(te, pp, dec.cuda())
+    got = syn.generate(sents, {"style": s.cuda(), "speed": 1}, stabilize=True, z=[z.cuda() for z in zs],
+                       noise=[(lambda F, f=f: f(F).cuda()) for f in nfs])
+    assert got.shape == want.shape
+    assert np.all(got[:4000] == 0) and np.all(got[-4000:] == 0)
+    err = float(np.abs(got - want).max())
+    print(f"generate: {len(sents)} sentences, {got.shape[0]} samples, max-abs vs oracle {err:.3e}")
+    assert err < 1e-3
+
+
+def test_generate_text_path_and_rng(mods):
+    """generate(text) splits and merges sentences as Preprocess.text_preprocess does, tokenizes each,
+    and draws its noise from torch's generator: reproducible under torch.manual_seed."""
+    from helpers import make_decoder
+    from stts2_mi355x.inference import Synthesizer, TextCleaner
+    te, pp = mods
+    dec, _ = make_decoder("hifigan")
+    table = {ch: i + 1 for i, ch in enumerate("abcdefghijklmnopqrstuvwxyz ,.")}
+    syn = Synthesizer(te, pp, dec.cuda(), tokenize=TextCleaner(table))
+    text = "one two three four. five six seven eight nine ten eleven twelve thirteen; fourteen"
+    style = {"style": torch.from_numpy(synth.normal("gen:s2", (1, 128))).cuda(), "speed": 1.0}
+    torch.manual_seed(5)
+    a = syn.generate(text, style, n_merge=4)
+    torch.manual_seed(5)
+    b = syn.generate(text, style, n_merge=4)
+    assert np.array_equal(a, b) and a.shape[0] > 8000 and np.isfinite(a).all()
+
+
+def test_lstm_cooperative_timeout_raises():
+    """A peer workgroup that never publishes its h (debug hook) makes every wait of the cooperative
+    recurrence time out: the kernel terminates, poisons y / h_n / c_n with NaN from that step on, and
+    the host raises at its next check instead of returning NaN audio silently."""
+    from stts2_mi355x import prosody
+    torch.manual_seed(13)
+    lstm = LSTM(40, 256, 1, batch_first=True, bidirectional=True).cuda()
+    x = torch.randn(1, 6, 40).cuda()
+    prosody.check_pending()
+    prosody.set_lstm_group(-1)
+    prosody.set_bilstm_debug(spin_limit=4000, drop=True)
+    y, (hn, cn) = lstm(x)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="timed out"):
+        prosody.check_pending()
+    assert torch.isnan(y[:, 1:]).all() and torch.isnan(hn).all() and torch.isnan(cn).all()
+    prosody.set_bilstm_debug(0, False)
+    y2, _ = lstm(x)  # healthy again, and the check passes
+    prosody.check_pending()
+    assert torch.isfinite(y2).all()

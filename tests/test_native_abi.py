@@ -150,3 +150,22 @@ def test_duration_modules_keep_reference_keys():
         assert k in pk, k
     with pytest.raises(RuntimeError):
         te(torch.zeros(1, 4, dtype=torch.long), torch.tensor([4]))
+
+
+def test_option_defaults_are_the_documented_ones():
+    """engine.OPT_DEFAULTS (what tests restore) equals the library's own production defaults."""
+    from stts2_mi355x import engine
+    engine.reset_options()
+    for k, v in engine.OPT_DEFAULTS.items():
+        assert engine.get_option(k) == v, (k, engine.get_option(k), v)
+    assert engine.lib().stts_get_option(999) < 0
+
+
+def test_bilstm_error_word_offset():
+    """The BiLSTM error word lies inside the workspace, 8-byte aligned, before the exchange words."""
+    from stts2_mi355x import prosody
+    L = prosody._L()
+    for B, T, H in ((1, 5, 256), (4, 37, 256), (32, 400, 256), (3, 7, 64)):
+        off = L.stts_bilstm_error_offset(B, T, H)
+        assert 0 < off and off % 8 == 0 and off + 8 <= L.stts_bilstm_workspace_bytes(B, T, H)
+    assert L.stts_bilstm_error_offset(-1, 1, 1) < 0
