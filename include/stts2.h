@@ -207,6 +207,9 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_SMALL_TILES 1 (default) = implicit-GEMM launches that would make fewer than half as many
  *                     256 x 128 tiles as there are CUs use 64 x 128 tiles; 0 = off (A/B). */
 #define STTS_OPT_SMALL_TILES 6
+/*   STTS_OPT_BIGCONV  2 (default) = the C = 128 / 256 resblock convs run on bigconv2.hip (per-wave
+ *                     LDS-DMA weight rings, one barrier per 32-channel group); 1 = bigconv.hip (A/B). */
+#define STTS_OPT_BIGCONV 7
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

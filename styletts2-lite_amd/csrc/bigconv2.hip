@@ -1,0 +1,517 @@
+// Resblock conv engine v2 for the wide generator stages (C = 128 / 256; MFMA-bound): the dilated
+// Conv1d(C, C, K, dilation d, padding d(K-1)/2) of every AdaINResBlock1 iteration
+// (Modules/hifigan.py:26-80, forward :65-74) with the AdaIN -> Snake prologue and the bias /
+// residual / resblock-average / InstanceNorm-statistics epilogue fused.  bf16 storage,
+// v_mfma_f32_32x32x16_bf16, fp32 accumulation.
+//
+// Why a v2: v1 staged weights and windows through registers shared by all 8 waves,
+// so every step needed a workgroup barrier, 256 VGPRs held staging copies, and the measured
+// phases (MFMA issue, weight staging, window staging) added up instead of overlapping.
+//
+// Layout of the work:
+//   * 8 waves; wave w owns 32 output channels (co block w % (C/32)) x 256 frames (frame half
+//     w / (C/32)): a tile is 256 (C = 256) or 512 (C = 128) frames x C channels, 128 fp32
+//     accumulator registers per lane.  Weight bytes are not duplicated across waves.
+//   * Weights: each wave streams ITS OWN 2 KB slice per step (32 co x 32 ci of one tap, the
+//     packed layout's contiguous block, already XOR-swizzled at pack time) by LDS-DMA into a
+//     private 3-slot ring, two steps ahead.  A wave waits only on its own vmcnt: no barrier.
+//   * Window: the raw bf16 window of the next 32-channel group (tile rows + halo) is LDS-DMA'd
+//     into the other half of a 2-buffer ring at the start of a group, and transformed IN PLACE
+//     (AdaIN -> Snake -> bf16, zero outside the utterance) by the lane that DMA'd it (so only
+//     that wave's vmcnt orders it), during the group's last tap.  One raw s_barrier per group
+//     (K steps) publishes it; DMAs stay in flight across it (counted vmcnt, never 0 in the loop).
+//   * Epilogue per tile from the accumulators: + residual, * out_scale, resblock average,
+//     bf16 stores, per-lane statistics reduced across the wave and added into LDS, flushed to
+//     the fp64 statistics when the workgroup leaves an utterance.
+#include "common.h"
+#include "conv_common.h"
+#include "kernels.h"
+
+namespace {
+
+template <int C, int NW, int K, int DIL>
+struct B2 {
+  static constexpr int NCBW = (C / 32 < NW) ? C / 32 : NW;  // 32-channel output blocks per block tile
+  static constexpr int FH = NW / NCBW;   // frame halves per tile (waves per co block)
+  static constexpr int NCO = 32 * NCBW;  // output channels per tile
+  static constexpr int NCH = C / NCO;    // output-channel parts per frame tile (tiles per frame range)
+  static constexpr int TM = 256 * FH;    // tile rows (frames)
+  static constexpr int NG = C / 32;      // 32-channel input groups per tile
+  static constexpr int PAD = DIL * (K - 1) / 2;
+  static constexpr int R = TM + DIL * (K - 1);                    // window rows a group needs
+  static constexpr int NWIN = (R * 4 + 64 * NW - 1) / (64 * NW);  // window DMA instructions per wave per group
+  static constexpr int WROWS = NWIN * NW * 16;                    // rows the waves' DMAs cover
+  // weight prefetch distance (steps): 3 where the LDS allows it (a DMA lands ~1.1 us after issue,
+  // MI355X_MICROARCH.md ldsdma-fill; a step is ~0.5 us of MFMA issue per SIMD)
+  static constexpr int PD_ = 3, RS_ = PD_ + 1;
+  static constexpr int OFF_COEF = 0;                  // [2][5][C] f32 (utterance parity)
+  static constexpr int OFF_BIAS = OFF_COEF + 2 * 5 * C * 4;
+  static constexpr int OFF_ST = OFF_BIAS + C * 4;     // [C][2] f32
+  static constexpr int OFF_W = (OFF_ST + 2 * C * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
+  static constexpr int LDS3 = OFF_W + NW * RS_ * 2048 + 2 * WROWS * 64;
+  static constexpr int BPC = NW == 4 ? 2 : 1;                     // blocks per CU
+  static constexpr int PD = LDS3 * BPC <= 160 * 1024 ? PD_ : 2, RS = PD + 1;
+  static constexpr int OFF_X = OFF_W + NW * RS * 2048; // [2][WROWS][64 B]
+  static constexpr int LDS = OFF_X + 2 * WROWS * 64;
+  static_assert(FH * NCBW == NW && NCH * NCO == C, "wave grid");
+  static_assert(LDS * BPC <= 160 * 1024, "LDS budget");
+  static_assert(K >= PD, "weight prefetch stays within one group");
+  static_assert(OFF_W % 1024 == 0 && OFF_X % 1024 == 0, "DMA bases");
+};
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void barrier_lds() {
+  // publish this wave's LDS writes, then a raw barrier: LDS-DMAs stay in flight across it
+  // (a __syncthreads() would drain vmcnt to 0)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS byte address of a pointer into the kernel's dynamic LDS
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// the five 16-byte coefficient vectors of 4 channels (rows stride_b bytes apart), read and waited
+// for in ONE asm statement: hipcc otherwise drains every in-flight LDS-DMA (vmcnt(0)) before these
+// reads, which are disjoint from every DMA destination
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_coef5(unsigned a, f32x4v& c0, f32x4v& c1, f32x4v& c2, f32x4v& c3, f32x4v& c4,
+                                          unsigned stride) {
+  const unsigned a1 = a + stride, a2 = a + 2 * stride, a3 = a + 3 * stride, a4 = a + 4 * stride;
+  asm volatile(
+      "ds_read_b128 %0, %5\n\t"
+      "ds_read_b128 %1, %6\n\t"
+      "ds_read_b128 %2, %7\n\t"
+      "ds_read_b128 %3, %8\n\t"
+      "ds_read_b128 %4, %9\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3), "=&v"(c4)
+      : "v"(a), "v"(a1), "v"(a2), "v"(a3), "v"(a4)
+      : "memory");
+}
+
+// an LDS store hipcc cannot see: it drains every in-flight LDS-DMA (vmcnt(0)) before a visible
+// ds_write, although the window units written here are never a pending DMA's destination (their
+// own DMA was waited for by vm_wait)
+__device__ __forceinline__ void lds_write_b64(unsigned a, const uint2& v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void bf4_to_f32(const uint2& r, float (&v)[4]) {
+  v[0] = __uint_as_float(r.x << 16);
+  v[1] = __uint_as_float(r.x & 0xffff0000u);
+  v[2] = __uint_as_float(r.y << 16);
+  v[3] = __uint_as_float(r.y & 0xffff0000u);
+}
+__device__ __forceinline__ uint2 f32_to_bf4(const float (&v)[4]) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = (bf16_t)v[j];
+  uint2 r;
+  __builtin_memcpy(&r, &o, 8);
+  return r;
+}
+__device__ __forceinline__ void bf8_to_f32v(const uint4& r, float* v) {
+  const unsigned w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 f32_to_bf8v(const float* v) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16_t)v[j];
+  uint4 r;
+  __builtin_memcpy(&r, &o, 16);
+  return r;
+}
+__device__ __forceinline__ void bstore16(Rsrc r, unsigned off, const uint4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) unsigned*>(&v),
+                                         r, (int)off, 0, 0);
+}
+
+template <int C, int NW, int K, int DIL, bool RES, bool ACC>
+__global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
+  using G = B2<C, NW, K, DIL>;
+  constexpr int NG = G::NG, TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
+  constexpr int NT = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* coef = reinterpret_cast<float*>(smem + G::OFF_COEF);
+  float* bias_s = reinterpret_cast<float*>(smem + G::OFF_BIAS);
+  float* st_lds = reinterpret_cast<float*>(smem + G::OFF_ST);
+
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+  const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index, provably uniform
+  const int cb = wu % G::NCBW, fh = wu / G::NCBW;
+  const int ntm = (p.Lq + TM - 1) / TM;
+  // tile t -> utterance t / (NCH ntm), output-channel part (t / ntm) % NCH, frame tile t % ntm
+  const long long total = (long long)ntm * NCH * p.B;
+  const int upb = ntm * NCH;  // tiles per utterance
+  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
+  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
+  if (tbeg >= tend) return;  // uniform over the block
+  const int NGG = (tend - tbeg) * NG;  // groups this block walks
+  const int NS = NGG * K;              // steps
+  const bool want_stats = !ACC && p.stats != nullptr;
+
+  for (int i = tid; i < C; i += NT) {
+    bias_s[i] = p.bias ? p.bias[i] : 0.f;
+    st_lds[2 * i] = st_lds[2 * i + 1] = 0.f;
+  }
+
+  // ---------------- weights: step s = (group, tap) -> this wave's 2 KB slice, slot s % RS
+  char* wring = smem + G::OFF_W + wu * RS * 2048;
+  const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)NG * K * C * 32 * 2));
+  auto issue_w = [&](int s) __attribute__((always_inline)) {
+    const int sc = s < NS ? s : NS - 1;  // past the end: a harmless reload keeps the counts uniform
+    const int gq = sc / K, t = sc - gq * K, gi = gq % NG;
+    const int ch = NCH > 1 ? ((tbeg + gq / NG) / ntm) % NCH : 0;
+    const unsigned base = (unsigned)((((size_t)gi * K + t) * C + ch * NCO + 32 * cb) * 64) + lane * 16;
+    char* dst = wring + (s % RS) * 2048;
+    glds16(rw, dst, base);
+    glds16(rw, dst + 1024, base + 1024);
+  };
+
+  // ---------------- window: group gg -> raw rows [gr0, gr0 + WROWS) of its 32 channels, buffer gg & 1
+  // LDS unit pidx = row * 4 + u' holds logical 16-B unit u = u' ^ ((row >> 2) & 3) of that row
+  auto issue_x = [&](int gg) __attribute__((always_inline)) {
+    const int gc = gg < NGG ? gg : NGG - 1;
+    const int t = tbeg + gc / NG, gi = gc % NG;
+    const int b = t / upb, mt = t % ntm;
+    const Rsrc rx = make_rsrc(reinterpret_cast<const bf16_t*>(p.x) + (size_t)b * p.x_bs,
+                              (unsigned)((size_t)p.Lin * p.x_ld * 2));
+    const int gr0 = mt * TM - G::PAD;
+    char* dst = smem + G::OFF_X + (gg & 1) * (G::WROWS * 64);
+#pragma unroll
+    for (int j = 0; j < NWIN; ++j) {
+      const int pidx = (j * NW + wu) * 64 + lane;
+      const int r = pidx >> 2, u = (pidx & 3) ^ ((r >> 2) & 3);
+      const int e = (gr0 + r) * p.x_ld + gi * 32 + 8 * u;
+      glds16(rx, dst + (j * NW + wu) * 1024, e >= 0 ? (unsigned)e * 2u : OOB);
+    }
+  };
+  // AdaIN + Snake coefficients of utterance b into parity slot b & 1 (see bigconv.hip)
+  auto set_coef = [&](int b) __attribute__((always_inline)) {
+    float* cf = coef + (b & 1) * 5 * C;
+    for (int ci = tid; ci < C; ci += NT) {
+      float mm, aa, be;
+      adain_coeffs(p.pro, b, ci, mm, aa, be);
+      const float al = p.pro.alpha[ci];
+      const float m1 = be - mm * aa, ia2 = 0.5f / al, alr = al * 0.31830988618379067f;
+      cf[ci] = m1 + ia2;
+      cf[C + ci] = aa;
+      cf[2 * C + ci] = aa * alr;
+      cf[3 * C + ci] = m1 * alr;
+      cf[4 * C + ci] = -ia2;
+    }
+  };
+  // in-place transform of the units this lane DMA'd for group gg: x -> AdaIN -> Snake -> bf16
+  // (Snake via sin^2(u) = (1 - cos 2u) / 2 on the hardware cosine, as resconv.hip), 0 outside [0, Lin)
+  const int my_u = (lane & 3) ^ ((lane >> 4) & 3);  // the lane's logical unit: the same in every row it owns
+  auto transform = [&](int gg) __attribute__((always_inline)) {
+    const int gc = gg < NGG ? gg : NGG - 1;
+    const int t = tbeg + gc / NG, gi = gc % NG;
+    const int b = t / upb, mt = t % ntm;
+    const int gr0 = mt * TM - G::PAD;
+    const float* cf = coef + (b & 1) * 5 * C + gi * 32 + 8 * my_u;
+    char* buf = smem + G::OFF_X + (gg & 1) * (G::WROWS * 64);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4v m2, a, ar, mr, nia;
+      lds_coef5(lds_addr(cf + 4 * h), m2, a, ar, mr, nia, (unsigned)(C * 4));
+      const float am[4] = {m2.x, m2.y, m2.z, m2.w}, aa[4] = {a.x, a.y, a.z, a.w};
+      const float aar[4] = {ar.x, ar.y, ar.z, ar.w}, amr[4] = {mr.x, mr.y, mr.z, mr.w};
+      const float ani[4] = {nia.x, nia.y, nia.z, nia.w};
+#pragma unroll
+      for (int j = 0; j < NWIN; ++j) {
+        const int pidx = (j * NW + wu) * 64 + lane;
+        const int r = pidx >> 2;
+        uint2* ptr = reinterpret_cast<uint2*>(buf + pidx * 16 + 8 * h);
+        float v[4];
+        bf4_to_f32(*ptr, v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x2 = __builtin_fmaf(v[e], aa[e], am[e]);
+          const float c = __builtin_amdgcn_cosf(__builtin_fmaf(v[e], aar[e], amr[e]));
+          v[e] = __builtin_fmaf(c, ani[e], x2);
+        }
+        uint2 o = f32_to_bf4(v);
+        if ((unsigned)(gr0 + r) >= (unsigned)p.Lin) o = make_uint2(0u, 0u);
+        lds_write_b64(lds_addr(ptr), o);
+      }
+    }
+  };
+
+  // ---------------- statistics: LDS per-block sums -> fp64 global when the block leaves an utterance
+  auto flush = [&](int b) __attribute__((always_inline)) {
+    for (int ci = tid; ci < C; ci += NT) {
+      double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ci) * 2;
+      atomicAdd(d, (double)st_lds[2 * ci]);
+      atomicAdd(d + 1, (double)st_lds[2 * ci + 1]);
+      st_lds[2 * ci] = st_lds[2 * ci + 1] = 0.f;
+    }
+  };
+
+  f32x16 acc[8];
+  auto epilogue = [&](int tt) __attribute__((always_inline)) {
+    const int b = tt / upb, mt = tt % ntm, ch = NCH > 1 ? (tt / ntm) % NCH : 0;
+    const int q0 = mt * TM + fh * 256 + l32;
+    // the lane's 16 consecutive output channels (packing permutation)
+    const int co0 = ch * NCO + 32 * cb + 16 * hi;
+    const Rsrc ry = make_rsrc(reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs, (unsigned)((size_t)p.Lq * p.y_ld * 2));
+    const Rsrc rr = make_rsrc(RES ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr,
+                              RES ? (unsigned)((size_t)p.Lq * p.res_ld * 2) : 0u);
+    const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const bf16_t*>(p.accb) + (size_t)b * p.acc_bs : nullptr,
+                              ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * 2) : 0u);
+    const float osc = p.out_scale;
+    const float adiv = (ACC && p.acc_div != 0.f) ? 1.0f / p.acc_div : 1.0f;
+    float ts[16], tq[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ts[r] = tq[r] = 0.f;
+    // Fragments in pairs, software-pipelined: the residual / running-sum loads of pair p+2 are in
+    // flight while pair p is finished, so the tile pays ~one load latency instead of four.  The
+    // builtin wait first retires this wave's in-flight weight DMAs in the compiler's own model, so
+    // it counts the loads below precisely (with an LDS-DMA pending it would wait vmcnt(0) at
+    // every use); the empty asm fences pin the issue order (and keep the register budget).
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unconstrained
+    uint4 rl[4][2][2], al[4][2][2];
+    auto load_pair = [&](int pi) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int q = q0 + 32 * (2 * pi + k);
+        if constexpr (RES) {
+          const unsigned er = (unsigned)(q * p.res_ld + co0) * 2u;
+          rl[pi][k][0] = bload16(rr, er);
+          rl[pi][k][1] = bload16(rr, er + 16u);
+        }
+        if constexpr (ACC) {
+          const unsigned ea = (unsigned)(q * p.acc_ld + co0) * 2u;
+          al[pi][k][0] = bload16(ra, ea);
+          al[pi][k][1] = bload16(ra, ea + 16u);
+        }
+      }
+    };
+    auto finish_pair = [&](int pi) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        f32x16& v = acc[2 * pi + k];  // in place: the accumulators of a finished tile are the output
+        const int q = q0 + 32 * (2 * pi + k);
+        if constexpr (RES) {
+          float r0[16];
+          bf8_to_f32v(rl[pi][k][0], r0);
+          bf8_to_f32v(rl[pi][k][1], r0 + 8);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = (v[r] + r0[r]) * osc;
+        }
+        if constexpr (ACC) {
+          float a0[16];
+          bf8_to_f32v(al[pi][k][0], a0);
+          bf8_to_f32v(al[pi][k][1], a0 + 8);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = (a0[r] + v[r]) * adiv;
+        }
+        const unsigned ey = (unsigned)(q * p.y_ld + co0) * 2u;
+        float o[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] = v[r];
+        bstore16(ry, ey, f32_to_bf8v(o));  // rows past Lq fall outside the descriptor: dropped
+        bstore16(ry, ey + 16u, f32_to_bf8v(o + 8));
+        if (!ACC) {
+          const float m = q < p.Lq ? 1.f : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float x = v[r] * m;
+            ts[r] += x;
+            tq[r] = __builtin_fmaf(x, x, tq[r]);
+          }
+        }
+      }
+    };
+    load_pair(0);
+    load_pair(1);
+    asm volatile("" ::: "memory");
+    finish_pair(0);
+    asm volatile("" ::: "memory");
+    load_pair(2);
+    asm volatile("" ::: "memory");
+    finish_pair(1);
+    asm volatile("" ::: "memory");
+    load_pair(3);
+    asm volatile("" ::: "memory");
+    finish_pair(2);
+    asm volatile("" ::: "memory");
+    finish_pair(3);
+    if (want_stats) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float a = ts[r], q = tq[r];
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) {
+          a += __shfl_xor(a, o);
+          q += __shfl_xor(q, o);
+        }
+        if (l32 == 0) {
+          atomicAdd(st_lds + 2 * (co0 + r), a);
+          atomicAdd(st_lds + 2 * (co0 + r) + 1, q);
+        }
+      }
+    }
+  };
+
+  // ---------------- one tap: weights of step s (slot s % RS), window of group gg (buffer gg & 1)
+  const int swz = (l32 >> 2) & 3;
+  auto mfma_tap = [&](int gg, int t, int s) __attribute__((always_inline)) {
+    const char* ws = wring + (s % RS) * 2048 + l32 * 64;
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(ws + ((hi) ^ swz) * 16);
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(ws + ((2 + hi) ^ swz) * 16);
+    const int r0 = fh * 256 + l32 + t * DIL;
+    const int sx = (r0 >> 2) & 3;  // rows r0 + 32 f share it
+    const char* row = smem + G::OFF_X + (gg & 1) * (G::WROWS * 64) + r0 * 64;
+    const int u0 = (hi ^ sx) * 16, u1 = ((2 + hi) ^ sx) * 16;
+    // all eight B fragments of the first 16 channels up front (LDS latency covered by 8 reads in
+    // flight), the second half's reads interleaved with the first half's MFMAs
+    // (sched_barrier: hipcc otherwise re-sequences to two reads in flight, exposing LDS latency)
+    bf16x8 b0[8], b1[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) b0[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) b1[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u1);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0[f], acc[f], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1[f], acc[f], 0, 0, 0);
+  };
+
+  // ---------------- prologue: coefficients, group 0's window transformed, weights of steps 0..PD-1
+  int cur_b = tbeg / upb;
+  set_coef(cur_b);
+  __syncthreads();  // nothing in flight yet
+  issue_x(0);
+#pragma unroll
+  for (int s = 0; s < PD; ++s) issue_w(s);
+  vm_wait<2 * PD>();  // this wave's window DMA of group 0 landed
+  transform(0);
+
+  // ---------------- main loop: one iteration per 32-channel group; K taps unrolled
+  for (int gg = 0; gg < NGG; ++gg) {
+    barrier_lds();  // group gg's window transformed by every wave; group gg-1's reads all done
+    const int tl = gg / NG, gi = gg - tl * NG, tt = tbeg + tl;
+    if (gi == 0) {
+      const int b = tt / upb;
+      if (b != cur_b) {  // the block left utterance cur_b: every epilogue of it ran >= 1 barrier ago
+        if (want_stats) flush(cur_b);
+        cur_b = b;
+      }
+      // the next tile opens another utterance: its coefficients, first read by the transform of its
+      // group 0 during this tile's last group, >= 1 barrier from here (NG >= 4)
+      if (tt + 1 < tend && (tt + 1) / upb != b) set_coef((tt + 1) / upb);
+      const int co0 = (NCH > 1 ? ((tt / ntm) % NCH) * NCO : 0) + 32 * cb + 16 * hi;
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {  // the accumulators start at the bias
+        float bb[16];
+        ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
+        ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[f][r] = bb[r];
+      }
+    }
+    issue_x(gg + 1);  // the next group's raw window: buffer (gg+1)&1, whose last reads were group gg-1's
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int s = gg * K + t;
+      // this wave's weights of step s: issued PD steps ago; younger VMEM ops since then are the
+      // weight DMAs of the steps between and, when step s-PD was in the previous group, this group's
+      // NWIN window DMAs (an epilogue's loads / stores in between are younger still: over-waiting)
+      if (t >= PD) vm_wait<2 * (PD - 1)>();
+      else vm_wait<2 * (PD - 1) + NWIN>();
+      issue_w(s + PD);  // into slot (s+PD) % RS = (s-1) % RS, whose reads (step s-1) are done
+      mfma_tap(gg, t, s);
+      if (t == K - 1) {
+        vm_wait<2 * K>();  // this wave's window DMAs of group gg+1 (older than the K taps' weight DMAs)
+        transform(gg + 1);
+      }
+    }
+    if (gi == NG - 1) epilogue(tt);
+  }
+  vm_wait<0>();  // nothing may land in LDS after the block's exit
+  barrier_lds();
+  if (want_stats) flush(cur_b);
+}
+
+template <int C, int NW, int K, int DIL, bool RES, bool ACC>
+int launch_b2(const ConvParams& p, hipStream_t stream) {
+  using G = B2<C, NW, K, DIL>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC>;
+  static bool attr = false;
+  if (!attr) {
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    attr = true;
+  }
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    ST_CHECK_HIP(hipGetDevice(&dev));
+    ST_CHECK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const long long tiles = (long long)((p.Lq + G::TM - 1) / G::TM) * G::NCH * p.B;
+  long long grid = (long long)ncu * G::BPC;
+  if (grid > tiles) grid = tiles;
+  if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), G::LDS, stream, p);
+  return (int)hipGetLastError();
+}
+
+template <int C, int NW, int K>
+int launch_b2_k(const ConvParams& p, hipStream_t s) {
+  if (!p.res) {  // conv1 of an iteration: dilation 1 / 3 / 5, no residual
+    if (p.accb) return ST_EINVAL;
+    switch (p.dil) {
+      case 1: return launch_b2<C, NW, K, 1, false, false>(p, s);
+      case 3: return launch_b2<C, NW, K, 3, false, false>(p, s);
+      case 5: return launch_b2<C, NW, K, 5, false, false>(p, s);
+      default: return ST_EINVAL;
+    }
+  }
+  if (p.dil != 1) return ST_EINVAL;  // conv2: dilation 1, residual, optionally the resblock sum
+  return p.accb ? launch_b2<C, NW, K, 1, true, true>(p, s) : launch_b2<C, NW, K, 1, true, false>(p, s);
+}
+
+template <int C, int NW>
+int launch_b2_c(const ConvParams& p, hipStream_t s) {
+  switch (p.KS) {
+    case 3: return launch_b2_k<C, NW, 3>(p, s);
+    case 7: return launch_b2_k<C, NW, 7>(p, s);
+    case 11: return launch_b2_k<C, NW, 11>(p, s);
+    default: return ST_EINVAL;
+  }
+}
+
+}  // namespace
+
+// STTS_OPT_BIGCONV: 1 = bigconv.hip (v1, A/B); 2 = this engine, 8-wave blocks (one per CU);
+// 3 = this engine, 4-wave blocks (two per CU, C = 256 split into two 128-channel output parts)
+int g_opt_bigconv = 2;
+
+bool st_bigconv2_eligible(const ConvParams& p) {
+  if (g_opt_bigconv < 2) return false;
+  if (p.res ? p.dil != 1 : (p.accb != nullptr)) return false;
+  return true;  // on top of st_bigconv_eligible
+}
+
+int st_bigconv2(const ConvParams& p, hipStream_t stream) {
+  const bool two = g_opt_bigconv == 3;
+  if (p.Cout == 128) return two ? launch_b2_c<128, 4>(p, stream) : launch_b2_c<128, 8>(p, stream);
+  if (p.Cout == 256) return two ? launch_b2_c<256, 4>(p, stream) : launch_b2_c<256, 8>(p, stream);
+  return ST_EINVAL;
+}

@@ -75,6 +75,11 @@ extern int g_opt_debug;     // resconv phase-skipping knob (timing experiments o
 // wide-stage resblock conv engine (bigconv.hip): bf16, C = 128 / 256, same contract
 bool st_bigconv_eligible(const ConvParams& p, int dtype);
 int st_bigconv(const ConvParams& p, hipStream_t stream);
+// v2 of that engine (bigconv2.hip: per-wave LDS-DMA weight rings, in-place window transform, one
+// barrier per 32-channel group); st_bigconv routes to it while g_opt_bigconv == 2 (the default)
+bool st_bigconv2_eligible(const ConvParams& p);
+int st_bigconv2(const ConvParams& p, hipStream_t stream);
+extern int g_opt_bigconv;
 
 // fused AdaINResBlock1 iteration (resfused.hip): bf16, C = 32 (K = 3/7/11) or 64 (K = 3).
 //   y = conv2(Snake2(AdaIN2(conv1(Snake1(AdaIN1(x)))))) + x     (hifigan.py:65-74)

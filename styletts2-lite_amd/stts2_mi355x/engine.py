@@ -89,9 +89,10 @@ OPT_STATS_SLOTS = 5
 
 
 OPT_SMALL_TILES = 6
+OPT_BIGCONV = 7
 # the production defaults of every STTS_OPT_* (include/stts2.h)
 OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
-                OPT_SMALL_TILES: 1}
+                OPT_SMALL_TILES: 1, OPT_BIGCONV: 2}
 
 
 def set_option(key: int, value: int) -> None:
@@ -253,8 +254,8 @@ class DecoderEngine(_Engine):
         so torch.manual_seed governs it and successive calls differ, as the reference's
         randn_like draws (hifigan.py:213) do."""
         dev = self.model.device
-        if noise is None and seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if noise is None else 0
         in_dev = asr.device if isinstance(asr, torch.Tensor) else torch.device("cpu")
         asr, F0_curve, N, s = (_dev_f32(t, dev) for t in (asr, F0_curve, N, s))
         B, C, T = asr.shape

@@ -26,6 +26,11 @@ CASES = [
     ("rb128_k11_d5", 128, 128, 11, 0, 1, 5, 25, 0, 777, 3),
     ("rb256_k3_d5", 256, 256, 3, 0, 1, 5, 5, 0, 600, 3),
     ("rb256_k7_d1", 256, 256, 7, 0, 1, 1, 3, 0, 513, 3),
+    # conv1 of a resblock iteration: no residual (bigconv2 RES = false), dilated
+    ("rb256_k3_d3_nores", 256, 256, 3, 0, 1, 3, 3, 0, 700, 3),
+    ("rb256_k11_d5_nores", 256, 256, 11, 0, 1, 5, 25, 0, 300, 3),
+    ("rb128_k11_d5_nores", 128, 128, 11, 0, 1, 5, 25, 0, 1500, 3),
+    ("rb128_k7_d1_nores", 128, 128, 7, 0, 1, 1, 3, 0, 511, 3),
     ("front_1090_1024", 1090, 1024, 3, 0, 1, 1, 1, 0, 40, 5),
     ("sc_1x1", 514, 1024, 1, 0, 1, 1, 0, 0, 37, 0),
     ("istft_noise_s6", 22, 256, 12, 0, 6, 1, 3, 0, 481, 0),
@@ -71,7 +76,7 @@ def run_case(case, dtype):
     alpha = torch.rand(Cin, generator=g) + 0.5
     slope = 0.2
     Lout = (L - 1) * st - 2 * pad + K + op if tr else (L + 2 * pad - dil * (K - 1) - 1) // st + 1
-    res = torch.randn(B, Lout, Cout, generator=g) if not tr else None
+    res = torch.randn(B, Lout, Cout, generator=g) if not tr and not name.endswith("_nores") else None
     scale = 0.70710677 if res is not None else 1.0
     ref = reference(x, w, b, gb, alpha, slope, res, scale, case)
     dev = "cuda"
@@ -126,6 +131,28 @@ def test_resconv_engine_matches_general_engine(case):
     err = (y1 - y0).abs().max().item()
     assert err <= 2 ** -7 * scale, f"{case[0]}: engines differ by {err}"
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
+
+
+WIDE_CASES = [c for c in RB_CASES if c[1] in (128, 256)]
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("case", WIDE_CASES, ids=[c[0] for c in WIDE_CASES])
+def test_bigconv_v2_matches_v1(case, mode):
+    """bf16: the C = 128 / 256 resblock engine v2 (bigconv2.hip; mode 2 = 8-wave blocks, mode 3 =
+    4-wave blocks two per CU) against v1 (bigconv.hip) on the same launch: same bf16 operands and
+    transform, fp32 accumulation in a different order, statistics from the fp32 epilogue values."""
+    try:
+        E.set_option(E.OPT_BIGCONV, 1)
+        _, y1, s1 = run_case(case, "bf16")
+        E.set_option(E.OPT_BIGCONV, mode)
+        _, y2, s2 = run_case(case, "bf16")
+    finally:
+        E.reset_options()
+    scale = max(1.0, y1.abs().max().item())
+    err = (y2 - y1).abs().max().item()
+    assert err <= 2 ** -7 * scale, f"{case[0]}: bigconv v2 vs v1 differ by {err}"
+    np.testing.assert_allclose(s2.numpy(), s1.numpy(), rtol=1e-4, atol=1e-2)
 
 
 @pytest.mark.parametrize("case", RB_CASES, ids=[c[0] for c in RB_CASES])

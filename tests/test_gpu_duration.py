@@ -357,7 +357,9 @@ def test_lstm_cooperative_timeout_raises():
     torch.cuda.synchronize()
     with pytest.raises(RuntimeError, match="timed out"):
         prosody.check_pending()
-    assert torch.isnan(y[:, 1:]).all() and torch.isnan(hn).all() and torch.isnan(cn).all()
+    # step 0 of each direction (t = 0 forward, t = T-1 reverse) ran before the failed wait
+    assert torch.isnan(y[:, 1:, :256]).all() and torch.isnan(y[:, :-1, 256:]).all()
+    assert torch.isnan(hn).all() and torch.isnan(cn).all()
     prosody.set_bilstm_debug(0, False)
     y2, _ = lstm(x)  # healthy again, and the check passes
     prosody.check_pending()
