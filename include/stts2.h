@@ -213,6 +213,9 @@ const char* stts_error_string(int code);
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);
+/* Diagnostics (not a product path): a device buffer of >= 16 uint64 that instrumented engines add
+ * per-phase s_memtime cycle sums into (bigconv2.hip: set STTS_OPT_DEBUG bit 64); NULL = off. */
+int stts_set_debug_buffer(void* buf);
 
 /* Optional per-launch timing of the conv engines (conv1d_igemm, resconv, bigconv) with hipEvents
  * recorded on `stream` around each launch: enable, run, then read totals (ms, launches). */

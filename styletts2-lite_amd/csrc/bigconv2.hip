@@ -41,21 +41,24 @@ struct B2 {
   static constexpr int R = TM + DIL * (K - 1);                    // window rows a group needs
   static constexpr int NWIN = (R * 4 + 64 * NW - 1) / (64 * NW);  // window DMA instructions per wave per group
   static constexpr int WROWS = NWIN * NW * 16;                    // rows the waves' DMAs cover
-  // weight prefetch distance (steps): 3 where the LDS allows it (a DMA lands ~1.1 us after issue,
-  // MI355X_MICROARCH.md ldsdma-fill; a step is ~0.5 us of MFMA issue per SIMD)
-  static constexpr int PD_ = 3, RS_ = PD_ + 1;
+  // weight prefetch distance (steps): as deep as the LDS allows, up to K (the waits below assume a
+  // target at most one group back) and 5.  It is also what covers the window DMA: vmcnt retires in
+  // issue order, so the first wait for a weight slice issued after a group's window DMA (PD taps
+  // later) also waits for that window (a DMA lands ~1.1 us after issue, MI355X_MICROARCH.md
+  // ldsdma-fill, later from HBM under load; a tap is ~0.5 us of MFMA issue per SIMD)
   static constexpr int OFF_COEF = 0;                  // [2][5][C] f32 (utterance parity)
   static constexpr int OFF_BIAS = OFF_COEF + 2 * 5 * C * 4;
   static constexpr int OFF_ST = OFF_BIAS + C * 4;     // [C][2] f32
   static constexpr int OFF_W = (OFF_ST + 2 * C * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
-  static constexpr int LDS3 = OFF_W + NW * RS_ * 2048 + 2 * WROWS * 64;
   static constexpr int BPC = NW == 4 ? 2 : 1;                     // blocks per CU
-  static constexpr int PD = LDS3 * BPC <= 160 * 1024 ? PD_ : 2, RS = PD + 1;
+  static constexpr int PDMAX_LDS = ((160 * 1024 / BPC - OFF_W - 2 * WROWS * 64) / (NW * 2048)) - 1;
+  static constexpr int PD0 = PDMAX_LDS < K ? PDMAX_LDS : K;
+  static constexpr int PD = PD0 < 5 ? PD0 : 5, RS = PD + 1;
   static constexpr int OFF_X = OFF_W + NW * RS * 2048; // [2][WROWS][64 B]
   static constexpr int LDS = OFF_X + 2 * WROWS * 64;
   static_assert(FH * NCBW == NW && NCH * NCO == C, "wave grid");
   static_assert(LDS * BPC <= 160 * 1024, "LDS budget");
-  static_assert(K >= PD, "weight prefetch stays within one group");
+  static_assert(K >= PD && PD >= 2, "weight prefetch stays within one group");
   static_assert(OFF_W % 1024 == 0 && OFF_X % 1024 == 0, "DMA bases");
 };
 
@@ -162,6 +165,22 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   const int NGG = (tend - tbeg) * NG;  // groups this block walks
   const int NS = NGG * K;              // steps
   const bool want_stats = !ACC && p.stats != nullptr;
+  // STTS_OPT_DEBUG phase skipping (timing attribution only; outputs are wrong while set):
+  // 1 transform, 4 epilogue, 8 weight DMAs, 16 window DMAs, 32 group barrier (2, MFMAs, is not
+  // honoured: a runtime branch around the pipelined taps keeps their fragments live everywhere)
+  const int dbg = p.dbg;
+  // diagnostics (dbg bit 64 + a debug buffer): per-wave s_memtime sums of the phases below
+  const bool stamp = (dbg & 64) && p.stamps;
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wW wX barrier transform epilogue total mfma issue
+  unsigned long long t_mark = stamp ? __builtin_amdgcn_s_memtime() : 0;
+  auto lap = [&](int k) __attribute__((always_inline)) {
+    if (stamp) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      st_acc[k] += t - t_mark;
+      t_mark = t;
+    }
+  };
+  const unsigned long long t_start = t_mark;
 
   for (int i = tid; i < C; i += NT) {
     bias_s[i] = p.bias ? p.bias[i] : 0.f;
@@ -172,6 +191,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   char* wring = smem + G::OFF_W + wu * RS * 2048;
   const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)NG * K * C * 32 * 2));
   auto issue_w = [&](int s) __attribute__((always_inline)) {
+    if (dbg & 8) return;
     const int sc = s < NS ? s : NS - 1;  // past the end: a harmless reload keeps the counts uniform
     const int gq = sc / K, t = sc - gq * K, gi = gq % NG;
     const int ch = NCH > 1 ? ((tbeg + gq / NG) / ntm) % NCH : 0;
@@ -184,6 +204,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   // ---------------- window: group gg -> raw rows [gr0, gr0 + WROWS) of its 32 channels, buffer gg & 1
   // LDS unit pidx = row * 4 + u' holds logical 16-B unit u = u' ^ ((row >> 2) & 3) of that row
   auto issue_x = [&](int gg) __attribute__((always_inline)) {
+    if (dbg & 16) return;
     const int gc = gg < NGG ? gg : NGG - 1;
     const int t = tbeg + gc / NG, gi = gc % NG;
     const int b = t / upb, mt = t % ntm;
@@ -218,6 +239,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   // (Snake via sin^2(u) = (1 - cos 2u) / 2 on the hardware cosine, as resconv.hip), 0 outside [0, Lin)
   const int my_u = (lane & 3) ^ ((lane >> 4) & 3);  // the lane's logical unit: the same in every row it owns
   auto transform = [&](int gg) __attribute__((always_inline)) {
+    if (dbg & 1) return;
     const int gc = gg < NGG ? gg : NGG - 1;
     const int t = tbeg + gc / NG, gi = gc % NG;
     const int b = t / upb, mt = t % ntm;
@@ -277,120 +299,127 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     float ts[16], tq[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) ts[r] = tq[r] = 0.f;
-    // Fragments in pairs, software-pipelined: the residual / running-sum loads of pair p+2 are in
-    // flight while pair p is finished, so the tile pays ~one load latency instead of four.  The
-    // builtin wait first retires this wave's in-flight weight DMAs in the compiler's own model, so
-    // it counts the loads below precisely (with an LDS-DMA pending it would wait vmcnt(0) at
-    // every use); the empty asm fences pin the issue order (and keep the register budget).
+    // The residual / running-sum loads of a whole batch of fragments go out together (8 fragments
+    // with a residual only, 2 x 4 with a residual and a running sum: the register budget), so a tile
+    // pays one load latency per batch.  The builtin wait first retires this wave's in-flight weight
+    // DMAs in the compiler's own model, so it counts the loads below precisely (with an LDS-DMA
+    // pending it would wait vmcnt(0) at every use); the empty asm fences pin the issue order.
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unconstrained
-    uint4 rl[4][2][2], al[4][2][2];
-    auto load_pair = [&](int pi) __attribute__((always_inline)) {
+    constexpr int NB = RES ? 2 : 1, FB = 8 / NB;
+    uint4 rl[FB][2], al[FB][2];
+    auto finish = [&](int f, const uint4 (&r2)[2], const uint4 (&a2)[2]) __attribute__((always_inline)) {
+      f32x16& v = acc[f];  // in place: the accumulators of a finished tile are the output
+      const int q = q0 + 32 * f;
+      if constexpr (RES) {
+        float r0[16];
+        bf8_to_f32v(r2[0], r0);
+        bf8_to_f32v(r2[1], r0 + 8);
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int q = q0 + 32 * (2 * pi + k);
+        for (int r = 0; r < 16; ++r) v[r] = (v[r] + r0[r]) * osc;
+      }
+      if constexpr (ACC) {
+        float a0[16];
+        bf8_to_f32v(a2[0], a0);
+        bf8_to_f32v(a2[1], a0 + 8);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = (a0[r] + v[r]) * adiv;
+      }
+      const unsigned ey = (unsigned)(q * p.y_ld + co0) * 2u;
+      float o[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] = v[r];
+      bstore16(ry, ey, f32_to_bf8v(o));  // rows past Lq fall outside the descriptor: dropped
+      bstore16(ry, ey + 16u, f32_to_bf8v(o + 8));
+      if (!ACC) {
+        const float m = q < p.Lq ? 1.f : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float x = v[r] * m;
+          ts[r] += x;
+          tq[r] = __builtin_fmaf(x, x, tq[r]);
+        }
+      }
+    };
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+#pragma unroll
+      for (int k = 0; k < FB; ++k) {
+        const int q = q0 + 32 * (nb * FB + k);
         if constexpr (RES) {
           const unsigned er = (unsigned)(q * p.res_ld + co0) * 2u;
-          rl[pi][k][0] = bload16(rr, er);
-          rl[pi][k][1] = bload16(rr, er + 16u);
+          rl[k][0] = bload16(rr, er);
+          rl[k][1] = bload16(rr, er + 16u);
         }
         if constexpr (ACC) {
           const unsigned ea = (unsigned)(q * p.acc_ld + co0) * 2u;
-          al[pi][k][0] = bload16(ra, ea);
-          al[pi][k][1] = bload16(ra, ea + 16u);
+          al[k][0] = bload16(ra, ea);
+          al[k][1] = bload16(ra, ea + 16u);
         }
       }
-    };
-    auto finish_pair = [&](int pi) __attribute__((always_inline)) {
+      asm volatile("" ::: "memory");
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        f32x16& v = acc[2 * pi + k];  // in place: the accumulators of a finished tile are the output
-        const int q = q0 + 32 * (2 * pi + k);
-        if constexpr (RES) {
-          float r0[16];
-          bf8_to_f32v(rl[pi][k][0], r0);
-          bf8_to_f32v(rl[pi][k][1], r0 + 8);
+      for (int k = 0; k < FB; ++k) finish(nb * FB + k, rl[k], al[k]);
+      asm volatile("" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the tile's stores before the reduction: fewer live values
+    if (want_stats) {
+      // reduce-scatter of the lane's 16 partial sums (then squares) over the 32 lanes of its half:
+      // 8 + 4 + 2 + 1 exchanges leave lane l32 with channel co0 + l32 / 2 summed over 16 lanes, one
+      // more exchange with lane l32 ^ 1 completes it; the even lane adds the sum, the odd one the
+      // sum of squares (32 exchanges and one LDS atomic per lane instead of 160 and 32)
+      auto rs16 = [&](float (&v)[16]) __attribute__((always_inline)) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = (v[r] + r0[r]) * osc;
-        }
-        if constexpr (ACC) {
-          float a0[16];
-          bf8_to_f32v(al[pi][k][0], a0);
-          bf8_to_f32v(al[pi][k][1], a0 + 8);
+        for (int m = 16, n = 16; m >= 2; m >>= 1, n >>= 1) {
+          const bool up = (l32 & m) != 0;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = (a0[r] + v[r]) * adiv;
-        }
-        const unsigned ey = (unsigned)(q * p.y_ld + co0) * 2u;
-        float o[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[r] = v[r];
-        bstore16(ry, ey, f32_to_bf8v(o));  // rows past Lq fall outside the descriptor: dropped
-        bstore16(ry, ey + 16u, f32_to_bf8v(o + 8));
-        if (!ACC) {
-          const float m = q < p.Lq ? 1.f : 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float x = v[r] * m;
-            ts[r] += x;
-            tq[r] = __builtin_fmaf(x, x, tq[r]);
+          for (int i = 0; i < n / 2; ++i) {
+            const float send = up ? v[i] : v[i + n / 2];
+            const float keep = up ? v[i + n / 2] : v[i];
+            v[i] = keep + __shfl_xor(send, m);
           }
         }
-      }
-    };
-    load_pair(0);
-    load_pair(1);
-    asm volatile("" ::: "memory");
-    finish_pair(0);
-    asm volatile("" ::: "memory");
-    load_pair(2);
-    asm volatile("" ::: "memory");
-    finish_pair(1);
-    asm volatile("" ::: "memory");
-    load_pair(3);
-    asm volatile("" ::: "memory");
-    finish_pair(2);
-    asm volatile("" ::: "memory");
-    finish_pair(3);
-    if (want_stats) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float a = ts[r], q = tq[r];
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) {
-          a += __shfl_xor(a, o);
-          q += __shfl_xor(q, o);
-        }
-        if (l32 == 0) {
-          atomicAdd(st_lds + 2 * (co0 + r), a);
-          atomicAdd(st_lds + 2 * (co0 + r) + 1, q);
-        }
-      }
+        return v[0] + __shfl_xor(v[0], 1);
+      };
+      const float s1 = rs16(ts);
+      const float s2 = rs16(tq);
+      atomicAdd(st_lds + 2 * (co0 + (l32 >> 1)) + (l32 & 1), (l32 & 1) ? s2 : s1);
     }
   };
 
-  // ---------------- one tap: weights of step s (slot s % RS), window of group gg (buffer gg & 1)
+  // ---------------- MFMA taps, software-pipelined within a group.  Tap t = two 8-MFMA halves (input
+  // channels 0-15 / 16-31 of the group: window fragments fb0 / fb1, weight fragments fa[t & 1][0 / 1]).
+  // While one half's MFMAs issue, the reads of the next half's fragments are in flight (one ds_read
+  // per MFMA gap, forced by sched_group_barrier), so the LDS latency is exposed once per group (its
+  // first tap) instead of twice per tap.
   const int swz = (l32 >> 2) & 3;
-  auto mfma_tap = [&](int gg, int t, int s) __attribute__((always_inline)) {
+  bf16x8 fa[2][2], fb0[8], fb1[8];
+  auto rd_a = [&](int s, bf16x8 (&a)[2]) __attribute__((always_inline)) {
     const char* ws = wring + (s % RS) * 2048 + l32 * 64;
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(ws + ((hi) ^ swz) * 16);
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(ws + ((2 + hi) ^ swz) * 16);
-    const int r0 = fh * 256 + l32 + t * DIL;
-    const int sx = (r0 >> 2) & 3;  // rows r0 + 32 f share it
-    const char* row = smem + G::OFF_X + (gg & 1) * (G::WROWS * 64) + r0 * 64;
-    const int u0 = (hi ^ sx) * 16, u1 = ((2 + hi) ^ sx) * 16;
-    // all eight B fragments of the first 16 channels up front (LDS latency covered by 8 reads in
-    // flight), the second half's reads interleaved with the first half's MFMAs
-    // (sched_barrier: hipcc otherwise re-sequences to two reads in flight, exposing LDS latency)
-    bf16x8 b0[8], b1[8];
+    a[0] = *reinterpret_cast<const bf16x8*>(ws + ((hi) ^ swz) * 16);
+    a[1] = *reinterpret_cast<const bf16x8*>(ws + ((2 + hi) ^ swz) * 16);
+  };
+  auto brow = [&](int gg, int t, int half, int& u) __attribute__((always_inline)) {
+    // an opaque copy of the lane index: the address is computed here, at the tap, instead of being
+    // hoisted out of the loop as K loop-invariant registers (which spill at K = 11)
+    int l = l32;
+    asm volatile("" : "+v"(l));
+    const int r0 = fh * 256 + l + t * DIL;
+    u = ((2 * half + hi) ^ ((r0 >> 2) & 3)) * 16;  // rows r0 + 32 f share the swizzle
+    return smem + G::OFF_X + (gg & 1) * (G::WROWS * 64) + r0 * 64;
+  };
+  auto rd_b = [&](bf16x8 (&fb)[8], int gg, int t, int half) __attribute__((always_inline)) {
+    int u;
+    const char* row = brow(gg, t, half, u);
 #pragma unroll
-    for (int f = 0; f < 8; ++f) b0[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u0);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int f = 0; f < 8; ++f) fb[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
+  };
+  // [MFMA, ds_read] x n in this order
+  auto interleave = [&](int n) __attribute__((always_inline)) {
 #pragma unroll
-    for (int f = 0; f < 8; ++f) b1[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u1);
-#pragma unroll
-    for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0[f], acc[f], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1[f], acc[f], 0, 0, 0);
+    for (int i = 0; i < n; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
   };
 
   // ---------------- prologue: coefficients, group 0's window transformed, weights of steps 0..PD-1
@@ -403,9 +432,25 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   vm_wait<2 * PD>();  // this wave's window DMA of group 0 landed
   transform(0);
 
+  // the accumulators of tile tt start at the bias.  Set right after the previous tile's epilogue
+  // (not at the next group 0), so the compiler sees them dead while that epilogue reduces statistics
+  auto init_acc = [&](int tt) __attribute__((always_inline)) {
+    const int co0 = (NCH > 1 ? ((tt / ntm) % NCH) * NCO : 0) + 32 * cb + 16 * hi;
+    float bb[16];
+    ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
+    ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[f][r] = bb[r];
+  };
+
   // ---------------- main loop: one iteration per 32-channel group; K taps unrolled
+  init_acc(tbeg);
   for (int gg = 0; gg < NGG; ++gg) {
-    barrier_lds();  // group gg's window transformed by every wave; group gg-1's reads all done
+    lap(6);
+    if (!(dbg & 32)) barrier_lds();  // group gg's window transformed by every wave; group gg-1's reads all done
+    lap(2);
     const int tl = gg / NG, gi = gg - tl * NG, tt = tbeg + tl;
     if (gi == 0) {
       const int b = tt / upb;
@@ -416,37 +461,91 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       // the next tile opens another utterance: its coefficients, first read by the transform of its
       // group 0 during this tile's last group, >= 1 barrier from here (NG >= 4)
       if (tt + 1 < tend && (tt + 1) / upb != b) set_coef((tt + 1) / upb);
-      const int co0 = (NCH > 1 ? ((tt / ntm) % NCH) * NCO : 0) + 32 * cb + 16 * hi;
-#pragma unroll
-      for (int f = 0; f < 8; ++f) {  // the accumulators start at the bias
-        float bb[16];
-        ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
-        ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[f][r] = bb[r];
-      }
     }
     issue_x(gg + 1);  // the next group's raw window: buffer (gg+1)&1, whose last reads were group gg-1's
+    // this wave's weights of step gg K: younger VMEM ops are the weight DMAs of the next PD - 1 steps
+    // and the window DMAs just issued
+    lap(6);
+    vm_wait<2 * (PD - 1) + NWIN>();
+    lap(0);
+    rd_a(gg * K, fa[0]);
+    rd_b(fb0, gg, 0, 0);
 #pragma unroll
     for (int t = 0; t < K; ++t) {
       const int s = gg * K + t;
-      // this wave's weights of step s: issued PD steps ago; younger VMEM ops since then are the
-      // weight DMAs of the steps between and, when step s-PD was in the previous group, this group's
-      // NWIN window DMAs (an epilogue's loads / stores in between are younger still: over-waiting)
-      if (t >= PD) vm_wait<2 * (PD - 1)>();
-      else vm_wait<2 * (PD - 1) + NWIN>();
-      issue_w(s + PD);  // into slot (s+PD) % RS = (s-1) % RS, whose reads (step s-1) are done
-      mfma_tap(gg, t, s);
-      if (t == K - 1) {
-        vm_wait<2 * K>();  // this wave's window DMAs of group gg+1 (older than the K taps' weight DMAs)
+      issue_w(s + PD);  // into slot (s+PD) % RS = (s-1) % RS, whose fragments tap s-1 consumed
+      {
+        const bf16x8(&a)[2] = fa[t & 1];
+        // half 0 of tap t; reads of half 1
+        {
+          int u;
+          const char* row = brow(gg, t, 1, u);
+#pragma unroll
+          for (int f = 0; f < 8; ++f) {
+            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], fb0[f], acc[f], 0, 0, 0);
+            fb1[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
+          }
+          interleave(8);
+        }
+        // half 1 of tap t; reads of half 0 of tap t+1 and, once its DMA is in, of its weights
+        if (t + 1 < K) {
+          int u;
+          const char* row = brow(gg, t + 1, 0, u);
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb1[f], acc[f], 0, 0, 0);
+            fb0[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
+          }
+          interleave(4);
+          // weights of step s+1: younger VMEM ops are the weight DMAs of steps s+2..s+PD and, while
+          // step s+1 precedes this group's window DMAs (t + 1 < PD), those
+          lap(6);
+          if (t + 1 < PD) vm_wait<2 * (PD - 1) + NWIN>();
+          else vm_wait<2 * (PD - 1)>();
+          lap(0);
+          rd_a(s + 1, fa[(t + 1) & 1]);
+#pragma unroll
+          for (int f = 4; f < 8; ++f) {
+            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb1[f], acc[f], 0, 0, 0);
+            fb0[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
+          }
+          interleave(4);
+        } else {
+#pragma unroll
+          for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb1[f], acc[f], 0, 0, 0);
+        }
+      }
+      // the next group's window: this wave's DMAs of it are older than the weight DMAs of taps
+      // 0..t.  With two waves per SIMD (NW = 8) the second half transforms one tap earlier, so each
+      // SIMD's transforms run beside its partner's MFMAs instead of beside each other
+      constexpr int TX = K - 1;
+      constexpr int TX2 = (NW == 8) ? K - 2 : K - 1;
+      if ((t == TX && (NW != 8 || wu < 4)) || (t == TX2 && NW == 8 && wu >= 4)) {
+        lap(6);
+        if (t == K - 1) vm_wait<2 * K>();
+        else vm_wait<2 * (K - 1)>();
+        lap(1);
         transform(gg + 1);
+        lap(3);
       }
     }
-    if (gi == NG - 1) epilogue(tt);
+    if (gi == NG - 1) {
+      lap(6);
+      if (!(dbg & 4)) epilogue(tt);
+      init_acc(tt + 1);
+      lap(4);
+    }
   }
   vm_wait<0>();  // nothing may land in LDS after the block's exit
   barrier_lds();
   if (want_stats) flush(cur_b);
+  if (stamp) {
+    lap(6);
+    st_acc[5] = __builtin_amdgcn_s_memtime() - t_start;
+    if (lane == 0)
+      for (int k = 0; k < 8; ++k) atomicAdd(p.stamps + k, st_acc[k]);
+    if (lane == 0 && wu == 0) atomicAdd(p.stamps + 8, 1ull);
+  }
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC>

@@ -49,6 +49,7 @@ struct ConvParams {
   // from the statistics (keeps the padded image borders zero); zc_period = 0 disables.
   int zc_period, zc_valid;
   int dbg;         // phase-skipping timing knob (STTS_OPT_DEBUG; results are wrong when set)
+  unsigned long long* stamps;  // diagnostics: per-phase s_memtime cycle sums (stts_set_debug_buffer), or null
   int tg;          // taps per staged weight group (set by the launcher)
   int cps;         // 32-channel chunks per pipeline step, 1 or 2 (set by the launcher)
   int w_resident;  // weights of the column tile stay in LDS across tiles (set by the launcher)
@@ -72,6 +73,7 @@ extern int g_opt_resconv;
 extern int g_opt_small_tiles;  // few-tile igemm launches use 64 x 128 tiles (STTS_OPT_SMALL_TILES)
 extern int g_opt_grid_cap;  // > 0: cap persistent conv grids (tests: many tiles per block)
 extern int g_opt_debug;     // resconv phase-skipping knob (timing experiments only)
+extern unsigned long long* g_dbg_stamps;  // stts_set_debug_buffer (diagnostics only)
 // wide-stage resblock conv engine (bigconv.hip): bf16, C = 128 / 256, same contract
 bool st_bigconv_eligible(const ConvParams& p, int dtype);
 int st_bigconv(const ConvParams& p, hipStream_t stream);

@@ -1309,6 +1309,11 @@ int stts_set_option(int key, int value) {
   }
 }
 
+int stts_set_debug_buffer(void* buf) {
+  g_dbg_stamps = reinterpret_cast<unsigned long long*>(buf);
+  return 0;
+}
+
 int stts_get_option(int key) {
   switch (key) {
     case STTS_OPT_RESCONV: return g_opt_resconv;

@@ -77,6 +77,8 @@ def lib():
     L.stts_set_option.restype = c_int
     L.stts_get_option.argtypes = [c_int]
     L.stts_get_option.restype = c_int
+    L.stts_set_debug_buffer.argtypes = [c_vp]
+    L.stts_set_debug_buffer.restype = c_int
     _LIB = L
     return L
 
