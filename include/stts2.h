@@ -208,8 +208,13 @@ const char* stts_error_string(int code);
  *                     256 x 128 tiles as there are CUs use 64 x 128 tiles; 0 = off (A/B). */
 #define STTS_OPT_SMALL_TILES 6
 /*   STTS_OPT_BIGCONV  2 (default) = the C = 128 / 256 resblock convs run on bigconv2.hip (per-wave
- *                     LDS-DMA weight rings, one barrier per 32-channel group); 1 = bigconv.hip (A/B). */
+ *                     LDS-DMA weight rings, one barrier per 32-channel group), except C = 128 with
+ *                     3 taps (bigconv.hip, measured faster); 1 = bigconv.hip everywhere; 3 =
+ *                     bigconv2.hip everywhere with 4-wave blocks, two per CU (A/B). */
 #define STTS_OPT_BIGCONV 7
+/*   STTS_OPT_HEAD     1 (default) = the HiFi-GAN output head (Snake -> conv_post -> tanh) runs as one
+ *                     streaming pass (head.hip); 0 = on the igemm engine (A/B). */
+#define STTS_OPT_HEAD 8
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

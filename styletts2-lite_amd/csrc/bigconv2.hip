@@ -605,6 +605,9 @@ int g_opt_bigconv = 2;
 bool st_bigconv2_eligible(const ConvParams& p) {
   if (g_opt_bigconv < 2) return false;
   if (p.res ? p.dil != 1 : (p.accb != nullptr)) return false;
+  // mode 2 (default) keeps v1 where it measured faster: C = 128 with 3 taps (12 taps per tile, so
+  // the per-tile window transform and epilogue dominate; profiles/r02_ab_bigconv_pipelined.txt)
+  if (g_opt_bigconv == 2 && p.Cout == 128 && p.KS == 3) return false;
   return true;  // on top of st_bigconv_eligible
 }
 

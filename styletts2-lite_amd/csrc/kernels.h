@@ -63,7 +63,7 @@ __device__ __forceinline__ double* stats_slot(const ConvParams& p, int g) {
 // stats[b][c] += sum of slots 1..S-1, and those slots are zeroed, for b < B, c < C
 int st_stats_fold(double* stats, int B, int ld, int C, int slots, long long slot_bs, hipStream_t s);
 // which engine st_conv1d routes p to (profiling records; bench.py names the dominant kernel)
-enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2, ST_ENGINE_RESFUSED = 3 };
+enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2, ST_ENGINE_RESFUSED = 3, ST_ENGINE_HEAD = 4 };
 int st_conv1d_engine(const ConvParams& p, int dtype);
 // resblock conv engine (resconv.hip): bf16, C = 32 / 64, 1-D 'same' dilated conv with the
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.
@@ -82,6 +82,11 @@ int st_bigconv(const ConvParams& p, hipStream_t stream);
 bool st_bigconv2_eligible(const ConvParams& p);
 int st_bigconv2(const ConvParams& p, hipStream_t stream);
 extern int g_opt_bigconv;
+// HiFi-GAN output head (head.hip): Snake -> conv_post (C -> 1, 7 taps) -> tanh as one streaming pass;
+// st_conv1d routes eligible launches to it while g_opt_head != 0
+bool st_head_eligible(const ConvParams& p);
+int st_head(const ConvParams& p, int dtype, hipStream_t stream);
+extern int g_opt_head;
 
 // fused AdaINResBlock1 iteration (resfused.hip): bf16, C = 32 (K = 3/7/11) or 64 (K = 3).
 //   y = conv2(Snake2(AdaIN2(conv1(Snake1(AdaIN1(x)))))) + x     (hifigan.py:65-74)

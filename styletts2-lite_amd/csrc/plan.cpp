@@ -1305,6 +1305,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_STATS_SLOTS: g_opt_stats_slots = value > 0 ? value : 0; return 0;
     case STTS_OPT_SMALL_TILES: g_opt_small_tiles = value != 0; return 0;
     case STTS_OPT_BIGCONV: g_opt_bigconv = (value >= 1 && value <= 3) ? value : 2; return 0;
+    case STTS_OPT_HEAD: g_opt_head = value ? 1 : 0; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1323,6 +1324,7 @@ int stts_get_option(int key) {
     case STTS_OPT_STATS_SLOTS: return g_opt_stats_slots;
     case STTS_OPT_SMALL_TILES: return g_opt_small_tiles;
     case STTS_OPT_BIGCONV: return g_opt_bigconv;
+    case STTS_OPT_HEAD: return g_opt_head;
     default: return ST_EINVAL;
   }
 }

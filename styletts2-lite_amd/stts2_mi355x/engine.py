@@ -92,9 +92,10 @@ OPT_STATS_SLOTS = 5
 
 OPT_SMALL_TILES = 6
 OPT_BIGCONV = 7
+OPT_HEAD = 8
 # the production defaults of every STTS_OPT_* (include/stts2.h)
 OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
-                OPT_SMALL_TILES: 1, OPT_BIGCONV: 2}
+                OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1}
 
 
 def set_option(key: int, value: int) -> None:
@@ -370,7 +371,7 @@ def profile_read():
     return {"ms": t.value, "launches": n.value, "flops": f.value, "bytes": b.value}
 
 
-ENGINE_KERNELS = ("conv1d_igemm_kernel", "k_resconv", "k_bigconv", "k_resfused")  # engine ids 0..3
+ENGINE_KERNELS = ("conv1d_igemm_kernel", "k_resconv", "k_bigconv", "k_resfused", "k_conv_post")  # engine ids 0..4
 
 
 def profile_launches():
@@ -383,5 +384,5 @@ def profile_launches():
         check(lib().stts_profile_launch(i, shape, v))
         out.append({"B": shape[0], "rows": shape[1], "N": shape[2], "Cin": shape[3], "taps": shape[4],
                     "dil": shape[5], "Lout": shape[6], "res_acc": shape[7] & 3,
-                    "kernel": ENGINE_KERNELS[(shape[7] >> 4) & 3], "ms": v[0], "flops": v[1], "bytes": v[2]})
+                    "kernel": ENGINE_KERNELS[(shape[7] >> 4) & 7], "ms": v[0], "flops": v[1], "bytes": v[2]})
     return out

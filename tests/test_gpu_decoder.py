@@ -108,6 +108,30 @@ def test_resconv_engine_decoder_ab():
     assert corr > 0.9995 and err < 5e-2
 
 
+@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-5), ("bf16", 2e-2)])
+def test_head_engine_ab(dtype, tol):
+    """HiFi-GAN output head (Snake -> conv_post -> tanh) on the streaming head.hip kernel against the
+    igemm engine running the same launch.  fp32: both exact fp32, differing by summation order
+    (tol 1e-5).  bf16: the igemm rounds the Snake outputs to bf16 for its MFMA operands, the head
+    keeps them fp32, so the two differ by that rounding (tol 2e-2 on a +-1 waveform); the head's
+    own accuracy is the golden test above (fp32 max-abs < 1e-3 vs the reference)."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_HEAD, 0)
+        ref = run("hifigan", 2, 40, dtype)
+        E.set_option(E.OPT_HEAD, 1)
+        E.profile_enable(True)
+        out = run("hifigan", 2, 40, dtype)
+        kernels = {r["kernel"] for r in E.profile_launches()}
+    finally:
+        E.profile_enable(False)
+        E.reset_options()
+    assert "k_conv_post" in kernels
+    err = np.abs(out - ref).max()
+    print(f"head A/B {dtype}: max-abs {err:.3e}")
+    assert err < tol
+
+
 @pytest.mark.parametrize("cap", [0, 3])
 def test_resfused_decoder_ab(cap):
     """bf16 HiFi-GAN decode with the fused resblock iterations (resfused.hip: statistics-only conv1
