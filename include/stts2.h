@@ -215,6 +215,10 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_HEAD     1 (default) = the HiFi-GAN output head (Snake -> conv_post -> tanh) runs as one
  *                     streaming pass (head.hip); 0 = on the igemm engine (A/B). */
 #define STTS_OPT_HEAD 8
+/*   STTS_OPT_SKEW     0 (default) = every bigconv2 workgroup starts at once; v != 0: half of them
+ *                     (odd ones for v > 0, the grid's second half for v < 0) start |v| x 1024 cycles
+ *                     late, so two workgroups sharing a CU run out of phase (A/B experiments). */
+#define STTS_OPT_SKEW 9
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

@@ -166,12 +166,15 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   const int NS = NGG * K;              // steps
   const bool want_stats = !ACC && p.stats != nullptr;
   // STTS_OPT_DEBUG phase skipping (timing attribution only; outputs are wrong while set):
-  // 1 transform, 4 epilogue, 8 weight DMAs, 16 window DMAs, 32 group barrier (2, MFMAs, is not
+  // 1 transform, 4 epilogue, 8 weight DMAs, 16 window DMAs, 32 group barrier, 128 epilogue stores,
+  // 256 epilogue statistics (2, MFMAs, is not
   // honoured: a runtime branch around the pipelined taps keeps their fragments live everywhere)
   const int dbg = p.dbg;
   // diagnostics (dbg bit 64 + a debug buffer): per-wave s_memtime sums of the phases below
   const bool stamp = (dbg & 64) && p.stamps;
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wW wX barrier transform epilogue total mfma issue
+  // slots: 0 weight wait, 1 window wait, 2 barrier, 3 transform, 4 epilogue tail, 5 total, 6 the rest
+  // (MFMA issue), 7 epilogue vmcnt(0), 8 epilogue loads + finish + stores, 9 epilogue statistics
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_mark = stamp ? __builtin_amdgcn_s_memtime() : 0;
   auto lap = [&](int k) __attribute__((always_inline)) {
     if (stamp) {
@@ -182,6 +185,13 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   };
   const unsigned long long t_start = t_mark;
 
+  // STTS_OPT_SKEW: half the workgroups start |skew| x 1024 cycles late (odd ones for skew > 0, the
+  // second half of the grid for skew < 0), so that two workgroups sharing a CU run out of phase
+  if (p.skew != 0 && (p.skew > 0 ? (blockIdx.x & 1) != 0 : blockIdx.x >= gridDim.x / 2)) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long d = (unsigned long long)(p.skew > 0 ? p.skew : -p.skew) * 1024ull;
+    while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
+  }
   for (int i = tid; i < C; i += NT) {
     bias_s[i] = p.bias ? p.bias[i] : 0.f;
     st_lds[2 * i] = st_lds[2 * i + 1] = 0.f;
@@ -217,7 +227,9 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       const int pidx = (j * NW + wu) * 64 + lane;
       const int r = pidx >> 2, u = (pidx & 3) ^ ((r >> 2) & 3);
       const int e = (gr0 + r) * p.x_ld + gi * 32 + 8 * u;
-      glds16(rx, dst + (j * NW + wu) * 1024, e >= 0 ? (unsigned)e * 2u : OOB);
+      // rows past the window (WROWS rounds R up to whole DMA instructions) read out of range: no
+      // HBM traffic for them (profiles/r02_pmc_bigconv.txt measured 1.5x the window bytes)
+      glds16(rx, dst + (j * NW + wu) * 1024, (e >= 0 && r < G::R) ? (unsigned)e * 2u : OOB);
     }
   };
   // AdaIN + Snake coefficients of utterance b into parity slot b & 1 (see bigconv.hip)
@@ -257,6 +269,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       for (int j = 0; j < NWIN; ++j) {
         const int pidx = (j * NW + wu) * 64 + lane;
         const int r = pidx >> 2;
+        if (G::WROWS > G::R && r >= G::R) continue;  // padding rows: never read by a tap
         uint2* ptr = reinterpret_cast<uint2*>(buf + pidx * 16 + 8 * h);
         float v[4];
         bf4_to_f32(*ptr, v);
@@ -284,6 +297,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   };
 
   f32x16 acc[8];
+  constexpr int NST = 16;  // vector-memory stores of one epilogue (8 fragments x 2)
   auto epilogue = [&](int tt) __attribute__((always_inline)) {
     const int b = tt / upb, mt = tt % ntm, ch = NCH > 1 ? (tt / ntm) % NCH : 0;
     const int q0 = mt * TM + fh * 256 + l32;
@@ -305,6 +319,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     // DMAs in the compiler's own model, so it counts the loads below precisely (with an LDS-DMA
     // pending it would wait vmcnt(0) at every use); the empty asm fences pin the issue order.
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unconstrained
+    lap(7);
     constexpr int NB = RES ? 2 : 1, FB = 8 / NB;
     uint4 rl[FB][2], al[FB][2];
     auto finish = [&](int f, const uint4 (&r2)[2], const uint4 (&a2)[2]) __attribute__((always_inline)) {
@@ -324,12 +339,16 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = (a0[r] + v[r]) * adiv;
       }
-      const unsigned ey = (unsigned)(q * p.y_ld + co0) * 2u;
       float o[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[r] = v[r];
-      bstore16(ry, ey, f32_to_bf8v(o));  // rows past Lq fall outside the descriptor: dropped
-      bstore16(ry, ey + 16u, f32_to_bf8v(o + 8));
+      if (!(dbg & 128)) {
+        // (an LDS-transposed variant writing 16 rows x 64 contiguous bytes per store measured the
+        // same in the decoder: the stores are bound by the chip-wide write burst, not by requests)
+        const unsigned ey = (unsigned)(q * p.y_ld + co0) * 2u;
+        bstore16(ry, ey, f32_to_bf8v(o));  // rows past Lq fall outside the descriptor: dropped
+        bstore16(ry, ey + 16u, f32_to_bf8v(o + 8));
+      }
       if (!ACC) {
         const float m = q < p.Lq ? 1.f : 0.f;
 #pragma unroll
@@ -362,7 +381,8 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       asm volatile("" ::: "memory");
     }
     __builtin_amdgcn_sched_barrier(0);  // the tile's stores before the reduction: fewer live values
-    if (want_stats) {
+    lap(8);
+    if (want_stats && !(dbg & 256)) {
       // reduce-scatter of the lane's 16 partial sums (then squares) over the 32 lanes of its half:
       // 8 + 4 + 2 + 1 exchanges leave lane l32 with channel co0 + l32 / 2 summed over 16 lanes, one
       // more exchange with lane l32 ^ 1 completes it; the even lane adds the sum, the odd one the
@@ -384,6 +404,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       const float s2 = rs16(tq);
       atomicAdd(st_lds + 2 * (co0 + (l32 >> 1)) + (l32 & 1), (l32 & 1) ? s2 : s1);
     }
+    lap(9);
   };
 
   // ---------------- MFMA taps, software-pipelined within a group.  Tap t = two 8-MFMA halves (input
@@ -465,8 +486,12 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     issue_x(gg + 1);  // the next group's raw window: buffer (gg+1)&1, whose last reads were group gg-1's
     // this wave's weights of step gg K: younger VMEM ops are the weight DMAs of the next PD - 1 steps
     // and the window DMAs just issued
+    // (in the group after an epilogue, that epilogue's NST stores are younger too: counted, so the
+    // wait does not also drain the stores' write acknowledgements)
+    const bool post_epi = gi == 0 && gg > 0;
     lap(6);
-    vm_wait<2 * (PD - 1) + NWIN>();
+    if (post_epi) vm_wait<2 * (PD - 1) + NWIN + NST>();
+    else vm_wait<2 * (PD - 1) + NWIN>();
     lap(0);
     rd_a(gg * K, fa[0]);
     rd_b(fb0, gg, 0, 0);
@@ -500,8 +525,12 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           // weights of step s+1: younger VMEM ops are the weight DMAs of steps s+2..s+PD and, while
           // step s+1 precedes this group's window DMAs (t + 1 < PD), those
           lap(6);
-          if (t + 1 < PD) vm_wait<2 * (PD - 1) + NWIN>();
-          else vm_wait<2 * (PD - 1)>();
+          if (t + 1 < PD) {
+            if (post_epi) vm_wait<2 * (PD - 1) + NWIN + NST>();
+            else vm_wait<2 * (PD - 1) + NWIN>();
+          } else {
+            vm_wait<2 * (PD - 1)>();
+          }
           lap(0);
           rd_a(s + 1, fa[(t + 1) & 1]);
 #pragma unroll
@@ -543,8 +572,8 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     lap(6);
     st_acc[5] = __builtin_amdgcn_s_memtime() - t_start;
     if (lane == 0)
-      for (int k = 0; k < 8; ++k) atomicAdd(p.stamps + k, st_acc[k]);
-    if (lane == 0 && wu == 0) atomicAdd(p.stamps + 8, 1ull);
+      for (int k = 0; k < 10; ++k) atomicAdd(p.stamps + k, st_acc[k]);
+    if (lane == 0 && wu == 0) atomicAdd(p.stamps + 15, 1ull);
   }
 }
 
@@ -567,7 +596,9 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
   long long grid = (long long)ncu * G::BPC;
   if (grid > tiles) grid = tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), G::LDS, stream, p);
+  ConvParams q = p;
+  q.skew = g_opt_skew;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
 
@@ -601,6 +632,7 @@ int launch_b2_c(const ConvParams& p, hipStream_t s) {
 // STTS_OPT_BIGCONV: 1 = bigconv.hip (v1, A/B); 2 = this engine, 8-wave blocks (one per CU);
 // 3 = this engine, 4-wave blocks (two per CU, C = 256 split into two 128-channel output parts)
 int g_opt_bigconv = 2;
+int g_opt_skew = 0;
 
 bool st_bigconv2_eligible(const ConvParams& p) {
   if (g_opt_bigconv < 2) return false;

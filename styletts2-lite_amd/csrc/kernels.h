@@ -49,6 +49,7 @@ struct ConvParams {
   // from the statistics (keeps the padded image borders zero); zc_period = 0 disables.
   int zc_period, zc_valid;
   int dbg;         // phase-skipping timing knob (STTS_OPT_DEBUG; results are wrong when set)
+  int skew;        // bigconv2 start skew of half the workgroups (STTS_OPT_SKEW, set by the launcher)
   unsigned long long* stamps;  // diagnostics: per-phase s_memtime cycle sums (stts_set_debug_buffer), or null
   int tg;          // taps per staged weight group (set by the launcher)
   int cps;         // 32-channel chunks per pipeline step, 1 or 2 (set by the launcher)
@@ -82,6 +83,7 @@ int st_bigconv(const ConvParams& p, hipStream_t stream);
 bool st_bigconv2_eligible(const ConvParams& p);
 int st_bigconv2(const ConvParams& p, hipStream_t stream);
 extern int g_opt_bigconv;
+extern int g_opt_skew;  // STTS_OPT_SKEW (bigconv2.hip)
 // HiFi-GAN output head (head.hip): Snake -> conv_post (C -> 1, 7 taps) -> tanh as one streaming pass;
 // st_conv1d routes eligible launches to it while g_opt_head != 0
 bool st_head_eligible(const ConvParams& p);

@@ -27,7 +27,9 @@ def main():
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--set", action="append", default=[], help="KEY=VALUE options held for every variant")
     a = ap.parse_args()
+    fixed = [tuple(int(x) for x in kv.split("=")) for kv in a.set]
     from stts2_mi355x import engine as E
     from stts2_mi355x import synth
     torch.cuda.set_device(0)
@@ -41,6 +43,8 @@ def main():
     outs = {}
     for r in range(a.rounds):
         for v in a.values:
+            for k, fv in fixed:
+                E.set_option(k, fv)
             E.set_option(a.opt, v)
             eng.forward(asr, f0, n, s, seed=5, out=out)  # warm
             torch.cuda.synchronize()

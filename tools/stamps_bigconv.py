@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 from stts2_mi355x import engine as E  # noqa: E402
 
-NAMES = ["w_wait", "x_wait", "barrier", "transform", "epilogue", "total", "rest"]
+NAMES = ["w_wait", "x_wait", "barrier", "transform", "epilogue", "total", "rest", "ep_vmwait", "ep_finish", "ep_stats"]
 
 
 def run(C, K, dil, res, B, L, stamps, skip=0):
@@ -40,7 +40,7 @@ def run(C, K, dil, res, B, L, stamps, skip=0):
     E.set_option(E.OPT_DEBUG, 0)
     v = stamps.cpu().tolist()
     tot = v[5] or 1
-    waves = max(v[8], 1) * 8
+    waves = max(v[15], 1) * 8
     tag = f" skip={skip:2d}" if skip else ""
     print(f"C={C} K={K:2d} d={dil} res={int(res)}{tag}: cycles/wave {v[5] / waves:9.0f}  " +
           "  ".join(f"{n} {100 * v[i] / tot:4.1f}%" for i, n in enumerate(NAMES) if i != 5), flush=True)
