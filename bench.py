@@ -178,8 +178,8 @@ class Stand_in:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10, help="timed steps (SURVEY §8(d): median of >= 10)")
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=400, help="asr frames per utterance (400 = 10 s)")
     ap.add_argument("--decoder", default="hifigan", choices=["hifigan", "istftnet"])
@@ -339,6 +339,8 @@ def main():
         "x_realtime_per_gpu": value / world / 24000.0,
         "hbm_fraction": a["bytes"][args.dtype] * value / world / PEAK_HBM,
         "mfma_fraction": a["flops"] * value / world / PEAK_MFMA[args.dtype],
+        # SURVEY §8(d)'s names: the same two whole-step fractions
+        "mfma_or_valu_fraction": a["flops"] * value / world / PEAK_MFMA[args.dtype],
         "roofline": roofline(prof_recs, args.dtype, 2, ms, B, T, args.decoder) if prof_recs else None,
     }
     if with_gather:
