@@ -219,6 +219,9 @@ const char* stts_error_string(int code);
  *                     (odd ones for v > 0, the grid's second half for v < 0) start |v| x 1024 cycles
  *                     late, so two workgroups sharing a CU run out of phase (A/B experiments). */
 #define STTS_OPT_SKEW 9
+/*   STTS_OPT_FRONT    1 (default) = the decoder front-end's k3 AdainResBlk1d convs (C_out 1024 / 512)
+ *                     run on the bigconv2 engine; 0 = on the igemm engine (A/B). */
+#define STTS_OPT_FRONT 10
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

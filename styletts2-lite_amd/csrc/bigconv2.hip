@@ -29,14 +29,20 @@
 
 namespace {
 
-template <int C, int NW, int K, int DIL>
+// prologue kinds: AdaIN -> Snake (the generator resblocks, 5 coefficients per channel), or
+// [AdaIN ->] LReLU (the decoder front-end's AdainResBlk1d convs, hifigan.py:359-403; 2 per
+// channel; no prologue = a = 1, m = 0, slope 1)
+enum { PK_SNAKE = 0, PK_LRELU = 1 };
+
+template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C>
 struct B2 {
+  static constexpr int NCOEF = PRO == PK_SNAKE ? 5 : 2;  // coefficient rows per input channel
   static constexpr int NCBW = (C / 32 < NW) ? C / 32 : NW;  // 32-channel output blocks per block tile
   static constexpr int FH = NW / NCBW;   // frame halves per tile (waves per co block)
   static constexpr int NCO = 32 * NCBW;  // output channels per tile
   static constexpr int NCH = C / NCO;    // output-channel parts per frame tile (tiles per frame range)
   static constexpr int TM = 256 * FH;    // tile rows (frames)
-  static constexpr int NG = C / 32;      // 32-channel input groups per tile
+  static constexpr int NG = CINP / 32;   // 32-channel input groups per tile (at most)
   static constexpr int PAD = DIL * (K - 1) / 2;
   static constexpr int R = TM + DIL * (K - 1);                    // window rows a group needs
   static constexpr int NWIN = (R * 4 + 64 * NW - 1) / (64 * NW);  // window DMA instructions per wave per group
@@ -46,8 +52,8 @@ struct B2 {
   // issue order, so the first wait for a weight slice issued after a group's window DMA (PD taps
   // later) also waits for that window (a DMA lands ~1.1 us after issue, MI355X_MICROARCH.md
   // ldsdma-fill, later from HBM under load; a tap is ~0.5 us of MFMA issue per SIMD)
-  static constexpr int OFF_COEF = 0;                  // [2][5][C] f32 (utterance parity)
-  static constexpr int OFF_BIAS = OFF_COEF + 2 * 5 * C * 4;
+  static constexpr int OFF_COEF = 0;                  // [2][NCOEF][CINP] f32 (utterance parity)
+  static constexpr int OFF_BIAS = OFF_COEF + 2 * NCOEF * CINP * 4;
   static constexpr int OFF_ST = OFF_BIAS + C * 4;     // [C][2] f32
   static constexpr int OFF_W = (OFF_ST + 2 * C * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
   static constexpr int BPC = NW == 4 ? 2 : 1;                     // blocks per CU
@@ -99,11 +105,27 @@ __device__ __forceinline__ void lds_coef5(unsigned a, f32x4v& c0, f32x4v& c1, f3
       : "memory");
 }
 
+__device__ __forceinline__ void lds_coef2(unsigned a, f32x4v& c0, f32x4v& c1, unsigned stride) {
+  const unsigned a1 = a + stride;
+  asm volatile(
+      "ds_read_b128 %0, %2\n\t"
+      "ds_read_b128 %1, %3\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(c0), "=&v"(c1)
+      : "v"(a), "v"(a1)
+      : "memory");
+}
+
 // an LDS store hipcc cannot see: it drains every in-flight LDS-DMA (vmcnt(0)) before a visible
 // ds_write, although the window units written here are never a pending DMA's destination (their
 // own DMA was waited for by vm_wait)
 __device__ __forceinline__ void lds_write_b64(unsigned a, const uint2& v) {
   asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_write_b128(unsigned a, const uint4& v) {
+  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+  const u32x4v w = {v.x, v.y, v.z, v.w};
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(w) : "memory");
 }
 
 __device__ __forceinline__ void bf4_to_f32(const uint2& r, float (&v)[4]) {
@@ -142,10 +164,13 @@ __device__ __forceinline__ void bstore16(Rsrc r, unsigned off, const uint4& v) {
                                          r, (int)off, 0, 0);
 }
 
-template <int C, int NW, int K, int DIL, bool RES, bool ACC>
+template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C>
 __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
-  using G = B2<C, NW, K, DIL>;
-  constexpr int NG = G::NG, TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
+  using G = B2<C, NW, K, DIL, PRO, CINP>;
+  constexpr int TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
+  constexpr int NCF = G::NCOEF;
+  // input-channel groups: C / 32 for the square resblock convs, ceil(Cin / 32) for the front-end
+  const int NG = (PRO == PK_SNAKE && CINP == C) ? C / 32 : (p.Cin + 31) / 32;
   constexpr int NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* coef = reinterpret_cast<float*>(smem + G::OFF_COEF);
@@ -163,7 +188,6 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
   if (tbeg >= tend) return;  // uniform over the block
   const int NGG = (tend - tbeg) * NG;  // groups this block walks
-  const int NS = NGG * K;              // steps
   const bool want_stats = !ACC && p.stats != nullptr;
   // STTS_OPT_DEBUG phase skipping (timing attribution only; outputs are wrong while set):
   // 1 transform, 4 epilogue, 8 weight DMAs, 16 window DMAs, 32 group barrier, 128 epilogue stores,
@@ -200,11 +224,10 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   // ---------------- weights: step s = (group, tap) -> this wave's 2 KB slice, slot s % RS
   char* wring = smem + G::OFF_W + wu * RS * 2048;
   const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)NG * K * C * 32 * 2));
-  auto issue_w = [&](int s) __attribute__((always_inline)) {
+  // (group index gi, output part ch and tap t of the step: from the group cursors below, so no
+  // runtime division by the group count runs per step)
+  auto issue_w = [&](int s, int gi, int ch, int t) __attribute__((always_inline)) {
     if (dbg & 8) return;
-    const int sc = s < NS ? s : NS - 1;  // past the end: a harmless reload keeps the counts uniform
-    const int gq = sc / K, t = sc - gq * K, gi = gq % NG;
-    const int ch = NCH > 1 ? ((tbeg + gq / NG) / ntm) % NCH : 0;
     const unsigned base = (unsigned)((((size_t)gi * K + t) * C + ch * NCO + 32 * cb) * 64) + lane * 16;
     char* dst = wring + (s % RS) * 2048;
     glds16(rw, dst, base);
@@ -213,11 +236,8 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 
   // ---------------- window: group gg -> raw rows [gr0, gr0 + WROWS) of its 32 channels, buffer gg & 1
   // LDS unit pidx = row * 4 + u' holds logical 16-B unit u = u' ^ ((row >> 2) & 3) of that row
-  auto issue_x = [&](int gg) __attribute__((always_inline)) {
+  auto issue_x = [&](int gg, int gi, int b, int mt) __attribute__((always_inline)) {
     if (dbg & 16) return;
-    const int gc = gg < NGG ? gg : NGG - 1;
-    const int t = tbeg + gc / NG, gi = gc % NG;
-    const int b = t / upb, mt = t % ntm;
     const Rsrc rx = make_rsrc(reinterpret_cast<const bf16_t*>(p.x) + (size_t)b * p.x_bs,
                               (unsigned)((size_t)p.Lin * p.x_ld * 2));
     const int gr0 = mt * TM - G::PAD;
@@ -234,34 +254,92 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   };
   // AdaIN + Snake coefficients of utterance b into parity slot b & 1 (see bigconv.hip)
   auto set_coef = [&](int b) __attribute__((always_inline)) {
-    float* cf = coef + (b & 1) * 5 * C;
-    for (int ci = tid; ci < C; ci += NT) {
-      float mm, aa, be;
-      adain_coeffs(p.pro, b, ci, mm, aa, be);
-      const float al = p.pro.alpha[ci];
-      const float m1 = be - mm * aa, ia2 = 0.5f / al, alr = al * 0.31830988618379067f;
-      cf[ci] = m1 + ia2;
-      cf[C + ci] = aa;
-      cf[2 * C + ci] = aa * alr;
-      cf[3 * C + ci] = m1 * alr;
-      cf[4 * C + ci] = -ia2;
+    float* cf = coef + (b & 1) * NCF * CINP;
+    if constexpr (PRO == PK_SNAKE) {
+      for (int ci = tid; ci < C; ci += NT) {
+        float mm, aa, be;
+        adain_coeffs(p.pro, b, ci, mm, aa, be);
+        const float al = p.pro.alpha[ci];
+        const float m1 = be - mm * aa, ia2 = 0.5f / al, alr = al * 0.31830988618379067f;
+        cf[ci] = m1 + ia2;
+        cf[CINP + ci] = aa;
+        cf[2 * CINP + ci] = aa * alr;
+        cf[3 * CINP + ci] = m1 * alr;
+        cf[4 * CINP + ci] = -ia2;
+      }
+    } else {  // x * a + m (AdaIN, or a = 1, m = 0 without it); channels >= Cin: a = m = 0 -> 0
+      for (int ci = tid; ci < CINP; ci += NT) {
+        float mm = 0.f, aa = 1.f, be = 0.f;
+        if (ci < p.Cin && (p.pro.mode & PRO_AFFINE)) adain_coeffs(p.pro, b, ci, mm, aa, be);
+        const bool ok = ci < p.Cin;
+        cf[ci] = ok ? be - mm * aa : 0.f;
+        cf[CINP + ci] = ok ? aa : 0.f;
+      }
     }
   };
   // in-place transform of the units this lane DMA'd for group gg: x -> AdaIN -> Snake -> bf16
   // (Snake via sin^2(u) = (1 - cos 2u) / 2 on the hardware cosine, as resconv.hip), 0 outside [0, Lin)
   const int my_u = (lane & 3) ^ ((lane >> 4) & 3);  // the lane's logical unit: the same in every row it owns
-  auto transform = [&](int gg) __attribute__((always_inline)) {
+  // The lane's NWIN units are read first (one LDS latency), transformed per 4-channel half with
+  // that half's coefficients, and written back with one 16-B store each.  Padding rows past R
+  // are transformed too (their DMA read zeros; no tap reads them): no per-unit branch.
+  auto transform = [&](int gg, int gi, int b, int mt) __attribute__((always_inline)) {
     if (dbg & 1) return;
-    const int gc = gg < NGG ? gg : NGG - 1;
-    const int t = tbeg + gc / NG, gi = gc % NG;
-    const int b = t / upb, mt = t % ntm;
     const int gr0 = mt * TM - G::PAD;
-    const float* cf = coef + (b & 1) * 5 * C + gi * 32 + 8 * my_u;
+    const float* cf = coef + (b & 1) * NCF * CINP + gi * 32 + 8 * my_u;
     char* buf = smem + G::OFF_X + (gg & 1) * (G::WROWS * 64);
+    if constexpr (PRO == PK_LRELU) {
+    // (in chunks of at most 3 units: C = 128's 5 units at once spill)
+    constexpr int JC = NWIN < 3 ? NWIN : 3;
+#pragma unroll
+    for (int j0 = 0; j0 < NWIN; j0 += JC) {
+    uint4 raw[JC];
+#pragma unroll
+    for (int jj = 0; jj < JC; ++jj)
+      if (j0 + jj < NWIN) raw[jj] = *reinterpret_cast<const uint4*>(buf + (((j0 + jj) * NW + wu) * 64 + lane) * 16);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      {
+        f32x4v m2, a;
+        lds_coef2(lds_addr(cf + 4 * h), m2, a, (unsigned)(CINP * 4));  // (its wait also covers raw[])
+        const float am[4] = {m2.x, m2.y, m2.z, m2.w}, aa[4] = {a.x, a.y, a.z, a.w};
+        const float slope = (p.pro.mode & PRO_LRELU) ? p.pro.slope : 1.0f;
+        // channels >= Cin (the last group's padding, whose memory may hold anything, NaN
+        // included) are forced to 0 rather than multiplied by 0
+        const int c0 = gi * 32 + 8 * my_u + 4 * h;
+#pragma unroll
+        for (int j = 0; j < JC; ++j) {
+          if (j0 + j >= NWIN) continue;
+          uint2 hv = h ? make_uint2(raw[j].z, raw[j].w) : make_uint2(raw[j].x, raw[j].y);
+          float v[4];
+          bf4_to_f32(hv, v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x2 = __builtin_fmaf(v[e], aa[e], am[e]);
+            v[e] = c0 + e < p.Cin ? (x2 > 0.f ? x2 : x2 * slope) : 0.f;
+          }
+          hv = f32_to_bf4(v);
+          if (h) { raw[j].z = hv.x; raw[j].w = hv.y; } else { raw[j].x = hv.x; raw[j].y = hv.y; }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < JC; ++j) {
+      if (j0 + j >= NWIN) continue;
+      const int pidx = ((j0 + j) * NW + wu) * 64 + lane;
+      uint4 o = raw[j];
+      if ((unsigned)(gr0 + (pidx >> 2)) >= (unsigned)p.Lin) o = make_uint4(0u, 0u, 0u, 0u);
+      lds_write_b128(lds_addr(buf + pidx * 16), o);
+    }
+    }
+      return;
+    }
+    // Snake: per unit (measured faster for the resblock convs than the batched form above, which
+    // spills at C = 128)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f32x4v m2, a, ar, mr, nia;
-      lds_coef5(lds_addr(cf + 4 * h), m2, a, ar, mr, nia, (unsigned)(C * 4));
+      lds_coef5(lds_addr(cf + 4 * h), m2, a, ar, mr, nia, (unsigned)(CINP * 4));
       const float am[4] = {m2.x, m2.y, m2.z, m2.w}, aa[4] = {a.x, a.y, a.z, a.w};
       const float aar[4] = {ar.x, ar.y, ar.z, ar.w}, amr[4] = {mr.x, mr.y, mr.z, mr.w};
       const float ani[4] = {nia.x, nia.y, nia.z, nia.w};
@@ -298,8 +376,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 
   f32x16 acc[8];
   constexpr int NST = 16;  // vector-memory stores of one epilogue (8 fragments x 2)
-  auto epilogue = [&](int tt) __attribute__((always_inline)) {
-    const int b = tt / upb, mt = tt % ntm, ch = NCH > 1 ? (tt / ntm) % NCH : 0;
+  auto epilogue = [&](int b, int mt, int ch) __attribute__((always_inline)) {
     const int q0 = mt * TM + fh * 256 + l32;
     // the lane's 16 consecutive output channels (packing permutation)
     const int co0 = ch * NCO + 32 * cb + 16 * hi;
@@ -365,7 +442,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       for (int k = 0; k < FB; ++k) {
         const int q = q0 + 32 * (nb * FB + k);
         if constexpr (RES) {
-          const unsigned er = (unsigned)(q * p.res_ld + co0) * 2u;
+          const unsigned er = (unsigned)((q >> p.res_shift) * p.res_ld + co0) * 2u;
           rl[k][0] = bload16(rr, er);
           rl[k][1] = bload16(rr, er + 16u);
         }
@@ -444,19 +521,37 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   };
 
   // ---------------- prologue: coefficients, group 0's window transformed, weights of steps 0..PD-1
-  int cur_b = tbeg / upb;
+  // group cursors: (tile, group, utterance, frame tile, output part) of the current and the next
+  // group, advanced incrementally (tiles run frame tile fastest, then output part, then utterance)
+  struct GCur { int tt, gi, b, mt, ch; };
+  auto advance = [&](GCur c) __attribute__((always_inline)) {
+    if (++c.gi == NG) {
+      c.gi = 0;
+      ++c.tt;
+      if (++c.mt == ntm) {
+        c.mt = 0;
+        if (++c.ch == NCH) {
+          c.ch = 0;
+          ++c.b;
+        }
+      }
+    }
+    return c;
+  };
+  GCur cur = {tbeg, 0, tbeg / upb, tbeg % ntm, NCH > 1 ? (tbeg / ntm) % NCH : 0};
+  int cur_b = cur.b;
   set_coef(cur_b);
   __syncthreads();  // nothing in flight yet
-  issue_x(0);
+  issue_x(0, 0, cur.b, cur.mt);
 #pragma unroll
-  for (int s = 0; s < PD; ++s) issue_w(s);
+  for (int s = 0; s < PD; ++s) issue_w(s, 0, cur.ch, s);
   vm_wait<2 * PD>();  // this wave's window DMA of group 0 landed
-  transform(0);
+  transform(0, 0, cur.b, cur.mt);
 
   // the accumulators of tile tt start at the bias.  Set right after the previous tile's epilogue
   // (not at the next group 0), so the compiler sees them dead while that epilogue reduces statistics
-  auto init_acc = [&](int tt) __attribute__((always_inline)) {
-    const int co0 = (NCH > 1 ? ((tt / ntm) % NCH) * NCO : 0) + 32 * cb + 16 * hi;
+  auto init_acc = [&](int ch) __attribute__((always_inline)) {
+    const int co0 = ch * NCO + 32 * cb + 16 * hi;
     float bb[16];
     ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
     ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
@@ -467,23 +562,26 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   };
 
   // ---------------- main loop: one iteration per 32-channel group; K taps unrolled
-  init_acc(tbeg);
+  init_acc(cur.ch);
   for (int gg = 0; gg < NGG; ++gg) {
     lap(6);
     if (!(dbg & 32)) barrier_lds();  // group gg's window transformed by every wave; group gg-1's reads all done
     lap(2);
-    const int tl = gg / NG, gi = gg - tl * NG, tt = tbeg + tl;
+    if (gg > 0) cur = advance(cur);
+    // the next group (past the end: the last group again, a harmless reload keeping counts uniform)
+    const GCur nxt = gg + 1 < NGG ? advance(cur) : cur;
+    const int gi = cur.gi, tt = cur.tt;
     if (gi == 0) {
-      const int b = tt / upb;
+      const int b = cur.b;
       if (b != cur_b) {  // the block left utterance cur_b: every epilogue of it ran >= 1 barrier ago
         if (want_stats) flush(cur_b);
         cur_b = b;
       }
       // the next tile opens another utterance: its coefficients, first read by the transform of its
       // group 0 during this tile's last group, >= 1 barrier from here (NG >= 4)
-      if (tt + 1 < tend && (tt + 1) / upb != b) set_coef((tt + 1) / upb);
+      if (tt + 1 < tend && cur.mt == ntm - 1 && cur.ch == NCH - 1) set_coef(b + 1);
     }
-    issue_x(gg + 1);  // the next group's raw window: buffer (gg+1)&1, whose last reads were group gg-1's
+    issue_x(gg + 1, nxt.gi, nxt.b, nxt.mt);  // buffer (gg+1)&1, whose last reads were group gg-1's
     // this wave's weights of step gg K: younger VMEM ops are the weight DMAs of the next PD - 1 steps
     // and the window DMAs just issued
     // (in the group after an epilogue, that epilogue's NST stores are younger too: counted, so the
@@ -498,7 +596,11 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 #pragma unroll
     for (int t = 0; t < K; ++t) {
       const int s = gg * K + t;
-      issue_w(s + PD);  // into slot (s+PD) % RS = (s-1) % RS, whose fragments tap s-1 consumed
+      // into slot (s+PD) % RS = (s-1) % RS, whose fragments tap s-1 consumed; step s+PD is tap
+      // t+PD of this group or tap t+PD-K of the next (PD <= K)
+      if (t + PD < K) issue_w(s + PD, gi, cur.ch, t + PD);
+      else if (gg + 1 < NGG) issue_w(s + PD, nxt.gi, nxt.ch, t + PD - K);
+      else issue_w(s + PD, gi, cur.ch, K - 1);
       {
         const bf16x8(&a)[2] = fa[t & 1];
         // half 0 of tap t; reads of half 1
@@ -554,14 +656,14 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
         if (t == K - 1) vm_wait<2 * K>();
         else vm_wait<2 * (K - 1)>();
         lap(1);
-        transform(gg + 1);
+        transform(gg + 1, nxt.gi, nxt.b, nxt.mt);
         lap(3);
       }
     }
     if (gi == NG - 1) {
       lap(6);
-      if (!(dbg & 4)) epilogue(tt);
-      init_acc(tt + 1);
+      if (!(dbg & 4)) epilogue(cur.b, cur.mt, cur.ch);
+      init_acc(nxt.ch);
       lap(4);
     }
   }
@@ -577,10 +679,10 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   }
 }
 
-template <int C, int NW, int K, int DIL, bool RES, bool ACC>
+template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
-  using G = B2<C, NW, K, DIL>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC>;
+  using G = B2<C, NW, K, DIL, PRO, CINP>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -641,6 +743,33 @@ bool st_bigconv2_eligible(const ConvParams& p) {
   // the per-tile window transform and epilogue dominate; profiles/r02_ab_bigconv_pipelined.txt)
   if (g_opt_bigconv == 2 && p.Cout == 128 && p.KS == 3) return false;
   return true;  // on top of st_bigconv_eligible
+}
+
+// ---- decoder front-end (AdainResBlk1d k3 convs, hifigan.py:359-403 / 427-432): C_out 1024 / 512
+// in 256-channel output parts, C_in up to 1120 (the 1090-channel concat), [AdaIN ->] LReLU prologue
+constexpr int FE_CINP = 1120;
+int g_opt_front = 1;
+
+bool st_front_eligible(const ConvParams& p, int dtype) {
+  if (!g_opt_front || dtype != ST_BF16) return false;
+  if (p.Cout != 1024 && p.Cout != 512) return false;
+  const int mode = p.pro.mode;
+  if (mode != 0 && mode != PRO_LRELU && mode != (PRO_AFFINE | PRO_LRELU) && mode != PRO_AFFINE) return false;
+  return p.N == p.Cout && p.KS == 3 && p.dil == 1 && p.stride == 1 && p.up == 1 && p.pad == 1 &&
+         (p.kw == 0 || p.kw == p.KS) && p.row_off == 0 && p.Cin >= 128 && p.Cin <= FE_CINP &&
+         p.Lin == p.Lq && p.Lout == p.Lq && !p.accb && !p.epi_tanh && !p.y_f32 && !p.reflect_front &&
+         p.zc_period == 0 && p.y_row_off == 0 && p.x_ld % 8 == 0 && p.y_ld % 8 == 0 &&
+         (!p.res || (p.res_ld % 8 == 0 && (p.res_shift == 0 || p.res_shift == 1)));
+}
+
+int st_bigconv2_front(const ConvParams& p, hipStream_t s) {
+  if (p.Cout == 1024)
+    return p.res ? launch_b2<1024, 8, 3, 1, true, false, PK_LRELU, FE_CINP>(p, s)
+                 : launch_b2<1024, 8, 3, 1, false, false, PK_LRELU, FE_CINP>(p, s);
+  if (p.Cout == 512)
+    return p.res ? launch_b2<512, 8, 3, 1, true, false, PK_LRELU, FE_CINP>(p, s)
+                 : launch_b2<512, 8, 3, 1, false, false, PK_LRELU, FE_CINP>(p, s);
+  return ST_EINVAL;
 }
 
 int st_bigconv2(const ConvParams& p, hipStream_t stream) {

@@ -797,6 +797,7 @@ int st_conv1d_engine(const ConvParams& p, int dtype) {
   ConvParams q = p;
   if (q.kw <= 0) q.kw = q.KS;
   if (g_opt_head && st_head_eligible(q)) return ST_ENGINE_HEAD;
+  if (st_front_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return ST_ENGINE_RESCONV;
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
   return ST_ENGINE_IGEMM;
@@ -811,6 +812,7 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   q.dbg = g_opt_debug;
   q.stamps = g_dbg_stamps;
   if (g_opt_head && st_head_eligible(q)) return st_head(q, dtype, stream);
+  if (st_front_eligible(q, dtype)) return st_bigconv2_front(q, stream);
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return st_resconv(q, stream);
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return st_bigconv(q, stream);
   if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);

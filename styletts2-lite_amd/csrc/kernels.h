@@ -84,6 +84,10 @@ bool st_bigconv2_eligible(const ConvParams& p);
 int st_bigconv2(const ConvParams& p, hipStream_t stream);
 extern int g_opt_bigconv;
 extern int g_opt_skew;  // STTS_OPT_SKEW (bigconv2.hip)
+// the decoder front-end's k3 AdainResBlk1d convs on the bigconv2 engine (STTS_OPT_FRONT)
+bool st_front_eligible(const ConvParams& p, int dtype);
+int st_bigconv2_front(const ConvParams& p, hipStream_t stream);
+extern int g_opt_front;
 // HiFi-GAN output head (head.hip): Snake -> conv_post (C -> 1, 7 taps) -> tanh as one streaming pass;
 // st_conv1d routes eligible launches to it while g_opt_head != 0
 bool st_head_eligible(const ConvParams& p);

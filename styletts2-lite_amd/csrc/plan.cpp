@@ -1307,6 +1307,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_BIGCONV: g_opt_bigconv = (value >= 1 && value <= 3) ? value : 2; return 0;
     case STTS_OPT_HEAD: g_opt_head = value ? 1 : 0; return 0;
     case STTS_OPT_SKEW: g_opt_skew = value; return 0;
+    case STTS_OPT_FRONT: g_opt_front = value ? 1 : 0; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1327,6 +1328,7 @@ int stts_get_option(int key) {
     case STTS_OPT_BIGCONV: return g_opt_bigconv;
     case STTS_OPT_HEAD: return g_opt_head;
     case STTS_OPT_SKEW: return g_opt_skew;
+    case STTS_OPT_FRONT: return g_opt_front;
     default: return ST_EINVAL;
   }
 }

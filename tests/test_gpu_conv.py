@@ -32,6 +32,11 @@ CASES = [
     ("rb128_k11_d5_nores", 128, 128, 11, 0, 1, 5, 25, 0, 1500, 3),
     ("rb128_k7_d1_nores", 128, 128, 7, 0, 1, 1, 3, 0, 511, 3),
     ("front_1090_1024", 1090, 1024, 3, 0, 1, 1, 1, 0, 40, 5),
+    # decoder front-end AdainResBlk1d convs on the bigconv2 engine (STTS_OPT_FRONT, bf16)
+    ("front_514_1024_nores", 514, 1024, 3, 0, 1, 1, 1, 0, 300, 5),
+    ("front_1024_1024", 1024, 1024, 3, 0, 1, 1, 1, 0, 400, 5),
+    ("front_1090_512", 1090, 512, 3, 0, 1, 1, 1, 0, 800, 5),
+    ("front_1090_512_nopro_nores", 1090, 512, 3, 0, 1, 1, 1, 0, 517, 0),
     ("sc_1x1", 514, 1024, 1, 0, 1, 1, 0, 0, 37, 0),
     ("istft_noise_s6", 22, 256, 12, 0, 6, 1, 3, 0, 481, 0),
     ("post_32_1", 32, 1, 7, 0, 1, 1, 3, 0, 999, 2),
@@ -169,3 +174,26 @@ def test_resblock_engines_many_tiles_per_workgroup(case):
     scale = max(1.0, y0.abs().max().item())
     assert (y - y0).abs().max().item() <= 2 ** -7 * scale, case[0]
     np.testing.assert_allclose(s.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
+
+
+FRONT_CASES = [c for c in CASES if c[0].startswith("front")]
+
+
+@pytest.mark.parametrize("cap", [0, 3])
+@pytest.mark.parametrize("case", FRONT_CASES, ids=[c[0] for c in FRONT_CASES])
+def test_front_engine_matches_igemm(case, cap):
+    """bf16: the front-end convs on the bigconv2 engine (C_in up to 1120, 256-channel output
+    parts, [AdaIN ->] LReLU prologue) against the igemm engine on the same launch; cap = 3 makes
+    every workgroup walk many tiles across output parts and utterances."""
+    try:
+        E.set_option(E.OPT_FRONT, 0)
+        _, y0, s0 = run_case(case, "bf16")
+        E.set_option(E.OPT_FRONT, 1)
+        E.set_option(E.OPT_GRID_CAP, cap)
+        _, y1, s1 = run_case(case, "bf16")
+    finally:
+        E.reset_options()
+    scale = max(1.0, y0.abs().max().item())
+    err = (y1 - y0).abs().max().item()
+    assert err <= 2 ** -7 * scale, f"{case[0]}: front engine vs igemm differ by {err}"
+    np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)

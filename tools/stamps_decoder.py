@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--skips", default="0", help="comma list of extra STTS_OPT_DEBUG phase-skip masks")
+    ap.add_argument("--set", action="append", default=[], help="KEY=VALUE options held for the run, e.g. 7=1 "
+                    "(resblocks on bigconv v1: the stamps then come from the front-end launches only)")
     a = ap.parse_args()
     ref = None
     for skip in (int(x) for x in a.skips.split(",")):
@@ -37,6 +39,9 @@ def run(a, skip):
     from stts2_mi355x import engine as E
     from stts2_mi355x import synth
     torch.cuda.set_device(0)
+    for kv in a.set:
+        k, v = (int(x) for x in kv.split("="))
+        E.set_option(k, v)
     dec, _ = bench.build_decoder("hifigan")
     eng = dec.cuda().engine("bf16")
     asr, f0, n, s = (torch.from_numpy(x).cuda() for x in synth.decoder_inputs(a.batch, a.frames))
