@@ -236,27 +236,34 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
         for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
     const bf16_t* xw = Xs + (size_t)(wm * FW + l32) * XP + hi * 8;
     const bf16_t* ww = Ws + (size_t)(wn * NTL * 32 + l32) * WP + hi * 8;
-#pragma unroll 1
-    for (int tap = 0; tap < ((p.dbg & 2) ? 0 : K); ++tap) {
+    // the (tap, chunk, k-half) steps fully unrolled with double-buffered fragments: the reads of
+    // step s+1 are issued before step s's MFMAs, so their LDS latency hides behind them (a read /
+    // wait / MFMA sequence per step left the loop latency-bound at C = 64, k7 / k11)
+    constexpr int S = K * NCH * 2;
+    auto ldfr = [&](int st, bf16x8 (&wa)[NTL], bf16x8 (&xb)[MT]) __attribute__((always_inline)) {
+      const int tap = st / (NCH * 2), c = (st / 2) % NCH, kk = st & 1;
       const bf16_t* xt = xw + tap * DIL * XP;
       const bf16_t* wt = ww + tap * C * WP;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c)
+      for (int ni = 0; ni < NTL; ++ni)
+        wa[ni] = *reinterpret_cast<const bf16x8*>(wt + (c * K * C + ni * 32) * WP + kk * 16);
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          bf16x8 wa[NTL], xb[MT];
+      for (int mi = 0; mi < MT; ++mi)
+        xb[mi] = *reinterpret_cast<const bf16x8*>(xt + mi * 32 * XP + c * 32 + kk * 16);
+    };
+    if (!(p.dbg & 2)) {
+      bf16x8 wa[2][NTL], xb[2][MT];
+      ldfr(0, wa[0], xb[0]);
+#pragma unroll
+      for (int st = 0; st < S; ++st) {
+        const int cb = st & 1;
+        if (st + 1 < S) ldfr(st + 1, wa[cb ^ 1], xb[cb ^ 1]);
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
           for (int ni = 0; ni < NTL; ++ni)
-            wa[ni] = *reinterpret_cast<const bf16x8*>(wt + (c * K * C + ni * 32) * WP + kk * 16);
-#pragma unroll
-          for (int mi = 0; mi < MT; ++mi)
-            xb[mi] = *reinterpret_cast<const bf16x8*>(xt + mi * 32 * XP + c * 32 + kk * 16);
-#pragma unroll
-          for (int mi = 0; mi < MT; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < NTL; ++ni)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ni], xb[mi], acc[mi][ni], 0, 0, 0);
-        }
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[cb][ni], xb[cb][mi], acc[mi][ni], 0, 0, 0);
+      }
     }
 
     // ---- epilogue: lane = frame l32 of block mi, channels (wn*NTL + ni)*32 + 16*hi + r
