@@ -208,9 +208,11 @@ const char* stts_error_string(int code);
  *                     256 x 128 tiles as there are CUs use 64 x 128 tiles; 0 = off (A/B). */
 #define STTS_OPT_SMALL_TILES 6
 /*   STTS_OPT_BIGCONV  2 (default) = the C = 128 / 256 resblock convs run on bigconv2.hip (per-wave
- *                     LDS-DMA weight rings, one barrier per 32-channel group), except C = 128 with
- *                     3 taps (bigconv.hip, measured faster); 1 = bigconv.hip everywhere; 3 =
- *                     bigconv2.hip everywhere with 4-wave blocks, two per CU (A/B). */
+ *                     LDS-DMA weight rings, one barrier per 32-channel group): 8-wave blocks, or
+ *                     4-wave blocks two per CU when a launch has fewer 8-wave tiles than CUs (small
+ *                     batches); C = 128 with 3 taps on bigconv.hip (measured faster); 1 =
+ *                     bigconv.hip everywhere; 3 = bigconv2.hip, 4-wave blocks; 4 = bigconv2.hip,
+ *                     8-wave blocks (A/B, tests). */
 #define STTS_OPT_BIGCONV 7
 /*   STTS_OPT_HEAD     1 (default) = the HiFi-GAN output head (Snake -> conv_post -> tanh) runs as one
  *                     streaming pass (head.hip); 0 = on the igemm engine (A/B). */
@@ -220,7 +222,8 @@ const char* stts_error_string(int code);
  *                     late, so two workgroups sharing a CU run out of phase (A/B experiments). */
 #define STTS_OPT_SKEW 9
 /*   STTS_OPT_FRONT    1 (default) = the decoder front-end's k3 AdainResBlk1d convs (C_out 1024 / 512)
- *                     run on the bigconv2 engine; 0 = on the igemm engine (A/B). */
+ *                     run on the bigconv2 engine when the launch has at least half as many tiles as
+ *                     CUs (else igemm: small batches); 2 = bigconv2 at any size (tests); 0 = igemm. */
 #define STTS_OPT_FRONT 10
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */

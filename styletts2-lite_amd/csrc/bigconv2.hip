@@ -741,8 +741,18 @@ bool st_bigconv2_eligible(const ConvParams& p) {
   if (p.res ? p.dil != 1 : (p.accb != nullptr)) return false;
   // mode 2 (default) keeps v1 where it measured faster: C = 128 with 3 taps (12 taps per tile, so
   // the per-tile window transform and epilogue dominate; profiles/r02_ab_bigconv_pipelined.txt)
-  if (g_opt_bigconv == 2 && p.Cout == 128 && p.KS == 3) return false;
+  if (g_opt_bigconv == 2 && p.Cout == 128 && p.KS == 3) return false;  // (modes 3 / 4: v2 everywhere)
   return true;  // on top of st_bigconv_eligible
+}
+
+static int b2_num_cu() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  return ncu;
 }
 
 // ---- decoder front-end (AdainResBlk1d k3 convs, hifigan.py:359-403 / 427-432): C_out 1024 / 512
@@ -752,6 +762,10 @@ int g_opt_front = 1;
 
 bool st_front_eligible(const ConvParams& p, int dtype) {
   if (!g_opt_front || dtype != ST_BF16) return false;
+  // few tiles (small batches: B = 1 has 8 at T = 400) leave the CUs idle behind long per-tile
+  // group chains; the igemm engine's smaller tiles do better there (profiles/r02_ab_b1.txt)
+  // (STTS_OPT_FRONT = 2 forces the engine at any size: tests)
+  if (g_opt_front == 1 && (long long)((p.Lq + 255) / 256) * (p.Cout / 256) * p.B < b2_num_cu() / 2) return false;
   if (p.Cout != 1024 && p.Cout != 512) return false;
   const int mode = p.pro.mode;
   if (mode != 0 && mode != PRO_LRELU && mode != (PRO_AFFINE | PRO_LRELU) && mode != PRO_AFFINE) return false;
@@ -772,8 +786,14 @@ int st_bigconv2_front(const ConvParams& p, hipStream_t s) {
   return ST_EINVAL;
 }
 
+
 int st_bigconv2(const ConvParams& p, hipStream_t stream) {
-  const bool two = g_opt_bigconv == 3;
+  // mode 3, or mode 2 with fewer 8-wave tiles than CUs (small batches: B = 1 at C = 256 has 32):
+  // 4-wave blocks, two per CU, twice the tiles (profiles/r02_ab_b1.txt: C = 256 k11 75 -> 61 us)
+  const int tm8 = p.Cout == 128 ? 512 : 256;
+  const long long tiles8 = (long long)((p.Lq + tm8 - 1) / tm8) * p.B;
+  // (mode 4 = 8-wave blocks at any size: tests)
+  const bool two = g_opt_bigconv == 3 || (g_opt_bigconv == 2 && tiles8 < b2_num_cu());
   if (p.Cout == 128) return two ? launch_b2_c<128, 4>(p, stream) : launch_b2_c<128, 8>(p, stream);
   if (p.Cout == 256) return two ? launch_b2_c<256, 4>(p, stream) : launch_b2_c<256, 8>(p, stream);
   return ST_EINVAL;

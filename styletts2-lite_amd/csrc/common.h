@@ -76,12 +76,20 @@ struct Prologue {
   int gb_C;              // C (offset of beta from gamma)
   const float* alpha;    // [C] snake alpha
   float slope;           // leaky-relu slope
+  // the producer spread its statistics over `stats_slots` copies stats_slot_bs doubles apart
+  // (small batches, ConvParams::stats_slots): the consumer sums them here, so no fold launch
+  int stats_slots;
+  long long stats_slot_bs;
 };
 
 // Per-(utterance, channel) AdaIN coefficients from raw stats: mean, a = (1+gamma)*rstd, beta.
 __device__ __forceinline__ void adain_coeffs(const Prologue& p, int b, int c, float& m, float& a, float& be) {
-  const double s = p.stats[((size_t)b * p.stats_ld + c) * 2 + 0];
-  const double ss = p.stats[((size_t)b * p.stats_ld + c) * 2 + 1];
+  const size_t i = ((size_t)b * p.stats_ld + c) * 2;
+  double s = p.stats[i], ss = p.stats[i + 1];
+  for (int k = 1; k < p.stats_slots; ++k) {
+    s += p.stats[(size_t)k * p.stats_slot_bs + i];
+    ss += p.stats[(size_t)k * p.stats_slot_bs + i + 1];
+  }
   const double mean = s * p.inv_n;
   double var = ss * p.inv_n - mean * mean;
   if (var < 0) var = 0;

@@ -451,6 +451,8 @@ Prologue pro_adain(Ctx& c, const WAdaIN& a, const double* stats, int stats_ld, i
   p.gb_C = a.C;
   p.alpha = alpha >= 0 ? c.P(alpha) : nullptr;
   p.slope = slope;
+  p.stats_slots = c.slots;  // every stats buffer of the arena has c.slots copies (unused ones zero)
+  p.stats_slot_bs = (long long)c.B * stats_ld * 2;
   return p;
 }
 
@@ -517,7 +519,7 @@ int conv_run(Ctx& c, ConvParams& p) {
   p.stats_slot_bs = (long long)c.B * p.stats_ld * 2;
   int r = st_conv1d(p, c.dtype, c.s);
   if (r) return r;
-  if (p.stats && c.slots > 1) ST_CHECK(st_stats_fold(p.stats, c.B, p.stats_ld, p.Cout, c.slots, p.stats_slot_bs, c.s));
+  // statistics slots are summed by the consumers' prologues (adain_coeffs): no fold launch
   if (prof) {
     // algorithmic work: a (transposed) conv is 2 * rows * N * Cin * taps flops on its GEMM view;
     // bytes = one read of the input, residual and running sum, one write of the output (none for a
@@ -539,7 +541,6 @@ int resfused_run(Ctx& c, ResFusedParams& p) {
   p.stats_slots = p.stats ? c.slots : 1;
   p.stats_slot_bs = (long long)c.B * p.stats_ld * 2;
   ST_CHECK(st_resfused(p, c.s));
-  if (p.stats && c.slots > 1) ST_CHECK(st_stats_fold(p.stats, c.B, p.stats_ld, p.C, c.slots, p.stats_slot_bs, c.s));
   if (prof) {
     // algorithmic work of the two convs; bytes = x once (window + residual), running sum, y
     const double fl = 2.0 * 2.0 * p.B * (double)p.L * p.C * p.C * p.K;
@@ -820,6 +821,9 @@ int decoder_forward(Ctx& c, const DecIO& io) {
       p.stats_ld = ld_cat;
     }
     RUN(conv_run(c, p));
+    // these statistics are copied slot 0 only into the other concat buffers' stats below: fold
+    if (w == 0 && c.slots > 1)
+      RUN(st_stats_fold(p.stats, c.B, p.stats_ld, p.Cout, c.slots, (long long)c.B * p.stats_ld * 2, c.s));
   }
   if (!c.dry) {  // the constant concat channels share their statistics across the 4 blocks
     for (int k = 1; k < 4; ++k)
@@ -1304,10 +1308,10 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_DEBUG: g_opt_debug = value; return 0;
     case STTS_OPT_STATS_SLOTS: g_opt_stats_slots = value > 0 ? value : 0; return 0;
     case STTS_OPT_SMALL_TILES: g_opt_small_tiles = value != 0; return 0;
-    case STTS_OPT_BIGCONV: g_opt_bigconv = (value >= 1 && value <= 3) ? value : 2; return 0;
+    case STTS_OPT_BIGCONV: g_opt_bigconv = (value >= 1 && value <= 4) ? value : 2; return 0;
     case STTS_OPT_HEAD: g_opt_head = value ? 1 : 0; return 0;
     case STTS_OPT_SKEW: g_opt_skew = value; return 0;
-    case STTS_OPT_FRONT: g_opt_front = value ? 1 : 0; return 0;
+    case STTS_OPT_FRONT: g_opt_front = (value >= 0 && value <= 2) ? value : 1; return 0;
     default: return ST_EINVAL;
   }
 }

@@ -141,12 +141,13 @@ def test_resconv_engine_matches_general_engine(case):
 WIDE_CASES = [c for c in RB_CASES if c[1] in (128, 256)]
 
 
-@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("mode", [2, 3, 4])
 @pytest.mark.parametrize("case", WIDE_CASES, ids=[c[0] for c in WIDE_CASES])
 def test_bigconv_v2_matches_v1(case, mode):
-    """bf16: the C = 128 / 256 resblock engine v2 (bigconv2.hip; mode 2 = 8-wave blocks, mode 3 =
-    4-wave blocks two per CU) against v1 (bigconv.hip) on the same launch: same bf16 operands and
-    transform, fp32 accumulation in a different order, statistics from the fp32 epilogue values."""
+    """bf16: the C = 128 / 256 resblock engine v2 (bigconv2.hip; mode 2 = automatic, mode 3 =
+    4-wave blocks two per CU, mode 4 = 8-wave blocks) against v1 (bigconv.hip) on the same launch:
+    same bf16 operands and transform, fp32 accumulation in a different order, statistics from the
+    fp32 epilogue values."""
     try:
         E.set_option(E.OPT_BIGCONV, 1)
         _, y1, s1 = run_case(case, "bf16")
@@ -188,7 +189,7 @@ def test_front_engine_matches_igemm(case, cap):
     try:
         E.set_option(E.OPT_FRONT, 0)
         _, y0, s0 = run_case(case, "bf16")
-        E.set_option(E.OPT_FRONT, 1)
+        E.set_option(E.OPT_FRONT, 2)  # the engine at any size (default 1 keeps small launches on igemm)
         E.set_option(E.OPT_GRID_CAP, cap)
         _, y1, s1 = run_case(case, "bf16")
     finally:
@@ -197,3 +198,19 @@ def test_front_engine_matches_igemm(case, cap):
     err = (y1 - y0).abs().max().item()
     assert err <= 2 ** -7 * scale, f"{case[0]}: front engine vs igemm differ by {err}"
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("case", WIDE_CASES, ids=[c[0] for c in WIDE_CASES])
+def test_bigconv_8wave_many_tiles_per_workgroup(case):
+    """The 8-wave bigconv2 blocks (STTS_OPT_BIGCONV = 4; at these small sizes the automatic mode
+    picks 4-wave blocks) with the grid capped at 3 workgroups: long tile walks across utterances."""
+    try:
+        E.set_option(E.OPT_BIGCONV, 4)
+        _, y0, s0 = run_case(case, "bf16")
+        E.set_option(E.OPT_GRID_CAP, 3)
+        _, y, s = run_case(case, "bf16")
+    finally:
+        E.reset_options()
+    scale = max(1.0, y0.abs().max().item())
+    assert (y - y0).abs().max().item() <= 2 ** -7 * scale, case[0]
+    np.testing.assert_allclose(s.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
