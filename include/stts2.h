@@ -34,6 +34,8 @@ typedef struct stts_model stts_model;
 #define STTS_KIND_ISTFTNET 1 /* Modules/istftnet.py Decoder  */
 #define STTS_KIND_F0N 2      /* models.py ProsodyPredictor F0/N conv stacks */
 #define STTS_KIND_STYLE 3    /* models.py StyleEncoder       */
+#define STTS_KIND_MPD 4      /* Modules/discriminators.py MultiPeriodDiscriminator (training step, config 5);
+                                cfg = {n, period_1 .. period_n}, the reference's {5, 2, 3, 5, 7, 11} */
 
 /* compute / activation dtypes */
 #define STTS_FP32 0 /* fp32 storage, exact-fp32 MFMA (parity mode)          */
@@ -88,6 +90,23 @@ int stts_f0n_fwd(stts_model* m, int dtype, const float* x, const float* s, int B
 /* Style encoder: mel [B][1][80][T] -> style [B][style_dim]. */
 int stts_style_fwd(stts_model* m, int dtype, const float* mel, int B, int T, float* out, void* workspace,
                    long long ws_bytes, void* stream);
+
+/* MultiPeriodDiscriminator forward, <- Modules/discriminators.py:108-129 DiscriminatorP.forward for
+ * every period (MultiPeriodDiscriminator.forward :143-156 calls it on y and y_hat: pass both as one
+ * batch).  wave [B][T] fp32 (the reference's [B, 1, T]).  out (fp32, >= stts_mpd_out_elems) receives,
+ * period by period, the 6 feature maps of fmap (:118-128, LeakyReLU(0.1) applied to the first 5) as
+ * frames [B*p][L_j][C_j], row b*p + j = column j of utterance b: the reference's [B, C_j, L_j, p]
+ * tensor is its permutation; the last map (C = 1) flattened is the score.  Workspace:
+ * stts_workspace_bytes(m, dtype, B, T).  T must exceed each period's reflect pad, as in the reference. */
+long long stts_mpd_out_elems(const stts_model* m, int B, int T);
+int stts_mpd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, float* out, long long out_elems,
+                 void* workspace, long long ws_bytes, void* stream);
+/* GAN losses over stts_mpd_fwd's output for a batch of 2B = B real then B generated waveforms,
+ * <- losses.py:97-128 feature_loss(fmap_r, fmap_g), generator_loss(y_d_gs)[0] and
+ * discriminator_loss(y_d_rs, y_d_gs)[0] over the MultiPeriodDiscriminator outputs.  loss (device,
+ * 3 doubles) = {feature, generator, discriminator}; scratch (device) >= 4 * 6 * n_periods doubles. */
+int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
+                    void* stream);
 
 /* Style front-end, <- inference.py:43-49 Preprocess.wave_preprocess(wave) (the torchaudio
  * MelSpectrogram(n_mels=80, n_fft=2048, win_length=1200, hop_length=300) it builds, then

@@ -550,3 +550,40 @@ def generate(sentences, s, te_sd, pp_sd, dec_sd, dec_cfg, zs, noise_fns, stabili
         wavs.append(wav.numpy()[4000:-4000])
     out = np.concatenate(wavs)
     return np.concatenate([np.zeros([4000]), out, np.zeros([4000])], axis=0)
+
+
+# ----------------------------------------------------------------------- training step (§8(f) rank 3)
+MPD_PERIODS = (2, 3, 5, 7, 11)
+
+
+def discriminator_p(x, sd, prefix, period):
+    """DiscriminatorP.forward (Modules/discriminators.py:108-129): x [B, 1, T] -> (score, fmap)."""
+    b, c, t = x.shape
+    if t % period != 0:  # :112-115 reflect pad on the right
+        n_pad = period - (t % period)
+        x = F.pad(x, (0, n_pad), "reflect")
+        t = t + n_pad
+    x = x.view(b, c, t // period, period)
+    fmap = []
+    for j in range(5):  # :117-120
+        p = f"{prefix}.convs.{j}"
+        x = F.conv2d(x, wn(sd, p), _t(sd, p + ".bias"), (3 if j < 4 else 1, 1), (2, 0))
+        x = F.leaky_relu(x, 0.1)
+        fmap.append(x)
+    p = f"{prefix}.conv_post"
+    x = F.conv2d(x, wn(sd, p), _t(sd, p + ".bias"), 1, (1, 0))  # :121-122
+    fmap.append(x)
+    return torch.flatten(x, 1, -1), fmap
+
+
+def mpd(y, y_hat, sd, periods=MPD_PERIODS):
+    """MultiPeriodDiscriminator.forward (discriminators.py:143-156)."""
+    y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
+    for i, p in enumerate(periods):
+        r, fr = discriminator_p(y, sd, f"discriminators.{i}", p)
+        g, fg = discriminator_p(y_hat, sd, f"discriminators.{i}", p)
+        y_d_rs.append(r)
+        y_d_gs.append(g)
+        fmap_rs.append(fr)
+        fmap_gs.append(fg)
+    return y_d_rs, y_d_gs, fmap_rs, fmap_gs

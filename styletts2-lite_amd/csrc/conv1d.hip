@@ -620,6 +620,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
                     for (int i = 0; i < 8; ++i) pw(v, i, pr(r, i) + pr(v, i));
                   }
                 }
+                if (p.epi_lrelu) {
+#pragma unroll
+                  for (int j = 0; j < 16; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * p.epi_slope;
+                }
                 store16(yT + (size_t)orow * p.y_ld + co0, v);
                 if constexpr (!C::BF) {
 #pragma unroll
@@ -642,6 +646,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
                   x = v[j] + bias_s[nl + j];
                   if (resb) x = (x + to_f32(resb[(size_t)(orow >> p.res_shift) * p.res_ld + co])) * p.out_scale;
                   if (p.epi_tanh) x = tanhf(x);
+                  if (p.epi_lrelu) x = x > 0.f ? x : x * p.epi_slope;
                   if (p.y_f32) {
                     yF[(size_t)orow * p.y_ld + co] = x;
                   } else {

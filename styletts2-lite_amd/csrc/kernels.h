@@ -35,6 +35,8 @@ struct ConvParams {
   int acc_ld;
   float acc_div;
   int epi_tanh, reflect_front;
+  int epi_lrelu;      // LeakyReLU(epi_slope) on the stored output (discriminator feature maps)
+  float epi_slope;
   double* stats;  // [B][stats_ld][2] accumulated statistics of the stored output
   int stats_ld;
   // small-batch atomic spreading: workgroup g accumulates into slot g % stats_slots, the slot
@@ -181,6 +183,17 @@ int st_pack_conv(const float* w, int Cin, int Cout, int K, int transposed, int u
 size_t st_packed_conv_elems(int Cin, int Cout, int K, int transposed, int u);
 // frames (dtype) [B][L][ld] -> fp32 frames [B][L][C]
 int st_frames_to_f32(const void* src, int B, int L, int C, int ld, float* dst, int dtype, hipStream_t s);
+// GAN losses over the MPD engine's outputs (misc.hip): per (period, layer) block, its offset, the
+// size of its real half, and whether it is a score block (conv_post)
+constexpr int kMpdMaxSegs = 64;
+struct MpdLossSegs {
+  int n;
+  long long off[kMpdMaxSegs], half[kMpdMaxSegs];
+  int score[kMpdMaxSegs];
+};
+int st_mpd_losses(const float* out, const MpdLossSegs& sg, double* sums, double* loss, hipStream_t s);
+// DiscriminatorP input: waveform [B][Tn] -> frames [B*p][L0][8] (reflect pad to L0*p)
+int st_period_frames(const float* wave, int B, int Tn, int p, int L0, void* dst, int dtype, hipStream_t s);
 // ---------------------------------------------------------------- style encoder (2-D, padded NHWC)
 // An image [H][W] is stored zero-padded as rows (H+2)*(W+2) of ld channels ("padded frames").
 // mel fp32 [B][1][H][W] -> padded frames (channel 0), ld = 8

@@ -691,6 +691,96 @@ int st_frames_convert(const float* src, int B, int L, int C, int ld_in, void* ds
   return (int)hipGetLastError();
 }
 
+// DiscriminatorP 1-d -> 2-d (Modules/discriminators.py:112-118): the waveform reflect-padded on the
+// right to a multiple of the period p and viewed [B, 1, T/p, p]; its (k, 1) convs run along T/p
+// for every column j, so column j of utterance b becomes frames row b*p + j: [B*p][L0][8]
+// (channel 0 = the sample, channels 1..7 zero: the frames layout pads channels to 8)
+template <typename T>
+__global__ void __launch_bounds__(256) k_period_frames(const float* __restrict__ wave, int Tn, int p, int L0,
+                                                       long long rows, T* __restrict__ dst) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * L0) return;
+  const long long r = i / L0;
+  const int t = (int)(i - r * L0);
+  const int b = (int)(r / p), j = (int)(r - (long long)b * p);
+  int k = t * p + j;
+  if (k >= Tn) k = 2 * (Tn - 1) - k;  // F.pad(..., "reflect") on the right
+  T o[8];
+  o[0] = from_f32<T>(wave[(size_t)b * Tn + k]);
+#pragma unroll
+  for (int c = 1; c < 8; ++c) o[c] = from_f32<T>(0.f);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) dst[i * 8 + c] = o[c];
+}
+
+int st_period_frames(const float* wave, int B, int Tn, int p, int L0, void* dst, int dtype, hipStream_t s) {
+  if (B <= 0 || Tn <= 0 || p <= 0 || L0 * p < Tn || L0 * p - Tn >= Tn) return ST_EINVAL;
+  const long long rows = (long long)B * p, n = rows * L0;
+  dim3 grid((unsigned)((n + 255) / 256));
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_period_frames<T>, grid, dim3(256), 0, s, wave, Tn, p, L0, rows,
+                                              reinterpret_cast<T*>(dst)));
+  return (int)hipGetLastError();
+}
+
+// GAN losses over the MPD outputs (losses.py:97-128): each (period, layer) block of the engine's
+// output holds the real half then the generated half (same element order), so
+//   feature_loss = 2 sum_blocks mean|r - g|,  generator_loss = sum_periods mean((1 - g)^2),
+//   discriminator_loss = sum_periods mean((1 - r)^2) + mean(g^2)   (scores = the conv_post blocks)
+// Per-block sums: fp32 per thread, fp64 per workgroup (atomics); k_mpd_loss_final combines them.
+__global__ void __launch_bounds__(256) k_mpd_loss_sums(const float* __restrict__ out, MpdLossSegs sg,
+                                                       double* __restrict__ sums) {
+  const int seg = blockIdx.y;
+  if (seg >= sg.n) return;
+  const long long half = sg.half[seg];
+  const float* r = out + sg.off[seg];
+  const float* g = r + half;
+  float a = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < half; i += (long long)gridDim.x * 256) {
+    const float x = r[i], y = g[i];
+    a += fabsf(x - y);
+    if (sg.score[seg]) {
+      q1 += (1.f - x) * (1.f - x);
+      q2 += (1.f - y) * (1.f - y);
+      q3 += y * y;
+    }
+  }
+  float v[4] = {a, q1, q2, q3};
+  __shared__ float red[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    for (int o = 32; o >= 1; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    atomicAdd(sums + seg * 4 + k, (double)red[k][0] + red[k][1] + red[k][2] + red[k][3]);
+  }
+}
+
+__global__ void k_mpd_loss_final(MpdLossSegs sg, const double* __restrict__ sums, double* __restrict__ loss) {
+  double fm = 0, gen = 0, disc = 0;
+  for (int s = 0; s < sg.n; ++s) {
+    const double n = (double)sg.half[s];
+    fm += sums[s * 4] / n;
+    if (sg.score[s]) {
+      gen += sums[s * 4 + 2] / n;
+      disc += (sums[s * 4 + 1] + sums[s * 4 + 3]) / n;
+    }
+  }
+  loss[0] = 2.0 * fm;
+  loss[1] = gen;
+  loss[2] = disc;
+}
+
+int st_mpd_losses(const float* out, const MpdLossSegs& sg, double* sums, double* loss, hipStream_t s) {
+  if (sg.n <= 0 || sg.n > kMpdMaxSegs) return ST_EINVAL;
+  ST_CHECK_HIP(hipMemsetAsync(sums, 0, sizeof(double) * 4 * sg.n, s));
+  hipLaunchKernelGGL(k_mpd_loss_sums, dim3(64, sg.n), dim3(256), 0, s, out, sg, sums);
+  hipLaunchKernelGGL(k_mpd_loss_final, dim3(1), dim3(1), 0, s, sg, sums, loss);
+  return (int)hipGetLastError();
+}
+
 int st_frames_to_f32(const void* src, int B, int L, int C, int ld, float* dst, int dtype, hipStream_t s) {
   dim3 grid((unsigned)(((size_t)L * C + 255) / 256), B);
   DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_frames_to_f32<T>, grid, dim3(256), 0, s,

@@ -118,6 +118,12 @@ struct stts_model {
   } se_blk[4];
   WConv se_conv0, se_last;
   int se_lin_w = -1, se_lin_b = -1, se_dim = 0;
+  // -------- MultiPeriodDiscriminator (Modules/discriminators.py:96-156)
+  struct DiscP {
+    int period = 0;
+    WConv convs[5], post;
+  };
+  std::vector<DiscP> mpd;
   // -------- AdaIN projections (all AdaIN layers share one GEMV: H = s @ Wt + b)
   std::vector<WAdaIN*> adains;
   int Htot = 0;
@@ -331,6 +337,44 @@ int build_style(Model& m, const int* cfg, int n) {
   m.se_lin_b = m.P.add("unshared.bias", m.style_dim);
   m.se_dim = d;
   return ST_OK;
+}
+
+// MultiPeriodDiscriminator: DiscriminatorP(p) for each period (discriminators.py:132-141); each is
+// 5 weight-norm Conv2d (k, 1) stride (3, 1) [the last stride 1] + conv_post (3, 1)
+// (discriminators.py:96-106), i.e. 1-d convs along T/p with the same weight memory layout
+constexpr int kMpdCh[6] = {1, 32, 128, 512, 1024, 1024};
+int build_mpd(Model& m, const int* cfg, int n) {
+  if (n < 2 || cfg[0] != n - 1) return ST_EINVAL;
+  m.mpd.resize(cfg[0]);  // sized once: add_wconv keeps pointers into it
+  for (int i = 0; i < cfg[0]; ++i) {
+    if (cfg[1 + i] < 1) return ST_EINVAL;
+    auto& d = m.mpd[i];
+    d.period = cfg[1 + i];
+    const std::string p = "discriminators." + std::to_string(i);
+    for (int j = 0; j < 5; ++j)
+      add_wconv(m, d.convs[j], p + ".convs." + std::to_string(j), kMpdCh[j], kMpdCh[j + 1], 5, true, true);
+    add_wconv(m, d.post, p + ".conv_post", 1024, 1, 3, true, true);
+  }
+  return ST_OK;
+}
+
+// per-layer frame counts of DiscriminatorP(p) over Tn samples: L[0] = ceil(Tn / p), then the 4
+// stride-3 convs (k5, pad 2), then the stride-1 conv and conv_post keep L[4]
+void mpd_lengths(int Tn, int p, int (&L)[6]) {
+  L[0] = (Tn + p - 1) / p;
+  for (int j = 0; j < 4; ++j) L[j + 1] = (L[j] + 4 - 5) / 3 + 1;
+  L[5] = L[4];
+}
+
+long long mpd_out_elems(const Model& m, int B, int Tn) {
+  long long n = 0;
+  for (const auto& d : m.mpd) {
+    int L[6];
+    mpd_lengths(Tn, d.period, L);
+    for (int j = 0; j < 5; ++j) n += (long long)B * d.period * L[j + 1] * kMpdCh[j + 1];
+    n += (long long)B * d.period * L[5];
+  }
+  return n;
 }
 
 void finalize_layout(Model& m) {
@@ -962,6 +1006,55 @@ int decoder_forward(Ctx& c, const DecIO& io) {
   return 0;
 }
 
+// --------------------------------------------------------------------- MPD forward
+// DiscriminatorP.forward (discriminators.py:108-129) for every period: reflect pad + 1-d -> 2-d
+// view (k_period_frames), 5 convs with LeakyReLU(0.1) fused into the epilogue (the activated
+// output is the feature map AND the next conv's input), conv_post.  `out` (fp32) receives, per
+// period in order, the 6 feature maps as frames [B*p][L_j][C_j] (the reference's [B, C_j, L_j, p]
+// tensors permuted; conv_post's map, C = 1, is also the score before flatten).
+int mpd_forward(Ctx& c, const float* wave, int Tn, float* out) {
+  Model& m = *c.m;
+  const int B0 = c.B;
+  size_t off = 0;
+  for (const auto& d : m.mpd) {
+    const int p = d.period;
+    int L[6];
+    mpd_lengths(Tn, p, L);
+    c.B = B0 * p;  // the conv batch: every (utterance, column) sequence
+    Buf x = c.frames(L[0], 8);
+    RUN(st_period_frames(wave, B0, Tn, p, L[0], x.p, c.dtype, c.s));
+    for (int j = 0; j < 5; ++j) {
+      Buf y = c.frames(L[j + 1], kMpdCh[j + 1]);
+      ConvParams q = conv_base(c, d.convs[j], x, 0);
+      q.stride = j < 4 ? 3 : 1;
+      q.pad = 2;
+      q.Lq = L[j + 1];
+      conv_out(q, c, y, 0, L[j + 1]);
+      q.epi_lrelu = 1;
+      q.epi_slope = 0.1f;  // LRELU_SLOPE (discriminators.py:9)
+      RUN(conv_run(c, q));
+      RUN(st_frames_to_f32(y.p, c.B, L[j + 1], kMpdCh[j + 1], y.ld, out ? out + off : nullptr, c.dtype, c.s));
+      off += (size_t)c.B * L[j + 1] * kMpdCh[j + 1];
+      x = y;
+    }
+    {
+      ConvParams q = conv_base(c, d.post, x, 0);
+      q.pad = 1;
+      q.Lq = L[5];
+      q.y = out ? out + off : nullptr;
+      q.y_bs = L[5];
+      q.y_ld = 1;
+      q.y_f32 = 1;
+      q.Lout = L[5];
+      RUN(conv_run(c, q));
+      off += (size_t)c.B * L[5];
+    }
+    c.B = B0;
+  }
+  c.stats_begin = c.stats_off = c.off;  // no statistics: the workspace is the buffers above
+  return 0;
+}
+
 // --------------------------------------------------------------------- F0/N forward
 int f0n_forward(Ctx& c, const float* x, const float* s, int T, float* F0, float* Nout) {
   Model& m = *c.m;
@@ -1154,7 +1247,9 @@ int with_ctx(Model* m, int dtype, int B, void* ws, long long ws_bytes, void* str
   c.packed = m->packed[dtype];
   c.aux = m->packed[dtype] ? const_cast<char*>(m->packed[dtype]) + m->aux_off[dtype] : nullptr;
   ST_CHECK(body(c));  // dry run: layout
-  const size_t total = c.stats_off;
+  // the statistics region follows the buffers (stats_off >= off when the body set it); a body
+  // without statistics may leave it unset: the buffers alone then size the workspace
+  const size_t total = std::max(c.stats_off, c.off);
   if (need) {
     *need = total;
     return 0;
@@ -1187,6 +1282,8 @@ int stts_model_create(int kind, const int* cfg, int ncfg, stts_model** out) {
     r = build_f0n(*m, cfg, ncfg);
   else if (kind == STTS_KIND_STYLE)
     r = build_style(*m, cfg, ncfg);
+  else if (kind == STTS_KIND_MPD)
+    r = build_mpd(*m, cfg, ncfg);
   if (r != 0) {
     delete m;
     return r;
@@ -1245,6 +1342,9 @@ long long stts_workspace_bytes(const stts_model* mc, int dtype, int B, int T) {
   } else if (m->kind == STTS_KIND_F0N) {
     r = with_ctx(m, dtype, B, nullptr, 0, nullptr,
                  [&](Ctx& c) { return f0n_forward(c, nullptr, nullptr, T, nullptr, nullptr); }, &need);
+  } else if (m->kind == STTS_KIND_MPD) {
+    r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return mpd_forward(c, nullptr, T, nullptr); },
+                 &need);
   } else {
     r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return style_forward(c, nullptr, T, nullptr); },
                  &need);
@@ -1277,6 +1377,44 @@ int stts_style_fwd(stts_model* m, int dtype, const float* mel, int B, int T, flo
   if (B <= 0 || T <= 0 || !mel || !out) return ST_EINVAL;
   ST_CHECK(check_params(*m));
   return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return style_forward(c, mel, T, out); }, nullptr);
+}
+
+long long stts_mpd_out_elems(const stts_model* m, int B, int T) {
+  if (!m || m->kind != STTS_KIND_MPD || B <= 0 || T <= 0) return ST_EINVAL;
+  return mpd_out_elems(*m, B, T);
+}
+
+int stts_mpd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, float* out, long long out_elems,
+                 void* ws, long long ws_bytes, void* stream) {
+  if (!m || m->kind != STTS_KIND_MPD) return ST_EINVAL;
+  if (B <= 0 || !wave || !out) return ST_EINVAL;
+  for (const auto& d : m->mpd)  // the reference's reflect pad needs the pad < T
+    if (T < 2 || (T + d.period - 1) / d.period * d.period - T >= T) return ST_EINVAL;
+  if (out_elems < mpd_out_elems(*m, B, T)) return ST_EINVAL;
+  ST_CHECK(check_params(*m));
+  return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return mpd_forward(c, wave, T, out); }, nullptr);
+}
+
+int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
+                    void* stream) {
+  if (!m || m->kind != STTS_KIND_MPD || B <= 0 || T <= 0 || !out || !scratch || !loss) return ST_EINVAL;
+  MpdLossSegs sg;
+  memset(&sg, 0, sizeof(sg));
+  long long off = 0;
+  for (const auto& d : m->mpd) {
+    int L[6];
+    mpd_lengths(T, d.period, L);
+    for (int j = 0; j < 6; ++j) {
+      if (sg.n >= kMpdMaxSegs) return ST_EINVAL;
+      const long long half = (long long)B * d.period * L[j < 5 ? j + 1 : 5] * kMpdCh[j < 5 ? j + 1 : 0];
+      sg.off[sg.n] = off;
+      sg.half[sg.n] = half;
+      sg.score[sg.n] = j == 5;
+      ++sg.n;
+      off += 2 * half;
+    }
+  }
+  return st_mpd_losses(out, sg, scratch, loss, (hipStream_t)stream);
 }
 
 long long stts_mel_frames(long long L) { return st_mel_frames(L); }

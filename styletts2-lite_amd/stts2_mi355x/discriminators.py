@@ -1,0 +1,78 @@
+"""Drop-in MultiPeriodDiscriminator (Modules/discriminators.py:96-156) for the training step
+(SURVEY §8(f) rank 3, config 5): same constructor, sub-module names and state-dict keys
+(`discriminators.{i}.convs.{j}.weight_g / weight_v / bias`, `discriminators.{i}.conv_post.*`), the
+forward on the HIP engine (stts_mpd_fwd).  Forward only: the reference trains these with autograd;
+backward kernels are not built.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+from torch.nn import Conv2d
+from torch.nn.utils import weight_norm
+
+LRELU_SLOPE = 0.1
+
+
+def get_padding(kernel_size, dilation=1):
+    return int((kernel_size * dilation - dilation) / 2)
+
+
+class DiscriminatorP(nn.Module):
+    """Parameter holder with the reference's layout (discriminators.py:96-106)."""
+
+    def __init__(self, period, kernel_size=5, stride=3, use_spectral_norm=False):
+        super().__init__()
+        if use_spectral_norm or kernel_size != 5 or stride != 3:
+            raise NotImplementedError("the HIP engine implements the reference's weight-norm k5 / s3 configuration")
+        self.period = period
+        self.convs = nn.ModuleList([
+            weight_norm(Conv2d(1, 32, (kernel_size, 1), (stride, 1), padding=(get_padding(5, 1), 0))),
+            weight_norm(Conv2d(32, 128, (kernel_size, 1), (stride, 1), padding=(get_padding(5, 1), 0))),
+            weight_norm(Conv2d(128, 512, (kernel_size, 1), (stride, 1), padding=(get_padding(5, 1), 0))),
+            weight_norm(Conv2d(512, 1024, (kernel_size, 1), (stride, 1), padding=(get_padding(5, 1), 0))),
+            weight_norm(Conv2d(1024, 1024, (kernel_size, 1), 1, padding=(2, 0))),
+        ])
+        self.conv_post = weight_norm(Conv2d(1024, 1, (3, 1), 1, padding=(1, 0)))
+
+
+class MultiPeriodDiscriminator(nn.Module):
+    """MultiPeriodDiscriminator (discriminators.py:132-156) on the HIP engine.
+
+    forward(y, y_hat) -> (y_d_rs, y_d_gs, fmap_rs, fmap_gs) as the reference: one score
+    [B, L*p] and six feature maps [B, C, L, p] per period (the maps are permuted views of the
+    engine's frames layout).  y and y_hat go through the engine as one batch."""
+
+    def __init__(self, periods=(2, 3, 5, 7, 11)):
+        super().__init__()
+        self.discriminators = nn.ModuleList([DiscriminatorP(p) for p in periods])
+        self._engine = None
+
+    def engine(self, dtype="fp32"):
+        from .engine import MPDEngine
+        if self._engine is None or self._engine.dtype != dtype or self._engine.stale(self):
+            self._engine = MPDEngine(self, dtype=dtype)
+        return self._engine
+
+    def invalidate(self):
+        self._engine = None
+
+    def forward(self, y, y_hat, dtype="fp32"):
+        B = y.shape[0]
+        res = self.engine(dtype).forward(torch.cat([y, y_hat], 0))
+        y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
+        for score, fmaps in res:
+            y_d_rs.append(score[:B])
+            y_d_gs.append(score[B:])
+            fmap_rs.append([f[:B] for f in fmaps])
+            fmap_gs.append([f[B:] for f in fmaps])
+        return y_d_rs, y_d_gs, fmap_rs, fmap_gs
+
+
+def mpd_gan_losses(mpd: MultiPeriodDiscriminator, y, y_hat, dtype="fp32"):
+    """One MPD forward of (y, y_hat) and, on the device, the reference's
+    feature_loss(fmap_rs, fmap_gs), generator_loss(y_d_gs)[0] and discriminator_loss(y_d_rs, y_d_gs)[0]
+    (losses.py:97-128) over its outputs -> (feature, generator, discriminator) float64 scalars."""
+    mpd(y, y_hat, dtype=dtype)
+    loss = mpd.engine(dtype).gan_losses()
+    return loss[0], loss[1], loss[2]

@@ -14,7 +14,7 @@ import os
 import numpy as np
 import torch
 
-KIND_HIFIGAN, KIND_ISTFTNET, KIND_F0N, KIND_STYLE = 0, 1, 2, 3
+KIND_HIFIGAN, KIND_ISTFTNET, KIND_F0N, KIND_STYLE, KIND_MPD = 0, 1, 2, 3, 4
 DTYPES = {"fp32": 0, "bf16": 1}
 
 _LIB = None
@@ -58,6 +58,12 @@ def lib():
     L.stts_f0n_fwd.restype = c_int
     L.stts_style_fwd.argtypes = [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_ll, c_vp]
     L.stts_style_fwd.restype = c_int
+    L.stts_mpd_out_elems.argtypes = [c_vp, c_int, c_int]
+    L.stts_mpd_out_elems.restype = c_ll
+    L.stts_mpd_fwd.argtypes = [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_ll, c_vp, c_ll, c_vp]
+    L.stts_mpd_fwd.restype = c_int
+    L.stts_mpd_losses.argtypes = [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]
+    L.stts_mpd_losses.restype = c_int
     L.stts_mel_frames.argtypes = [c_ll]
     L.stts_mel_frames.restype = c_ll
     L.stts_mel_workspace_bytes.argtypes = []
@@ -337,6 +343,73 @@ class StyleEngine(_Engine):
         check(lib().stts_style_fwd(self.model.h, DTYPES[self.dtype], _ptr(mel), B, T, _ptr(out), _ptr(ws), nb,
                                    _stream()), "stts_style_fwd")
         return out if in_dev.type == "cuda" else out.to(in_dev)
+
+
+MPD_CH = (1, 32, 128, 512, 1024, 1024, 1)
+
+
+def mpd_lengths(T: int, p: int):
+    """Frame counts of DiscriminatorP(p)'s 6 feature maps over T samples (plan.cpp mpd_lengths)."""
+    L = [(T + p - 1) // p]
+    for _ in range(4):
+        L.append((L[-1] + 4 - 5) // 3 + 1)
+    L.append(L[-1])
+    return L
+
+
+class MPDEngine(_Engine):
+    """HIP forward of Modules/discriminators.py MultiPeriodDiscriminator's DiscriminatorP stacks
+    (reference :108-129): one batch of waveforms [B, 1, T] -> per period (scores [B, L*p], fmaps)."""
+
+    def __init__(self, module, dtype="fp32"):
+        super().__init__(module, dtype)
+        self.periods = [d.period for d in module.discriminators]
+        self.model = NativeModel(KIND_MPD, [len(self.periods), *self.periods], module)
+        self.model.pack(dtype)
+
+    def forward(self, x):
+        dev = self.model.device
+        in_dev = x.device
+        w = _dev_f32(x, dev)
+        if w.dim() != 3 or w.shape[1] != 1:
+            raise ValueError(f"waveform must be [B, 1, T], got {tuple(w.shape)}")
+        B, _, T = w.shape
+        for p in self.periods:
+            if (-T) % p >= T:
+                raise ValueError(f"T = {T} too short for the period-{p} reflect pad")
+        n = lib().stts_mpd_out_elems(self.model.h, B, T)
+        check(int(n) if n < 0 else 0, "stts_mpd_out_elems")
+        out = torch.empty(int(n), dtype=torch.float32, device=dev)
+        ws, nb = self.model.workspace(self.dtype, B, T)
+        check(lib().stts_mpd_fwd(self.model.h, DTYPES[self.dtype], _ptr(w), B, T, _ptr(out), int(n), _ptr(ws), nb,
+                                 _stream()), "stts_mpd_fwd")
+        self.last = (out, B, T)
+        res, off = [], 0
+        for p in self.periods:
+            L = mpd_lengths(T, p)
+            fmaps = []
+            for j in range(6):
+                C, Lj = MPD_CH[j + 1], L[j + 1] if j < 5 else L[5]
+                k = B * p * Lj * C
+                # frames [B*p][L][C] -> the reference's [B, C, L, p] (a permuted view)
+                f = out[off:off + k].view(B, p, Lj, C).permute(0, 3, 2, 1)
+                fmaps.append(f if in_dev.type == "cuda" else f.to(in_dev))
+                off += k
+            score = torch.flatten(fmaps[-1], 1, -1)  # discriminators.py:129
+            res.append((score, fmaps))
+        return res
+
+    def gan_losses(self):
+        """losses.py:97-128 feature_loss, generator_loss[0], discriminator_loss[0] of the last
+        forward, whose batch was B real then B generated waveforms: device float64 tensor [3]."""
+        out, B2, T = self.last
+        if B2 % 2:
+            raise ValueError("the last forward's batch is not real + generated halves")
+        scratch = torch.zeros(4 * 6 * len(self.periods), dtype=torch.float64, device=out.device)
+        loss = torch.empty(3, dtype=torch.float64, device=out.device)
+        check(lib().stts_mpd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), _ptr(loss), _stream()),
+              "stts_mpd_losses")
+        return loss
 
 
 N_MELS, MEL_HOP, MEL_NFFT = 80, 300, 2048
