@@ -6,6 +6,7 @@
  *
  *   stts_decoder_fwd  <- Modules/hifigan.py:446  Decoder.forward(asr, F0_curve, N, s)
  *                        Modules/istftnet.py:692 Decoder.forward(asr, F0_curve, N, s)
+ *                        Modules/vocos.py:392    Decoder.forward(asr, F0_curve, N, s)
  *   stts_f0n_fwd      <- models.py:448           ProsodyPredictor.F0Ntrain(x, s)  (conv stacks
  *                        after the shared BiLSTM, models.py:451-461)
  *   stts_style_fwd    <- models.py:145           StyleEncoder.forward(x)
@@ -36,6 +37,7 @@ typedef struct stts_model stts_model;
 #define STTS_KIND_STYLE 3    /* models.py StyleEncoder       */
 #define STTS_KIND_MPD 4      /* Modules/discriminators.py MultiPeriodDiscriminator (training step, config 5);
                                 cfg = {n, period_1 .. period_n}, the reference's {5, 2, 3, 5, 7, 11} */
+#define STTS_KIND_VOCOS 5    /* Modules/vocos.py Decoder (front-end + ConvNeXt generator + ISTFTHead) */
 
 /* compute / activation dtypes */
 #define STTS_FP32 0 /* fp32 storage, exact-fp32 MFMA (parity mode)          */
@@ -55,6 +57,10 @@ typedef struct stts_model stts_model;
  *             (reference Decoder(dim_in, style_dim, resblock_kernel_sizes, upsample_rates,
  *              upsample_initial_channel, resblock_dilation_sizes, upsample_kernel_sizes))
  *   ISTFTNET: as HIFIGAN, then gen_istft_n_fft, gen_istft_hop_size
+ *   VOCOS   : dim_in (512), style_dim, intermediate_dim, num_layers, gen_istft_n_fft, gen_istft_hop_size
+ *             (reference vocos.Decoder(dim_in, style_dim, dim_out, intermediate_dim, num_layers,
+ *              gen_istft_n_fft, gen_istft_hop_size), inference.py:112-118; weight-norm parameters
+ *              are named <layer>.parametrizations.weight.original0 / original1 there)
  *   F0N     : d_hid, style_dim                     (ProsodyPredictor(style_dim, d_hid, ...))
  *   STYLE   : dim_in, style_dim, max_conv_dim      (StyleEncoder(dim_in, style_dim, max_conv_dim))
  */
@@ -75,7 +81,8 @@ int stts_pack(stts_model* m, int dtype, void* packed, long long bytes, void* str
  * F0N: T = text-aligned frames; STYLE: T = mel frames). */
 long long stts_workspace_bytes(const stts_model* m, int dtype, int B, int T);
 
-/* Decoder: asr [B][dim_in][T], F0_curve [B][2T], N [B][2T], s [B][style_dim] -> out [B][1][600T].
+/* Decoder: asr [B][dim_in][T], F0_curve [B][2T], N [B][2T], s [B][style_dim] -> out [B][1][600T]
+ * (VOCOS: out [B][1][2T * gen_istft_hop_size]; it has no source, noise / seed are ignored).
  * noise: [B][600T][9] = the SineGen randn_like draw (hifigan.py:213), or NULL to draw it on the
  * device from a counter RNG keyed by (seed, utt_offset + b, sample, harmonic). */
 int stts_decoder_fwd(stts_model* m, int dtype, const float* asr, const float* f0_curve, const float* n,

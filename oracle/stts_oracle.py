@@ -587,3 +587,70 @@ def mpd(y, y_hat, sd, periods=MPD_PERIODS):
         fmap_rs.append(fr)
         fmap_gs.append(fg)
     return y_d_rs, y_d_gs, fmap_rs, fmap_gs
+
+
+# ----------------------------------------------------------------------- Vocos decoder (§8(f) rank 4)
+def vocos_alias(sd):
+    """Modules/vocos.py builds its weight-norm layers with torch.nn.utils.parametrizations.weight_norm
+    (:10): state-dict keys `<p>.parametrizations.weight.original0` (g) / `original1` (v) instead of
+    `<p>.weight_g` / `<p>.weight_v`.  Same fold (dim 0), so alias them for wn()."""
+    out = dict(sd)
+    for k in list(sd):
+        for suf, new in ((".parametrizations.weight.original0", ".weight_g"),
+                         (".parametrizations.weight.original1", ".weight_v")):
+            if k.endswith(suf):
+                out[k[: -len(suf)] + new] = sd[k]
+    return out
+
+
+def convnext_block(x, s, sd, p):
+    """ConvNeXtBlock.forward (Modules/vocos.py:56-69): depthwise k7 conv, AdaIN1d, Linear ->
+    GELU (erf) -> Linear, layer scale gamma, residual."""
+    C = x.shape[1]
+    r = x
+    x = F.conv1d(x, _t(sd, p + ".dwconv.weight"), _t(sd, p + ".dwconv.bias"), 1, 3, 1, C)
+    x = adain1d(x, s, sd, p + ".norm")
+    x = x.transpose(1, 2)
+    x = F.linear(x, _t(sd, p + ".pwconv1.weight"), _t(sd, p + ".pwconv1.bias"))
+    x = F.gelu(x)
+    x = F.linear(x, _t(sd, p + ".pwconv2.weight"), _t(sd, p + ".pwconv2.bias"))
+    x = _t(sd, p + ".gamma") * x
+    return r + x.transpose(1, 2)
+
+
+def vocos_istft(spec, window, n_fft, hop):
+    """ISTFT.forward, padding 'same' (Modules/vocos.py:190-232): irfft, window, overlap-add by
+    fold, divide by the folded squared-window envelope, trim (win - hop) / 2 each side."""
+    pad = (n_fft - hop) // 2
+    B, N, T = spec.shape
+    ifft = torch.fft.irfft(spec, n_fft, dim=1, norm="backward") * window[None, :, None]
+    out_size = (T - 1) * hop + n_fft
+    y = F.fold(ifft, output_size=(1, out_size), kernel_size=(1, n_fft), stride=(1, hop))[:, 0, 0, pad:-pad]
+    wsq = window.square().expand(1, T, -1).transpose(1, 2)
+    env = F.fold(wsq, output_size=(1, out_size), kernel_size=(1, n_fft), stride=(1, hop)).squeeze()[pad:-pad]
+    return y / env
+
+
+def generator_vocos(x, s, sd, cfg, taps=None):
+    """Generator.forward (Modules/vocos.py:157-162) + ISTFTHead.forward (:271-296)."""
+    for i in range(cfg["num_layers"]):
+        x = convnext_block(x, s, sd, f"generator.convnext.{i}")
+    x = F.layer_norm(x.transpose(1, 2), (x.shape[1],), _t(sd, "generator.final_layer_norm.weight"),
+                     _t(sd, "generator.final_layer_norm.bias"), 1e-6)
+    if taps is not None:
+        taps["ln"] = x
+    x = F.linear(x, _t(sd, "generator.stft.out.weight"), _t(sd, "generator.stft.out.bias")).transpose(1, 2)
+    mag, p = x.chunk(2, dim=1)
+    mag = torch.clip(torch.exp(mag), max=1e2)
+    S = mag * (torch.cos(p) + 1j * torch.sin(p))
+    return vocos_istft(S, _t(sd, "generator.stft.istft.window"), cfg["n_fft"], cfg["hop"])
+
+
+def decoder_vocos(asr, F0_curve, N, s, sd, cfg, taps=None):
+    """Decoder.forward (Modules/vocos.py:392-421, eval): the hifigan front-end, the ConvNeXt
+    generator, unsqueeze(1)."""
+    sd = vocos_alias(sd)
+    x = decoder_frontend(asr, F0_curve, N, s, sd)
+    if taps is not None:
+        taps["frontend"] = x
+    return generator_vocos(x, s, sd, cfg, taps).unsqueeze(1)

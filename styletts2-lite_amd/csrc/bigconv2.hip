@@ -769,7 +769,7 @@ bool st_front_eligible(const ConvParams& p, int dtype) {
   if (p.Cout != 1024 && p.Cout != 512) return false;
   const int mode = p.pro.mode;
   if (mode != 0 && mode != PRO_LRELU && mode != (PRO_AFFINE | PRO_LRELU) && mode != PRO_AFFINE) return false;
-  return p.N == p.Cout && p.KS == 3 && p.dil == 1 && p.stride == 1 && p.up == 1 && p.pad == 1 && !p.epi_lrelu &&
+  return p.N == p.Cout && p.KS == 3 && p.dil == 1 && p.stride == 1 && p.up == 1 && p.pad == 1 && !p.epi_lrelu && !p.epi_gelu &&
          (p.kw == 0 || p.kw == p.KS) && p.row_off == 0 && p.Cin >= 128 && p.Cin <= FE_CINP &&
          p.Lin == p.Lq && p.Lout == p.Lq && !p.accb && !p.epi_tanh && !p.y_f32 && !p.reflect_front &&
          p.zc_period == 0 && p.y_row_off == 0 && p.x_ld % 8 == 0 && p.y_ld % 8 == 0 &&

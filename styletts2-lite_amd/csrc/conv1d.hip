@@ -624,6 +624,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
 #pragma unroll
                   for (int j = 0; j < 16; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * p.epi_slope;
                 }
+                if (p.epi_gelu) {  // nn.GELU() (erf form), Modules/vocos.py:48
+#pragma unroll
+                  for (int j = 0; j < 16; ++j) v[j] = 0.5f * v[j] * (1.0f + erff(v[j] * 0.7071067811865476f));
+                }
                 store16(yT + (size_t)orow * p.y_ld + co0, v);
                 if constexpr (!C::BF) {
 #pragma unroll
@@ -647,6 +651,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
                   if (resb) x = (x + to_f32(resb[(size_t)(orow >> p.res_shift) * p.res_ld + co])) * p.out_scale;
                   if (p.epi_tanh) x = tanhf(x);
                   if (p.epi_lrelu) x = x > 0.f ? x : x * p.epi_slope;
+                  if (p.epi_gelu) x = 0.5f * x * (1.0f + erff(x * 0.7071067811865476f));
                   if (p.y_f32) {
                     yF[(size_t)orow * p.y_ld + co] = x;
                   } else {

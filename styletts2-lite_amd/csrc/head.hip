@@ -108,7 +108,7 @@ int launch_head(const ConvParams& p, hipStream_t s) {
 bool st_head_eligible(const ConvParams& p) {
   return p.N == 1 && p.Cout == 1 && p.KS == 7 && p.pad == 3 && p.dil == 1 && p.stride == 1 && p.up == 1 &&
          (p.Cin == 32 || p.Cin == 64) && p.pro.mode == PRO_SNAKE && p.y_f32 && p.y_ld == 1 && p.y_bs == p.Lq &&
-         p.epi_tanh && !p.epi_lrelu && !p.res && !p.accb && !p.stats && p.Lin == p.Lq && p.Lout == p.Lq && p.y_row_off == 0 &&
+         p.epi_tanh && !p.epi_lrelu && !p.epi_gelu && !p.res && !p.accb && !p.stats && p.Lin == p.Lq && p.Lout == p.Lq && p.y_row_off == 0 &&
          p.x_ld >= p.Cin && p.x_ld % 8 == 0;
 }
 

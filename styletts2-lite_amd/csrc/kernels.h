@@ -37,6 +37,7 @@ struct ConvParams {
   int epi_tanh, reflect_front;
   int epi_lrelu;      // LeakyReLU(epi_slope) on the stored output (discriminator feature maps)
   float epi_slope;
+  int epi_gelu;       // exact (erf) GELU on the stored output (Vocos ConvNeXt pwconv1 -> act)
   double* stats;  // [B][stats_ld][2] accumulated statistics of the stored output
   int stats_ld;
   // small-batch atomic spreading: workgroup g accumulates into slot g % stats_slots, the slot
@@ -213,3 +214,21 @@ long long st_mel_frames(long long L);
 long long st_mel_workspace_bytes();
 int st_wave_preprocess(const float* wave, int B, long long L, long long ld, float* mel, void* ws, long long ws_bytes,
                        hipStream_t stream);
+
+// ---------------------------------------------------------------- Vocos decoder (vocos.hip)
+// depthwise Conv1d(C, C, 7, pad 3) + bias over frames [B][L][x_ld] -> frames [B][L][y_ld], with the
+// per-(utterance, channel) statistics of the output (slot = block % slots) for the next AdaIN
+int st_dwconv7(const void* x, long long x_bs, int x_ld, int B, int L, int C, const float* w, const float* bias, void* y,
+               long long y_bs, int y_ld, double* stats, int stats_ld, int slots, long long slot_bs, int dtype,
+               hipStream_t s);
+// LayerNorm(C, eps, affine g / b) over each of `rows` frame rows
+int st_frame_ln(const void* x, int x_ld, long long rows, int C, float eps, const float* g, const float* b, void* y,
+                int y_ld, int dtype, hipStream_t s);
+// ISTFTHead + ISTFT('same'): head frames h [B][F][ld] (dtype; channels [0, nb) log-magnitude, [nb, 2nb)
+// phase, nb = N/2 + 1) -> windowed irfft frames fr fp32 [B][F][N] -> out fp32 [B][(F-1) hop + N - 2 pad]
+int st_istft_head(const void* h, int B, int F, int ld, int N, int hop, const float* window, float* fr, float* out,
+                  int dtype, hipStream_t s);
+int st_istft_factor(int N, int* N1, int* N2);
+// out[r][i] = r < rows_src ? src[r][i] * (scale ? scale[r] : 1) : 0 for r < rows_dst (pack-time prep)
+int st_scale_rows(const float* src, const float* scale, int rows_src, long long inner, int rows_dst, float* out,
+                  hipStream_t s);

@@ -52,6 +52,11 @@ struct WConv {
   int v = -1, g = -1, bias = -1;
   int Cin = 0, Cout = 0, K = 0, transposed = 0, u = 1;
   int reframe = 0;  // > 0: a Conv1d(1, Cout, 2S, stride S) packed as a 2-tap conv over S-sample frames
+  // pack-time prep (Vocos): rows scaled by parameter `rs` (layer scale), or only `src_rows` < Cout rows
+  // in the parameter (the rest packed as zero columns); the bias then lives folded / padded in aux
+  int rs = -1, src_rows = 0;
+  size_t bias_aux = 0;
+  bool aux_bias = false;
   size_t off[2] = {0, 0};
   int taps() const { return transposed ? (K + u - 1) / u : K; }
   int N() const { return transposed ? u * Cout : Cout; }
@@ -105,7 +110,17 @@ struct stts_model {
   std::vector<int> alphas;
   WConv conv_post;
   int stft_fr = -1, stft_fi = -1, stft_br = -1, stft_bi = -1;
-  // -------- F0N
+  // -------- Vocos generator (Modules/vocos.py:108-162, ISTFTHead :248-296)
+  bool pwn = false;  // weight norm as torch.nn.utils.parametrizations (original0 = g, original1 = v)
+  int vc_inter = 0, vc_layers = 0;
+  struct CNX {
+    int dw_w = -1, dw_b = -1, gamma = -1;
+    WAdaIN norm;
+    WConv pw1, pw2;
+  };
+  std::vector<CNX> cnx;
+  int ln_w = -1, ln_b = -1, vwin = -1;
+  WConv vhead;  // -------- F0N
   int d_hid = 512;
   AdainBlk f0blk[3], nblk[3];
   WConv f0_proj, n_proj;
@@ -152,8 +167,8 @@ void add_wconv(Model& m, WConv& c, const std::string& p, int cin, int cout, int 
   c.u = u;
   if (bias) c.bias = m.P.add(p + ".bias", cout);
   if (wn) {
-    c.g = m.P.add(p + ".weight_g", transposed ? cin : cout);
-    c.v = m.P.add(p + ".weight_v", (long long)cin * cout / groups * k);
+    c.g = m.P.add(p + (m.pwn ? ".parametrizations.weight.original0" : ".weight_g"), transposed ? cin : cout);
+    c.v = m.P.add(p + (m.pwn ? ".parametrizations.weight.original1" : ".weight_v"), (long long)cin * cout / groups * k);
   } else {
     c.v = m.P.add(p + ".weight", (long long)cin * cout / groups * k);
   }
@@ -191,8 +206,8 @@ void add_adainblk(Model& m, AdainBlk& b, const std::string& p, int cin, int cout
   if (b.learned) add_wconv(m, b.sc, p + ".conv1x1", cin, cout, 1, true, false);
   if (up) {
     b.pool_b = m.P.add(p + ".pool.bias", cin);
-    b.pool_g = m.P.add(p + ".pool.weight_g", cin);
-    b.pool_v = m.P.add(p + ".pool.weight_v", (long long)cin * 3);
+    b.pool_g = m.P.add(p + (m.pwn ? ".pool.parametrizations.weight.original0" : ".pool.weight_g"), cin);
+    b.pool_v = m.P.add(p + (m.pwn ? ".pool.parametrizations.weight.original1" : ".pool.weight_v"), (long long)cin * 3);
     m.pools.push_back(&b);
   }
 }
@@ -201,9 +216,62 @@ void add_small_wn(Model& m, Small& s, const std::string& p, long long rows, long
   s.rows = rows;
   s.inner = inner;
   s.bias = m.P.add(p + ".bias", rows);
-  s.g = m.P.add(p + ".weight_g", rows);
-  s.v = m.P.add(p + ".weight_v", rows * inner);
+  s.g = m.P.add(p + (m.pwn ? ".parametrizations.weight.original0" : ".weight_g"), rows);
+  s.v = m.P.add(p + (m.pwn ? ".parametrizations.weight.original1" : ".weight_v"), rows * inner);
   m.smalls.push_back(&s);
+}
+
+// decoder front-end (hifigan.py:427-440 == istftnet.py:673-686 == vocos.py:370-390)
+void add_frontend(Model& m) {
+  add_adainblk(m, m.encode, "encode", m.dim_in + 2, 1024, false);
+  for (int k = 0; k < 4; ++k)
+    add_adainblk(m, m.decode[k], "decode." + std::to_string(k), 1024 + 2 + 64, k == 3 ? 512 : 1024, k == 3);
+  add_small_wn(m, m.F0_conv, "F0_conv", 1, 3);
+  add_small_wn(m, m.N_conv, "N_conv", 1, 3);
+  add_wconv(m, m.asr_res, "asr_res.0", m.dim_in, 64, 1, true, true);
+}
+
+// Vocos Decoder (Modules/vocos.py:364-390): cfg = dim_in, style_dim, intermediate_dim, num_layers,
+// n_fft, hop.  The generator's dim is dim_in and its input is decode.3's 512 channels, so the
+// reference itself only runs with dim_in = 512.
+int build_vocos(Model& m, const int* cfg, int n) {
+  if (n != 6) return ST_EINVAL;
+  m.dim_in = cfg[0];
+  m.style_dim = cfg[1];
+  m.vc_inter = cfg[2];
+  m.vc_layers = cfg[3];
+  m.n_fft = cfg[4];
+  m.hop = cfg[5];
+  if (m.dim_in != 512 || m.style_dim <= 0 || m.vc_inter <= 0 || m.vc_inter % 32 || m.vc_layers <= 0 ||
+      m.vc_layers > 64 || m.hop <= 0 || m.hop > m.n_fft || (m.n_fft - m.hop) / 2 <= 0)
+    return ST_EINVAL;
+  int n1 = 0, n2 = 0;
+  if (st_istft_factor(m.n_fft, &n1, &n2) != ST_OK) return ST_EINVAL;
+  m.pwn = true;
+  add_frontend(m);
+  const int d = m.dim_in;
+  m.cnx.resize(m.vc_layers);  // sized once: add_wconv / add_adain keep pointers into it
+  for (int i = 0; i < m.vc_layers; ++i) {
+    auto& b = m.cnx[i];
+    const std::string p = "generator.convnext." + std::to_string(i);
+    b.dw_w = m.P.add(p + ".dwconv.weight", (long long)d * 7);
+    b.dw_b = m.P.add(p + ".dwconv.bias", d);
+    add_adain(m, b.norm, p + ".norm", d);
+    add_wconv(m, b.pw1, p + ".pwconv1", d, m.vc_inter, 1, false, true);  // nn.Linear == [Cout][Cin][1]
+    add_wconv(m, b.pw2, p + ".pwconv2", m.vc_inter, d, 1, false, true);
+    b.gamma = m.P.add(p + ".gamma", d);
+    b.pw2.rs = b.gamma;  // gamma * (W x + b) folded into the packed weights and bias
+    b.pw2.aux_bias = true;
+  }
+  m.ln_w = m.P.add("generator.final_layer_norm.weight", d);
+  m.ln_b = m.P.add("generator.final_layer_norm.bias", d);
+  const int nout = 2 * (m.n_fft / 2 + 1);
+  add_wconv(m, m.vhead, "generator.stft.out", d, nout, 1, false, true);
+  m.vhead.src_rows = nout;  // columns padded to the MFMA 16-column multiple (the wide epilogue)
+  m.vhead.Cout = (nout + 15) & ~15;
+  m.vhead.aux_bias = true;
+  m.vwin = m.P.add("generator.stft.istft.window", m.n_fft);
+  return ST_OK;
 }
 
 int build_decoder(Model& m, const int* cfg, int n) {
@@ -235,13 +303,7 @@ int build_decoder(Model& m, const int* cfg, int n) {
   if (i != n) return ST_EINVAL;
   if (m.init_ch != 512) return ST_EINVAL;  // decode.3 emits 512 channels (hifigan.py:432)
   const bool ist = m.kind == STTS_KIND_ISTFTNET;
-  // front-end (hifigan.py:427-440)
-  add_adainblk(m, m.encode, "encode", m.dim_in + 2, 1024, false);
-  for (int k = 0; k < 4; ++k)
-    add_adainblk(m, m.decode[k], "decode." + std::to_string(k), 1024 + 2 + 64, k == 3 ? 512 : 1024, k == 3);
-  add_small_wn(m, m.F0_conv, "F0_conv", 1, 3);
-  add_small_wn(m, m.N_conv, "N_conv", 1, 3);
-  add_wconv(m, m.asr_res, "asr_res.0", m.dim_in, 64, 1, true, true);
+  add_frontend(m);
   // generator (hifigan.py:272-319 / istftnet.py:494-540)
   m.l_lin_w = m.P.add("generator.m_source.l_linear.weight", 9);
   m.l_lin_b = m.P.add("generator.m_source.l_linear.bias", 1);
@@ -406,10 +468,15 @@ void finalize_layout(Model& m) {
     p->pool_off = a;
     a += rup((size_t)p->cin * 3 * 4, ALIGN);
   }
+  for (auto* c : m.convs)
+    if (c->aux_bias) {
+      c->bias_aux = a;
+      a += rup((size_t)c->Cout * 4, ALIGN);
+    }
   m.aux_bytes = a;
   size_t sc = 0;
   for (auto* c : m.convs)
-    if (c->g >= 0 || c->reframe) sc = std::max(sc, (size_t)c->Cin * c->Cout * c->K * 4);
+    if (c->g >= 0 || c->reframe || c->rs >= 0 || c->src_rows) sc = std::max(sc, (size_t)c->Cin * c->Cout * c->K * 4);
   m.scratch_bytes = rup(sc, ALIGN);
   for (int dt = 0; dt < 2; ++dt) {
     m.aux_off[dt] = m.conv_bytes[dt];
@@ -516,7 +583,7 @@ ConvParams conv_base(Ctx& c, const WConv& w, const Buf& x, int c0) {
   p.N = w.N();
   p.w = c.wpk(w);
   p.nchunks = (w.Cin + 31) / 32;
-  p.bias = c.P(w.bias);
+  p.bias = w.aux_bias ? c.aux_f(w.bias_aux) : c.P(w.bias);
   p.Cout = w.Cout;
   p.pro = pro_none();
   p.up = 1;
@@ -785,21 +852,82 @@ struct DecIO {
   float* out;
 };
 
+// front-end buffers (hifigan.py:458-472); X0 = decode.3's output [B][2T][512]
+struct FrontBufs {
+  Buf ENC, CAT[2], H1, SC, POOL, X0;
+};
+
+FrontBufs alloc_front(Ctx& c, int T) {
+  Model& m = *c.m;
+  const int ld_enc = rup8(m.dim_in + 2), ld_cat = rup8(1024 + 2 + 64);
+  FrontBufs f;
+  f.ENC = c.frames(T, ld_enc);
+  f.CAT[0] = c.frames(T, ld_cat);
+  f.CAT[1] = c.frames(T, ld_cat);
+  f.H1 = c.frames(2 * T, 1024);
+  f.SC = c.frames(T, 1024);
+  f.POOL = c.frames(2 * T, ld_cat);
+  f.X0 = c.frames(2 * T, 512);
+  c.H = reinterpret_cast<float*>(c.alloc((size_t)c.B * m.Htot * 4));
+  return f;
+}
+
+// the style projections of every AdaIN layer, then the front-end (hifigan.py:458-472 ==
+// istftnet.py:704-718 == vocos.py:404-419, eval branch) into f.X0
+int run_front(Ctx& c, const DecIO& io, FrontBufs& f) {
+  Model& m = *c.m;
+  const int B = c.B, T = io.T, n = 2 * T;
+  const int ld_enc = rup8(m.dim_in + 2), ld_cat = rup8(1024 + 2 + 64);
+  Buf &ENC = f.ENC, *CAT = f.CAT, &H1 = f.H1, &SC = f.SC, &POOL = f.POOL, &X0 = f.X0;
+  RUN(st_linear(io.s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
+  double* S_enc = c.stat(ld_enc);
+  RUN(st_ncl_to_frames(io.asr, B, m.dim_in, T, ENC.p, ld_enc, 0, ENC.bs, S_enc, ld_enc, c.dtype, c.s));
+  double* S_cat[4];
+  for (int k = 0; k < 4; ++k) S_cat[k] = c.stat(ld_cat);
+  for (int w = 0; w < 2; ++w) {
+    const Small& sm = w == 0 ? m.F0_conv : m.N_conv;
+    const float* src = w == 0 ? io.f0 : io.n;
+    SmallConvDst d[3];
+    d[0] = {ENC.p, ENC.bs, ld_enc, m.dim_in + w, S_enc, ld_enc};
+    d[1] = {CAT[0].p, CAT[0].bs, ld_cat, 1024 + 64 + w, S_cat[0], ld_cat};
+    d[2] = {CAT[1].p, CAT[1].bs, ld_cat, 1024 + 64 + w, nullptr, 0};
+    RUN(st_conv_cin1(src, n, n, B, c.aux_f(sm.off), c.P(sm.bias), 1, 3, 2, 1, T, d, 3, c.dtype, c.s));
+  }
+  for (int w = 0; w < 2; ++w) {  // asr_res (hifigan.py:438-440, 464) into both concat buffers
+    ConvParams p = conv_base(c, m.asr_res, ENC, 0);
+    p.Lq = T;
+    conv_out(p, c, CAT[w], 1024, T);
+    if (w == 0) {
+      p.stats = S_cat[0] + 1024 * 2;
+      p.stats_ld = ld_cat;
+    }
+    RUN(conv_run(c, p));
+    // these statistics are copied slot 0 only into the other concat buffers' stats below: fold
+    if (w == 0 && c.slots > 1)
+      RUN(st_stats_fold(p.stats, c.B, p.stats_ld, p.Cout, c.slots, (long long)c.B * p.stats_ld * 2, c.s));
+  }
+  if (!c.dry) {  // the constant concat channels share their statistics across the 4 blocks
+    for (int k = 1; k < 4; ++k)
+      ST_CHECK_HIP(hipMemcpy2DAsync(S_cat[k] + 1024 * 2, (size_t)ld_cat * 16, S_cat[0] + 1024 * 2,
+                                    (size_t)ld_cat * 16, 66 * 16, B, hipMemcpyDeviceToDevice, c.s));
+  }
+  ST_CHECK(adain_blk(c, m.encode, ENC, 0, S_enc, ld_enc, CAT[0], 0, S_cat[0], ld_cat, H1, SC, POOL));
+  ST_CHECK(adain_blk(c, m.decode[0], CAT[0], 0, S_cat[0], ld_cat, CAT[1], 0, S_cat[1], ld_cat, H1, SC, POOL));
+  ST_CHECK(adain_blk(c, m.decode[1], CAT[1], 0, S_cat[1], ld_cat, CAT[0], 0, S_cat[2], ld_cat, H1, SC, POOL));
+  ST_CHECK(adain_blk(c, m.decode[2], CAT[0], 0, S_cat[2], ld_cat, CAT[1], 0, S_cat[3], ld_cat, H1, SC, POOL));
+  ST_CHECK(adain_blk(c, m.decode[3], CAT[1], 0, S_cat[3], ld_cat, X0, 0, nullptr, 0, H1, SC, POOL));
+  return 0;
+}
+
 int decoder_forward(Ctx& c, const DecIO& io) {
   Model& m = *c.m;
   const int B = c.B, T = io.T;
   const bool ist = m.kind == STTS_KIND_ISTFTNET;
   const int nup = (int)m.rates.size(), nrb = (int)m.rbk.size();
-  const int ld_enc = rup8(m.dim_in + 2), ld_cat = rup8(1024 + 2 + 64);
   const size_t esz = c.esz;
   // ---------------- allocations (identical in dry and real runs)
-  Buf ENC = c.frames(T, ld_enc);
-  Buf CAT[2] = {c.frames(T, ld_cat), c.frames(T, ld_cat)};
-  Buf H1 = c.frames(2 * T, 1024);
-  Buf SC = c.frames(T, 1024);
-  Buf POOL = c.frames(2 * T, ld_cat);
-  Buf X0 = c.frames(2 * T, 512);
-  c.H = reinterpret_cast<float*>(c.alloc((size_t)B * m.Htot * 4));
+  FrontBufs fb = alloc_front(c, T);
+  Buf& X0 = fb.X0;
   const int n = 2 * T;
   int scale = 1;
   for (int r : m.rates) scale *= r;
@@ -840,45 +968,8 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     POST = c.frames(F, ld_h);
   }
   c.stats_begin = c.stats_off = c.off;  // stats region follows; its size is known after the dry run
-  // ---------------- style projections for every AdaIN layer
-  RUN(st_linear(io.s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
-  // ---------------- front-end (hifigan.py:458-472)
-  double* S_enc = c.stat(ld_enc);
-  RUN(st_ncl_to_frames(io.asr, B, m.dim_in, T, ENC.p, ld_enc, 0, ENC.bs, S_enc, ld_enc, c.dtype, c.s));
-  double* S_cat[4];
-  for (int k = 0; k < 4; ++k) S_cat[k] = c.stat(ld_cat);
-  for (int w = 0; w < 2; ++w) {
-    const Small& sm = w == 0 ? m.F0_conv : m.N_conv;
-    const float* src = w == 0 ? io.f0 : io.n;
-    SmallConvDst d[3];
-    d[0] = {ENC.p, ENC.bs, ld_enc, m.dim_in + w, S_enc, ld_enc};
-    d[1] = {CAT[0].p, CAT[0].bs, ld_cat, 1024 + 64 + w, S_cat[0], ld_cat};
-    d[2] = {CAT[1].p, CAT[1].bs, ld_cat, 1024 + 64 + w, nullptr, 0};
-    RUN(st_conv_cin1(src, n, n, B, c.aux_f(sm.off), c.P(sm.bias), 1, 3, 2, 1, T, d, 3, c.dtype, c.s));
-  }
-  for (int w = 0; w < 2; ++w) {  // asr_res (hifigan.py:438-440, 464) into both concat buffers
-    ConvParams p = conv_base(c, m.asr_res, ENC, 0);
-    p.Lq = T;
-    conv_out(p, c, CAT[w], 1024, T);
-    if (w == 0) {
-      p.stats = S_cat[0] + 1024 * 2;
-      p.stats_ld = ld_cat;
-    }
-    RUN(conv_run(c, p));
-    // these statistics are copied slot 0 only into the other concat buffers' stats below: fold
-    if (w == 0 && c.slots > 1)
-      RUN(st_stats_fold(p.stats, c.B, p.stats_ld, p.Cout, c.slots, (long long)c.B * p.stats_ld * 2, c.s));
-  }
-  if (!c.dry) {  // the constant concat channels share their statistics across the 4 blocks
-    for (int k = 1; k < 4; ++k)
-      ST_CHECK_HIP(hipMemcpy2DAsync(S_cat[k] + 1024 * 2, (size_t)ld_cat * 16, S_cat[0] + 1024 * 2,
-                                    (size_t)ld_cat * 16, 66 * 16, B, hipMemcpyDeviceToDevice, c.s));
-  }
-  ST_CHECK(adain_blk(c, m.encode, ENC, 0, S_enc, ld_enc, CAT[0], 0, S_cat[0], ld_cat, H1, SC, POOL));
-  ST_CHECK(adain_blk(c, m.decode[0], CAT[0], 0, S_cat[0], ld_cat, CAT[1], 0, S_cat[1], ld_cat, H1, SC, POOL));
-  ST_CHECK(adain_blk(c, m.decode[1], CAT[1], 0, S_cat[1], ld_cat, CAT[0], 0, S_cat[2], ld_cat, H1, SC, POOL));
-  ST_CHECK(adain_blk(c, m.decode[2], CAT[0], 0, S_cat[2], ld_cat, CAT[1], 0, S_cat[3], ld_cat, H1, SC, POOL));
-  ST_CHECK(adain_blk(c, m.decode[3], CAT[1], 0, S_cat[3], ld_cat, X0, 0, nullptr, 0, H1, SC, POOL));
+  // ---------------- style projections + front-end (hifigan.py:458-472)
+  ST_CHECK(run_front(c, io, fb));
   // ---------------- harmonic source (hifigan.py:323-326 / istftnet.py:544-550)
   RUN(st_sine_phase(io.f0, B, n, scale, PH, c.s));
   RUN(st_sine_source(io.f0, PH, B, n, scale, c.P(m.l_lin_w), c.P(m.l_lin_b), io.noise, io.seed, io.utt, HAR, c.s));
@@ -1003,6 +1094,57 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     RUN(st_istft(POST.p, B, F, ld_h, m.n_fft, m.hop, c.P(m.stft_br), c.P(m.stft_bi), io.out, L, c.dtype, c.s));
   }
   (void)esz;
+  return 0;
+}
+
+// --------------------------------------------------------------------- Vocos forward
+// Decoder.forward (Modules/vocos.py:392-421, eval): the front-end, then Generator.forward (:157-162):
+// per ConvNeXtBlock (:56-69) dwconv (+ InstanceNorm statistics) -> [AdaIN prologue] pwconv1 [GELU
+// epilogue] -> pwconv2 with gamma folded [+ residual epilogue]; final LayerNorm; ISTFTHead.out, and
+// the exp / clip / cos / sin + irfft + window + overlap-add of ISTFTHead / ISTFT (:271-296, :190-232).
+int vocos_forward(Ctx& c, const DecIO& io) {
+  Model& m = *c.m;
+  const int B = c.B, T = io.T, L = 2 * T, d = m.dim_in;
+  FrontBufs fb = alloc_front(c, T);
+  Buf XB = c.frames(L, d), D = c.frames(L, d), HI = c.frames(L, m.vc_inter);
+  Buf POST = c.frames(L, m.vhead.Cout);
+  float* FR = reinterpret_cast<float*>(c.alloc((size_t)B * L * m.n_fft * 4));
+  c.stats_begin = c.stats_off = c.off;
+  ST_CHECK(run_front(c, io, fb));
+  Buf* x = &fb.X0;
+  Buf* y = &XB;
+  for (const auto& b : m.cnx) {
+    double* S_d = c.stat(d);
+    RUN(st_dwconv7(x->p, x->bs, x->ld, B, L, d, c.P(b.dw_w), c.P(b.dw_b), D.p, D.bs, D.ld, S_d, d, c.slots,
+                   (long long)B * d * 2, c.dtype, c.s));
+    {
+      ConvParams p = conv_base(c, b.pw1, D, 0);
+      p.pro = pro_adain(c, b.norm, S_d, d, L, 0, -1, 0.f);
+      p.Lq = L;
+      conv_out(p, c, HI, 0, L);
+      p.epi_gelu = 1;
+      RUN(conv_run(c, p));
+    }
+    {
+      ConvParams p = conv_base(c, b.pw2, HI, 0);
+      p.Lq = L;
+      conv_out(p, c, *y, 0, L);
+      p.res = x->p;
+      p.res_bs = x->bs;
+      p.res_ld = x->ld;
+      RUN(conv_run(c, p));
+    }
+    std::swap(x, y);
+  }
+  // final LayerNorm (eps 1e-6) into D, the head Linear into POST
+  RUN(st_frame_ln(x->p, x->ld, (long long)B * L, d, 1e-6f, c.P(m.ln_w), c.P(m.ln_b), D.p, D.ld, c.dtype, c.s));
+  {
+    ConvParams p = conv_base(c, m.vhead, D, 0);
+    p.Lq = L;
+    conv_out(p, c, POST, 0, L);
+    RUN(conv_run(c, p));
+  }
+  RUN(st_istft_head(POST.p, B, L, POST.ld, m.n_fft, m.hop, c.P(m.vwin), FR, io.out, c.dtype, c.s));
   return 0;
 }
 
@@ -1215,7 +1357,14 @@ int pack_model(Model& m, int dt, char* base, hipStream_t s) {
     } else if (c->reframe) {
       ST_CHECK(st_reframe_w(v, c->Cout, c->reframe, scratch, s));
       src = scratch;
+    } else if (c->rs >= 0 || c->src_rows) {
+      const int rows = c->src_rows ? c->src_rows : c->Cout;
+      ST_CHECK(st_scale_rows(v, c->rs >= 0 ? m.P[c->rs] : nullptr, rows, (long long)c->Cin * c->K, c->Cout, scratch, s));
+      src = scratch;
     }
+    if (c->aux_bias)
+      ST_CHECK(st_scale_rows(m.P[c->bias], c->rs >= 0 ? m.P[c->rs] : nullptr, c->src_rows ? c->src_rows : c->Cout, 1,
+                             c->Cout, reinterpret_cast<float*>(aux + c->bias_aux), s));
     ST_CHECK(st_pack_conv(src, c->Cin, c->Cout, c->K, c->transposed, c->u, base + c->off[dt], dt, s));
   }
   // AdaIN projections: Wt[k][hoff + n] = fc.weight[n][k]; bias concat
@@ -1284,6 +1433,8 @@ int stts_model_create(int kind, const int* cfg, int ncfg, stts_model** out) {
     r = build_style(*m, cfg, ncfg);
   else if (kind == STTS_KIND_MPD)
     r = build_mpd(*m, cfg, ncfg);
+  else if (kind == STTS_KIND_VOCOS)
+    r = build_vocos(*m, cfg, ncfg);
   if (r != 0) {
     delete m;
     return r;
@@ -1345,6 +1496,10 @@ long long stts_workspace_bytes(const stts_model* mc, int dtype, int B, int T) {
   } else if (m->kind == STTS_KIND_MPD) {
     r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return mpd_forward(c, nullptr, T, nullptr); },
                  &need);
+  } else if (m->kind == STTS_KIND_VOCOS) {
+    DecIO io{};
+    io.T = T;
+    r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return vocos_forward(c, io); }, &need);
   } else {
     r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return style_forward(c, nullptr, T, nullptr); },
                  &need);
@@ -1355,10 +1510,13 @@ long long stts_workspace_bytes(const stts_model* mc, int dtype, int B, int T) {
 int stts_decoder_fwd(stts_model* m, int dtype, const float* asr, const float* f0, const float* n, const float* s,
                      const float* noise, unsigned long long seed, long long utt_offset, int B, int T, float* out,
                      void* ws, long long ws_bytes, void* stream) {
-  if (!m || (m->kind != STTS_KIND_HIFIGAN && m->kind != STTS_KIND_ISTFTNET)) return ST_EINVAL;
+  if (!m || (m->kind != STTS_KIND_HIFIGAN && m->kind != STTS_KIND_ISTFTNET && m->kind != STTS_KIND_VOCOS))
+    return ST_EINVAL;
   if (B <= 0 || T <= 0 || !asr || !f0 || !n || !s || !out) return ST_EINVAL;
   ST_CHECK(check_params(*m));
   DecIO io{asr, f0, n, s, noise, seed, utt_offset, T, out};
+  if (m->kind == STTS_KIND_VOCOS)
+    return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return vocos_forward(c, io); }, nullptr);
   return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return decoder_forward(c, io); }, nullptr);
 }
 

@@ -14,7 +14,7 @@ import os
 import numpy as np
 import torch
 
-KIND_HIFIGAN, KIND_ISTFTNET, KIND_F0N, KIND_STYLE, KIND_MPD = 0, 1, 2, 3, 4
+KIND_HIFIGAN, KIND_ISTFTNET, KIND_F0N, KIND_STYLE, KIND_MPD, KIND_VOCOS = 0, 1, 2, 3, 4, 5
 DTYPES = {"fp32": 0, "bf16": 1}
 
 _LIB = None
@@ -243,19 +243,24 @@ class _Engine:
 
 
 class DecoderEngine(_Engine):
-    """HIP forward of Modules/hifigan.py / istftnet.py Decoder (reference :446 / :692)."""
+    """HIP forward of Modules/hifigan.py / istftnet.py / vocos.py Decoder (reference :446 / :692 / :392)."""
 
     def __init__(self, module, dtype="fp32"):
         super().__init__(module, dtype)
         g = module.generator
-        kind = KIND_ISTFTNET if module.decoder_type == "istftnet" else KIND_HIFIGAN
-        cfg = [module.dim_in, module.style_dim, g.upsample_initial_channel, len(g.upsample_rates),
-               *g.upsample_rates, *g.upsample_kernel_sizes, len(g.resblock_kernel_sizes),
-               *g.resblock_kernel_sizes, *[d for ds in g.resblock_dilation_sizes for d in ds]]
-        if kind == KIND_ISTFTNET:
-            cfg += [g.gen_istft_n_fft, g.gen_istft_hop_size]
+        if module.decoder_type == "vocos":
+            kind = KIND_VOCOS
+            cfg = [module.dim_in, module.style_dim, g.intermediate_dim, g.num_layers, g.n_fft, g.hop]
+            self.scale = g.hop  # output samples per F0 frame (2T frames x hop)
+        else:
+            kind = KIND_ISTFTNET if module.decoder_type == "istftnet" else KIND_HIFIGAN
+            cfg = [module.dim_in, module.style_dim, g.upsample_initial_channel, len(g.upsample_rates),
+                   *g.upsample_rates, *g.upsample_kernel_sizes, len(g.resblock_kernel_sizes),
+                   *g.resblock_kernel_sizes, *[d for ds in g.resblock_dilation_sizes for d in ds]]
+            if kind == KIND_ISTFTNET:
+                cfg += [g.gen_istft_n_fft, g.gen_istft_hop_size]
+            self.scale = g.upsample_scale
         self.kind = kind
-        self.scale = g.upsample_scale
         self.dim_in, self.style_dim = module.dim_in, module.style_dim
         self.model = NativeModel(kind, cfg, module)
         self.model.pack(dtype)
@@ -266,7 +271,7 @@ class DecoderEngine(_Engine):
         randn_like draws (hifigan.py:213) do."""
         dev = self.model.device
         if seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if noise is None else 0
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if noise is None and self.kind != KIND_VOCOS else 0
         in_dev = asr.device if isinstance(asr, torch.Tensor) else torch.device("cpu")
         asr, F0_curve, N, s = (_dev_f32(t, dev) for t in (asr, F0_curve, N, s))
         B, C, T = asr.shape
@@ -277,6 +282,8 @@ class DecoderEngine(_Engine):
         if T < 2:  # the reference's InstanceNorm1d raises on a single frame (torch F.instance_norm)
             raise ValueError(f"decoder inputs: need at least 2 asr frames, got {T}")
         Lw = 2 * T * self.scale
+        if noise is not None and self.kind == KIND_VOCOS:
+            raise ValueError("the Vocos decoder has no harmonic source: noise must be None")
         if noise is not None:
             noise = _dev_f32(noise, dev)
             if tuple(noise.shape) != (B, Lw, 9):

@@ -235,12 +235,18 @@ def build_models(config):
     """inference.py:88-122 with the drop-in classes: the parsed config.yaml (a dict) ->
     {'decoder', 'predictor', 'text_encoder', 'style_encoder'} modules (parameters on the CPU,
     move them with .to('cuda'))."""
-    from . import hifigan, istftnet
+    from . import hifigan, istftnet, vocos
     from .models import ProsodyPredictor, StyleEncoder, TextEncoder
     args = config["model_params"]
     _, n_token = symbol_table(config)
     dec = args["decoder"]
-    common = dict(dim_in=args["hidden_dim"], style_dim=args["style_dim"], dim_out=args["n_mels"],
+    if dec["type"] not in ("istftnet", "hifigan", "vocos"):  # inference.py:93
+        raise AssertionError("Decoder type unknown")
+    if dec["type"] == "vocos":  # inference.py:112-118 (no resblock / upsample keys in its config block)
+        decoder = vocos.Decoder(dim_in=args["hidden_dim"], style_dim=args["style_dim"], dim_out=args["n_mels"],
+                                intermediate_dim=dec["intermediate_dim"], num_layers=dec["num_layers"],
+                                gen_istft_n_fft=dec["gen_istft_n_fft"], gen_istft_hop_size=dec["gen_istft_hop_size"])
+    common = {} if dec["type"] == "vocos" else dict(dim_in=args["hidden_dim"], style_dim=args["style_dim"], dim_out=args["n_mels"],
                   resblock_kernel_sizes=dec["resblock_kernel_sizes"], upsample_rates=dec["upsample_rates"],
                   upsample_initial_channel=dec["upsample_initial_channel"],
                   resblock_dilation_sizes=dec["resblock_dilation_sizes"],
@@ -250,8 +256,6 @@ def build_models(config):
                                    gen_istft_hop_size=dec["gen_istft_hop_size"])
     elif dec["type"] == "hifigan":
         decoder = hifigan.Decoder(**common)
-    else:  # the reference also accepts 'vocos' (Modules/vocos.py): out of scope here
-        raise NotImplementedError(f"decoder type {dec['type']!r}: only hifigan / istftnet run on the HIP path")
     return {
         "decoder": decoder,
         "predictor": ProsodyPredictor(style_dim=args["style_dim"], d_hid=args["hidden_dim"], nlayers=args["n_layer"],

@@ -79,9 +79,9 @@ def _g_target(key: str) -> float:
 def synth_param(key: str, shape) -> np.ndarray:
     """Formula value for one state-dict entry of the decoders / predictor / style encoder."""
     shape = tuple(int(s) for s in shape)
-    if key.endswith("weight_v"):
+    if key.endswith("weight_v") or key.endswith("parametrizations.weight.original1"):
         return uniform(key, shape, -1.0, 1.0)
-    if key.endswith("weight_g"):
+    if key.endswith("weight_g") or key.endswith("parametrizations.weight.original0"):
         return (_g_target(key) * uniform(key, shape, 0.8, 1.2)).astype(np.float32)
     if ".alpha" in key or key.startswith("generator.alphas") or ".alphas." in key:
         return uniform(key, shape, 0.6, 1.4)
@@ -108,6 +108,10 @@ def synth_param(key: str, shape) -> np.ndarray:
         return uniform(key, shape, -1.0, 1.0) * np.float32(gain * np.sqrt(3.0 / fan_in))
     if key.endswith("bias"):
         return uniform(key, shape, -0.05, 0.05)
+    if ".convnext." in key and key.endswith(".gamma"):  # Vocos ConvNeXt layer scale (init 1/num_layers)
+        return uniform(key, shape, 0.1, 0.2)
+    if key.endswith("layer_norm.weight"):  # Vocos final LayerNorm
+        return uniform(key, shape, 0.8, 1.2)
     if key.endswith(".gamma"):
         return uniform(key, shape, 0.8, 1.2)
     if key.endswith(".beta"):
@@ -117,7 +121,7 @@ def synth_param(key: str, shape) -> np.ndarray:
 
 def is_fixed_buffer(key: str) -> bool:
     """Deterministic buffers the modules compute themselves (CustomSTFT bases)."""
-    return ".stft." in key
+    return ".stft." in key and not key.endswith((".out.weight", ".out.bias"))  # Vocos ISTFTHead.out is a Linear
 
 
 def synth_state_dict(named_shapes, prefix: str = "") -> dict:
