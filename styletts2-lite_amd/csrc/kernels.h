@@ -123,6 +123,8 @@ struct ResFusedParams {
   int stats_ld;
   int stats_slots;  // as ConvParams::stats_slots
   long long stats_slot_bs;
+  int dbg;  // phase-skipping timing bits (STTS_OPT_DEBUG, set by st_resfused): 1 prologue math, 2 MFMAs,
+            // 4 residual loads + stores, 8 window loads (results are wrong when set)
 };
 extern int g_opt_resfused;
 bool st_resfused_eligible(int C, int K, int dil, int dtype);

@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(512, 1) k_resfused(const ResFusedParams p) {
       const int u = tid + k * NT;
       const int e = (gr0 + u / G8) * p.x_ld + 8 * g8;
       const bool in = (k + 1) * NT <= UNITS || u < UNITS;
-      pre[k] = bload16(rx, in && e >= 0 ? (unsigned)e * 2u : OOB);
+      pre[k] = bload16(rx, in && e >= 0 && !(p.dbg & 8) ? (unsigned)e * 2u : OOB);
     }
   };
   auto transform = [&](int t) __attribute__((always_inline)) {
@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(512, 1) k_resfused(const ResFusedParams p) {
         const int r = u / G8;
         float v[8];
         bf8f(pre[k], v);
-        pro8<C>(coef1, 8 * g8, v);
+        if (!(p.dbg & 1)) pro8<C>(coef1, 8 * g8, v);
         uint4 o = f8bf(v);
         if ((unsigned)(gr0 + r) >= (unsigned)L) o = make_uint4(0, 0, 0, 0);  // conv1 zero padding
         *reinterpret_cast<uint4*>(X1s + r * XP + 8 * g8) = o;
@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(512, 1) k_resfused(const ResFusedParams p) {
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
       const int q = mt * BM + (wm + WMW * mi) * 32 + l32;
-      const unsigned er = (unsigned)(q * p.x_ld + co0) * 2u;
+      const unsigned er = (p.dbg & 4) ? OOB : (unsigned)(q * p.x_ld + co0) * 2u;
       rres[mi][0] = bload16(rr, er);
       rres[mi][1] = bload16(rr, er + 16u);
       if constexpr (ACC) {
@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(512, 1) k_resfused(const ResFusedParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][r] = 0.f;
 #pragma unroll 1
-    for (int tap = 0; tap < K; ++tap) {
+    for (int tap = 0; tap < ((p.dbg & 2) ? 0 : K); ++tap) {
       const bf16_t* xt = x1w + tap * DIL * XP;
       const bf16_t* wt = w1w + tap * C * WP;
 #pragma unroll
@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(512, 1) k_resfused(const ResFusedParams p) {
         ld8_lds(bias1 + co0 + 8 * h, bb);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = acc[mi][8 * h + j] + bb[j];
-        pro8<C>(coef2, co0 + 8 * h, v);
+        if (!(p.dbg & 1)) pro8<C>(coef2, co0 + 8 * h, v);
         uint4 o = f8bf(v);
         if (!in) o = make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4*>(X2s + r * XP + co0 + 8 * h) = o;
@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(512, 1) k_resfused(const ResFusedParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][r] = 0.f;
 #pragma unroll 1
-    for (int tap = 0; tap < K; ++tap) {
+    for (int tap = 0; tap < ((p.dbg & 2) ? 0 : K); ++tap) {
       const bf16_t* xt = x2w + tap * XP;
       const bf16_t* wt = w2w + tap * C * WP;
 #pragma unroll
@@ -337,8 +337,10 @@ __global__ void __launch_bounds__(512, 1) k_resfused(const ResFusedParams p) {
           }
         }
         bf16_t* dst = yb + (size_t)q * p.y_ld + co0;
-        *reinterpret_cast<uint4*>(dst) = f8bf(&v[0]);
-        *reinterpret_cast<uint4*>(dst + 8) = f8bf(&v[8]);
+        if (!(p.dbg & 4)) {
+          *reinterpret_cast<uint4*>(dst) = f8bf(&v[0]);
+          *reinterpret_cast<uint4*>(dst + 8) = f8bf(&v[8]);
+        }
         if constexpr (!ACC) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -401,8 +403,10 @@ bool st_resfused_eligible(int C, int K, int dil, int dtype) {
   return false;
 }
 
-int st_resfused(const ResFusedParams& p, hipStream_t stream) {
-  if (p.B <= 0 || p.L <= 0) return ST_OK;
+int st_resfused(const ResFusedParams& pin, hipStream_t stream) {
+  if (pin.B <= 0 || pin.L <= 0) return ST_OK;
+  ResFusedParams p = pin;
+  p.dbg = g_opt_debug;
   if (!st_resfused_eligible(p.C, p.K, p.dil, ST_BF16)) return ST_EINVAL;
   if (p.x_ld % 8 || p.y_ld % 8 || (p.accb && p.acc_ld % 8) || (p.accb && p.stats)) return ST_EINVAL;
   if (!p.pro1.stats || !p.pro1.gamma || !p.pro1.alpha || !p.pro2.stats || !p.pro2.gamma || !p.pro2.alpha)
