@@ -37,6 +37,9 @@ typedef struct stts_model stts_model;
 #define STTS_KIND_STYLE 3    /* models.py StyleEncoder       */
 #define STTS_KIND_MPD 4      /* Modules/discriminators.py MultiPeriodDiscriminator (training step, config 5);
                                 cfg = {n, period_1 .. period_n}, the reference's {5, 2, 3, 5, 7, 11} */
+#define STTS_KIND_MSD 6      /* Modules/discriminators.py MultiResSpecDiscriminator (training step, config 5);
+                                cfg = {n, (fft_size, hop_size, win_length) x n}, the reference's
+                                {3, 1024, 120, 600, 2048, 240, 1200, 512, 50, 240} */
 #define STTS_KIND_VOCOS 5    /* Modules/vocos.py Decoder (front-end + ConvNeXt generator + ISTFTHead) */
 
 /* compute / activation dtypes */
@@ -113,6 +116,32 @@ int stts_mpd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, floa
  * discriminator_loss(y_d_rs, y_d_gs)[0] over the MultiPeriodDiscriminator outputs.  loss (device,
  * 3 doubles) = {feature, generator, discriminator}; scratch (device) >= 4 * 6 * n_periods doubles. */
 int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
+                    void* stream);
+
+/* Multi-resolution mel loss, <- losses.py:55-94 MultiResolutionSTFTLoss(fft_sizes, hop_sizes, win_lengths)
+ * .forward(x, y) as train.py:282 calls it (stft_loss(y_rec, wav)): per resolution r the torchaudio
+ * MelSpectrogram(sample_rate, n_ffts[r], wins[r], hops[r], window_fn=hann) (n_mels = 128 at its default,
+ * f_max sr/2, power 2, center/reflect, HTK) of x and y, (log(1e-5 + mel) + 4) / 4, and
+ * SpectralConvergengeLoss = ||y_mag - x_mag||_1 / ||y_mag||_1 over the whole batch; loss (device, 1 double)
+ * = the mean over the n_res resolutions.  x, y: [B][ld] fp32 (L samples each, L > n_fft / 2); n_ffts are
+ * powers of two <= 2048 (the reference's 1024, 2048, 512); the int arrays are HOST pointers.
+ * Workspace >= stts_mrstft_workspace_bytes(B, L, hops, n_res, n_mels). */
+long long stts_mrstft_workspace_bytes(int B, long long L, const int* hops, int n_res, int n_mels);
+int stts_mrstft_loss(const float* x, const float* y, int B, long long L, long long ld, const int* n_ffts,
+                     const int* hops, const int* wins, int n_res, int sample_rate, int n_mels, double* loss,
+                     void* workspace, long long ws_bytes, void* stream);
+
+/* MultiResSpecDiscriminator forward, <- Modules/discriminators.py:47-63 SpecDiscriminator.forward for every
+ * resolution (MultiResSpecDiscriminator.forward :80-94 calls it on y and y_hat: pass both as one batch).
+ * wave [B][T] fp32.  out (fp32, >= stts_msd_out_elems) receives, resolution by resolution, the 5
+ * LeakyReLU(0.1)-activated feature maps as [B][H][W_j][32] (the reference's [B, 32, H, W_j] permuted;
+ * H = 1 + T / hop frames, W = n_fft/2 + 1 bins halved by each stride-(1, 2) conv) and the out map
+ * [B][H][W_5] (flattened = the score).  Workspace: stts_workspace_bytes(m, dtype, B, T). */
+long long stts_msd_out_elems(const stts_model* m, int B, int T);
+int stts_msd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, float* out, long long out_elems,
+                 void* workspace, long long ws_bytes, void* stream);
+/* The GAN losses of stts_mpd_losses over stts_msd_fwd's output (losses.py:97-128 with the MSD outputs). */
+int stts_msd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
                     void* stream);
 
 /* Style front-end, <- inference.py:43-49 Preprocess.wave_preprocess(wave) (the torchaudio

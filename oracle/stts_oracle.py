@@ -654,3 +654,75 @@ def decoder_vocos(asr, F0_curve, N, s, sd, cfg, taps=None):
     if taps is not None:
         taps["frontend"] = x
     return generator_vocos(x, s, sd, cfg, taps).unsqueeze(1)
+
+
+# ----------------------------------------------------------------------- multi-resolution mel loss (§8(f) rank 3)
+MRSTFT = dict(fft_sizes=(1024, 2048, 512), hop_sizes=(120, 240, 50), win_lengths=(600, 1200, 240))
+
+
+def mel_spectrogram_sr(wave, sample_rate, n_fft, win_length, hop_length, n_mels=128):
+    """torchaudio.transforms.MelSpectrogram(sample_rate, n_fft, win_length, hop_length, window_fn=hann)
+    at its other defaults (losses.py:43): f_min 0, f_max sr // 2, power 2, center/reflect, HTK, no norm."""
+    spec = torch.stft(wave, n_fft, hop_length, win_length, torch.hann_window(win_length), center=True,
+                      pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
+    power = spec.abs().pow(2.0)
+    fb = melscale_fbanks(n_fft // 2 + 1, 0.0, float(sample_rate // 2), n_mels, sample_rate)
+    return torch.matmul(power.transpose(-1, -2), fb).transpose(-1, -2)
+
+
+def stft_loss(x, y, fft_size, shift_size, win_length, sample_rate=24000):
+    """STFTLoss.forward (losses.py:46-63) + SpectralConvergengeLoss (:18-21)."""
+    x_mag = (torch.log(1e-5 + mel_spectrogram_sr(x, sample_rate, fft_size, win_length, shift_size)) + 4) / 4
+    y_mag = (torch.log(1e-5 + mel_spectrogram_sr(y, sample_rate, fft_size, win_length, shift_size)) + 4) / 4
+    return torch.norm(y_mag - x_mag, p=1) / torch.norm(y_mag, p=1)
+
+
+def mrstft_loss(x, y, fft_sizes=MRSTFT["fft_sizes"], hop_sizes=MRSTFT["hop_sizes"],
+                win_lengths=MRSTFT["win_lengths"]):
+    """MultiResolutionSTFTLoss.forward (losses.py:79-94): the mean spectral-convergence loss."""
+    sc = 0.0
+    for fs, ss, wl in zip(fft_sizes, hop_sizes, win_lengths):
+        sc = sc + stft_loss(x, y, fs, ss, wl)
+    return sc / len(fft_sizes)
+
+
+# ----------------------------------------------------------------------- MultiResSpecDiscriminator (§8(f) rank 3)
+MSD_RES = ((1024, 120, 600), (2048, 240, 1200), (512, 50, 240))
+
+
+def spec_discriminator(y, sd, prefix, fft_size, hop, win):
+    """SpecDiscriminator.forward (Modules/discriminators.py:47-63): |torch.stft| image [B, 1, frames,
+    bins] -> 4 Conv2d (3, 9) [strides (1,1), (1,2) x 3] + LReLU(0.1) -> Conv2d (3, 3) + LReLU -> out."""
+    y = y.squeeze(1)
+    y = torch.stft(y, fft_size, hop, win, torch.hann_window(win), return_complex=True)  # stft() :11-27
+    y = torch.abs(y).transpose(2, 1).unsqueeze(1)
+    fmap = []
+    for j in range(5):
+        p = f"{prefix}.discriminators.{j}"
+        stride, pad = ((1, 2) if 1 <= j <= 3 else (1, 1)), ((1, 4) if j < 4 else (1, 1))
+        y = F.leaky_relu(F.conv2d(y, wn(sd, p), _t(sd, p + ".bias"), stride, pad), 0.1)
+        fmap.append(y)
+    y = F.conv2d(y, wn(sd, f"{prefix}.out"), _t(sd, f"{prefix}.out.bias"), 1, 1)
+    fmap.append(y)
+    return torch.flatten(y, 1, -1), fmap
+
+
+def msd(y, y_hat, sd, res=MSD_RES):
+    """MultiResSpecDiscriminator.forward (discriminators.py:80-94)."""
+    y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
+    for i, (f, h, w) in enumerate(res):
+        r, fr = spec_discriminator(y, sd, f"discriminators.{i}", f, h, w)
+        g, fg = spec_discriminator(y_hat, sd, f"discriminators.{i}", f, h, w)
+        y_d_rs.append(r)
+        y_d_gs.append(g)
+        fmap_rs.append(fr)
+        fmap_gs.append(fg)
+    return y_d_rs, y_d_gs, fmap_rs, fmap_gs
+
+
+def gan_losses(y_d_rs, y_d_gs, fmap_rs, fmap_gs):
+    """losses.py:97-128: feature_loss, generator_loss(.)[0], discriminator_loss(.)[0]."""
+    fm = sum(torch.mean(torch.abs(rl - gl)) for dr, dg in zip(fmap_rs, fmap_gs) for rl, gl in zip(dr, dg)) * 2
+    gen = sum(torch.mean((1 - dg) ** 2) for dg in y_d_gs)
+    disc = sum(torch.mean((1 - dr) ** 2) + torch.mean(dg ** 2) for dr, dg in zip(y_d_rs, y_d_gs))
+    return fm, gen, disc

@@ -234,3 +234,21 @@ int st_istft_factor(int N, int* N1, int* N2);
 // out[r][i] = r < rows_src ? src[r][i] * (scale ? scale[r] : 1) : 0 for r < rows_dst (pack-time prep)
 int st_scale_rows(const float* src, const float* scale, int rows_src, long long inner, int rows_dst, float* out,
                   hipStream_t s);
+
+// ---------------------------------------------------------------- training-step spectra (spec.hip)
+long long st_stft_frames(long long L, int hop);
+// torchaudio MelSpectrogram(sr, n_fft, win, hop, hann, n_mels) -> (log(1e-5 + mel) + 4) / 4:
+// x fp32 [S][ld] (L samples) -> out fp32 [S][n_mels][1 + L / hop]   (losses.py:44-54)
+int st_logmel(const float* x, int S, long long L, long long ld, int n_fft, int win, int hop, int n_mels, float sr,
+              float* out, hipStream_t s);
+// |torch.stft(x, n_fft, hop, win, hann(win))| (Modules/discriminators.py:11-27) time-expanded:
+// x3 [S][F][n_fft/2 + 1][8], channel dh = frame h + dh - 1 (channels 3..7 and out-of-range rows are not
+// written: zero the buffer first)
+int st_stft_mag_x3(const float* x, int S, long long L, long long ld, int n_fft, int win, int hop, void* x3, int dtype,
+                   hipStream_t s);
+// x3[s][h][w][c * 3 + dh] = y[s][h + dh - 1][w][c], 0 outside [0, H)
+int st_time_expand(const void* y, int S, int H, int W, int C, void* x3, int dtype, hipStream_t s);
+// sums[0] += sum |y - x|, sums[1] += sum |y|   (SpectralConvergengeLoss numerator / denominator)
+int st_sc_sums(const float* xm, const float* ym, long long n, double* sums, hipStream_t s);
+// loss[0] = mean_r sums[2r] / sums[2r + 1]
+int st_sc_final(const double* sums, int nres, double* loss, hipStream_t s);

@@ -139,6 +139,12 @@ struct stts_model {
     WConv convs[5], post;
   };
   std::vector<DiscP> mpd;
+  // -------- MultiResSpecDiscriminator (Modules/discriminators.py:29-94)
+  struct DiscS {
+    int n_fft = 0, hop = 0, win = 0;
+    WConv convs[5], out;
+  };
+  std::vector<DiscS> msd;
   // -------- AdaIN projections (all AdaIN layers share one GEMV: H = s @ Wt + b)
   std::vector<WAdaIN*> adains;
   int Htot = 0;
@@ -418,6 +424,55 @@ int build_mpd(Model& m, const int* cfg, int n) {
     add_wconv(m, d.post, p + ".conv_post", 1024, 1, 3, true, true);
   }
   return ST_OK;
+}
+
+// MultiResSpecDiscriminator: SpecDiscriminator(n_fft, hop, win) per resolution (discriminators.py:73-78),
+// each 4 weight-norm Conv2d (3, 9) [strides (1,1), (1,2) x 3] + Conv2d (3, 3) + out Conv2d(32, 1, 3)
+// (:38-45), cfg = {n, (n_fft, hop, win) x n}
+constexpr int kMsdCh = 32;
+int build_msd(Model& m, const int* cfg, int n) {
+  if (n < 4 || (n - 1) != 3 * cfg[0]) return ST_EINVAL;
+  m.msd.resize(cfg[0]);
+  for (int i = 0; i < cfg[0]; ++i) {
+    auto& d = m.msd[i];
+    d.n_fft = cfg[1 + 3 * i];
+    d.hop = cfg[2 + 3 * i];
+    d.win = cfg[3 + 3 * i];
+    if (d.n_fft < 16 || d.n_fft > 2048 || (d.n_fft & (d.n_fft - 1)) || d.hop <= 0 || d.win <= 0 || d.win > d.n_fft)
+      return ST_EINVAL;
+    const std::string p = "discriminators." + std::to_string(i);
+    // a (3, kw) Conv2d runs as a 1-D conv along the bins over 3 C (time-expanded) channels: the
+    // reference's [Cout][C][3][kw] weight is exactly the [Cout][3C][kw] Conv1d weight
+    for (int j = 0; j < 5; ++j)
+      add_wconv(m, d.convs[j], p + ".discriminators." + std::to_string(j), 3 * (j == 0 ? 1 : kMsdCh), kMsdCh,
+                j < 4 ? 9 : 3, true, true);
+    add_wconv(m, d.out, p + ".out", 3 * kMsdCh, 1, 3, true, true);
+  }
+  return ST_OK;
+}
+
+// geometry of SpecDiscriminator over Tn samples: H frames, widths W[0..5] (W[0] = bins; layers 1-3
+// halve with kernel 9, pad 4, stride 2)
+struct MsdGeom {
+  int H, W[6];
+};
+MsdGeom msd_geom(const Model::DiscS& d, int Tn) {
+  MsdGeom g;
+  g.H = 1 + Tn / d.hop;
+  g.W[0] = g.W[1] = d.n_fft / 2 + 1;
+  for (int j = 2; j <= 4; ++j) g.W[j] = (g.W[j - 1] - 1) / 2 + 1;
+  g.W[5] = g.W[4];
+  return g;
+}
+
+long long msd_out_elems(const Model& m, int S, int Tn) {
+  long long n = 0;
+  for (const auto& d : m.msd) {
+    const MsdGeom g = msd_geom(d, Tn);
+    for (int j = 1; j <= 5; ++j) n += (long long)S * g.H * g.W[j] * kMsdCh;
+    n += (long long)S * g.H * g.W[5];
+  }
+  return n;
 }
 
 // per-layer frame counts of DiscriminatorP(p) over Tn samples: L[0] = ceil(Tn / p), then the 4
@@ -1197,6 +1252,57 @@ int mpd_forward(Ctx& c, const float* wave, int Tn, float* out) {
   return 0;
 }
 
+// --------------------------------------------------------------------- MSD forward
+// SpecDiscriminator.forward (discriminators.py:47-63) for every resolution over S signals: |STFT| ->
+// 4 Conv2d (3, 9) + LeakyReLU(0.1) [the last three with stride (1, 2)] -> Conv2d (3, 3) + LeakyReLU
+// -> out Conv2d (3, 3).  Each (3, kw) Conv2d over the (frames, bins) image runs as a 1-D conv along the
+// bins of every frame (batch = S * H sequences) over 3 C time-expanded channels (k_time_expand /
+// k_stft_mag write x3[h][w][c * 3 + dh] = y[h + dh - 1][w][c]).  `out` (fp32) receives, per resolution,
+// the 5 activated feature maps [S][H][W_j][32] and the out map [S][H][W_5] (the reference's
+// [S, C, H, W] tensors permuted).
+int msd_forward(Ctx& c, const float* wave, int Tn, float* out) {
+  Model& m = *c.m;
+  const int S = c.B;
+  size_t off = 0;
+  for (const auto& d : m.msd) {
+    const MsdGeom g = msd_geom(d, Tn);
+    c.B = S * g.H;  // the conv batch: every (signal, frame) row of bins
+    Buf x3 = c.frames(g.W[0], 8);
+    if (!c.dry) ST_CHECK_HIP(hipMemsetAsync(x3.p, 0, (size_t)c.B * x3.bs * c.esz, c.s));
+    RUN(st_stft_mag_x3(wave, S, Tn, Tn, d.n_fft, d.win, d.hop, x3.p, c.dtype, c.s));
+    for (int j = 0; j < 5; ++j) {
+      Buf y = c.frames(g.W[j + 1], kMsdCh);
+      ConvParams q = conv_base(c, d.convs[j], x3, 0);
+      q.stride = (j >= 1 && j <= 3) ? 2 : 1;
+      q.pad = j < 4 ? 4 : 1;
+      q.Lq = g.W[j + 1];
+      conv_out(q, c, y, 0, g.W[j + 1]);
+      q.epi_lrelu = 1;
+      q.epi_slope = 0.1f;  // LRELU_SLOPE (discriminators.py:9)
+      RUN(conv_run(c, q));
+      RUN(st_frames_to_f32(y.p, c.B, g.W[j + 1], kMsdCh, kMsdCh, out ? out + off : nullptr, c.dtype, c.s));
+      off += (size_t)c.B * g.W[j + 1] * kMsdCh;
+      x3 = c.frames(g.W[j + 1], 3 * kMsdCh);
+      RUN(st_time_expand(y.p, S, g.H, g.W[j + 1], kMsdCh, x3.p, c.dtype, c.s));
+    }
+    {  // out: Conv2d(32, 1, 3, 1, 1) straight into the fp32 output
+      ConvParams q = conv_base(c, d.out, x3, 0);
+      q.pad = 1;
+      q.Lq = g.W[5];
+      q.y = out ? out + off : nullptr;
+      q.y_bs = g.W[5];
+      q.y_ld = 1;
+      q.y_f32 = 1;
+      q.Lout = g.W[5];
+      RUN(conv_run(c, q));
+      off += (size_t)c.B * g.W[5];
+    }
+    c.B = S;
+  }
+  c.stats_begin = c.stats_off = c.off;  // no statistics: the workspace is the buffers above
+  return 0;
+}
+
 // --------------------------------------------------------------------- F0/N forward
 int f0n_forward(Ctx& c, const float* x, const float* s, int T, float* F0, float* Nout) {
   Model& m = *c.m;
@@ -1435,6 +1541,8 @@ int stts_model_create(int kind, const int* cfg, int ncfg, stts_model** out) {
     r = build_mpd(*m, cfg, ncfg);
   else if (kind == STTS_KIND_VOCOS)
     r = build_vocos(*m, cfg, ncfg);
+  else if (kind == STTS_KIND_MSD)
+    r = build_msd(*m, cfg, ncfg);
   if (r != 0) {
     delete m;
     return r;
@@ -1495,6 +1603,9 @@ long long stts_workspace_bytes(const stts_model* mc, int dtype, int B, int T) {
                  [&](Ctx& c) { return f0n_forward(c, nullptr, nullptr, T, nullptr, nullptr); }, &need);
   } else if (m->kind == STTS_KIND_MPD) {
     r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return mpd_forward(c, nullptr, T, nullptr); },
+                 &need);
+  } else if (m->kind == STTS_KIND_MSD) {
+    r = with_ctx(m, dtype, B, nullptr, 0, nullptr, [&](Ctx& c) { return msd_forward(c, nullptr, T, nullptr); },
                  &need);
   } else if (m->kind == STTS_KIND_VOCOS) {
     DecIO io{};
@@ -1568,6 +1679,76 @@ int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double*
       sg.off[sg.n] = off;
       sg.half[sg.n] = half;
       sg.score[sg.n] = j == 5;
+      ++sg.n;
+      off += 2 * half;
+    }
+  }
+  return st_mpd_losses(out, sg, scratch, loss, (hipStream_t)stream);
+}
+
+// MultiResolutionSTFTLoss (losses.py:55-94): workspace = the per-resolution sums + one resolution's
+// log-mels of both signals (resolutions run one after the other on the stream)
+long long stts_mrstft_workspace_bytes(int B, long long L, const int* hops, int n_res, int n_mels) {
+  if (B <= 0 || L <= 0 || !hops || n_res <= 0 || n_res > 16 || n_mels <= 0) return ST_EINVAL;
+  long long f = 0;
+  for (int r = 0; r < n_res; ++r) {
+    if (hops[r] <= 0) return ST_EINVAL;
+    f = std::max(f, st_stft_frames(L, hops[r]));
+  }
+  return 256 + 2LL * B * n_mels * f * 4;
+}
+
+int stts_mrstft_loss(const float* x, const float* y, int B, long long L, long long ld, const int* n_ffts,
+                     const int* hops, const int* wins, int n_res, int sample_rate, int n_mels, double* loss, void* ws,
+                     long long ws_bytes, void* stream) {
+  if (!x || !y || !loss || !n_ffts || !hops || !wins || B <= 0 || sample_rate <= 0) return ST_EINVAL;
+  const long long need = stts_mrstft_workspace_bytes(B, L, hops, n_res, n_mels);
+  if (need < 0) return (int)need;
+  if (!ws || ws_bytes < need) return ST_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  double* sums = reinterpret_cast<double*>(ws);
+  ST_CHECK_HIP(hipMemsetAsync(sums, 0, 2 * n_res * sizeof(double), s));
+  float* mx = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + 256);
+  for (int r = 0; r < n_res; ++r) {
+    const long long F = st_stft_frames(L, hops[r]);
+    float* my = mx + (size_t)B * n_mels * F;
+    ST_CHECK(st_logmel(x, B, L, ld, n_ffts[r], wins[r], hops[r], n_mels, (float)sample_rate, mx, s));
+    ST_CHECK(st_logmel(y, B, L, ld, n_ffts[r], wins[r], hops[r], n_mels, (float)sample_rate, my, s));
+    ST_CHECK(st_sc_sums(mx, my, (long long)B * n_mels * F, sums + 2 * r, s));
+  }
+  return st_sc_final(sums, n_res, loss, s);
+}
+
+long long stts_msd_out_elems(const stts_model* m, int B, int T) {
+  if (!m || m->kind != STTS_KIND_MSD || B <= 0 || T <= 0) return ST_EINVAL;
+  return msd_out_elems(*m, B, T);
+}
+
+int stts_msd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, float* out, long long out_elems,
+                 void* ws, long long ws_bytes, void* stream) {
+  if (!m || m->kind != STTS_KIND_MSD) return ST_EINVAL;
+  if (B <= 0 || !wave || !out) return ST_EINVAL;
+  for (const auto& d : m->msd)  // torch.stft's reflect pad needs n_fft / 2 < T
+    if (T <= d.n_fft / 2) return ST_EINVAL;
+  if (out_elems < msd_out_elems(*m, B, T)) return ST_EINVAL;
+  ST_CHECK(check_params(*m));
+  return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return msd_forward(c, wave, T, out); }, nullptr);
+}
+
+int stts_msd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
+                    void* stream) {
+  if (!m || m->kind != STTS_KIND_MSD || B <= 0 || T <= 0 || !out || !scratch || !loss) return ST_EINVAL;
+  MpdLossSegs sg;
+  memset(&sg, 0, sizeof(sg));
+  long long off = 0;
+  for (const auto& d : m->msd) {
+    const MsdGeom g = msd_geom(d, T);
+    for (int j = 1; j <= 6; ++j) {
+      if (sg.n >= kMpdMaxSegs) return ST_EINVAL;
+      const long long half = (long long)B * g.H * g.W[j < 6 ? j : 5] * (j < 6 ? kMsdCh : 1);
+      sg.off[sg.n] = off;
+      sg.half[sg.n] = half;
+      sg.score[sg.n] = j == 6;
       ++sg.n;
       off += 2 * half;
     }

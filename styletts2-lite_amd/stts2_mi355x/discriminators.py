@@ -1,14 +1,15 @@
-"""Drop-in MultiPeriodDiscriminator (Modules/discriminators.py:96-156) for the training step
-(SURVEY §8(f) rank 3, config 5): same constructor, sub-module names and state-dict keys
-(`discriminators.{i}.convs.{j}.weight_g / weight_v / bias`, `discriminators.{i}.conv_post.*`), the
-forward on the HIP engine (stts_mpd_fwd).  Forward only: the reference trains these with autograd;
-backward kernels are not built.
+"""Drop-in MultiPeriodDiscriminator (Modules/discriminators.py:96-156) and MultiResSpecDiscriminator
+(:29-94) for the training step: same constructors, sub-module names and
+state-dict keys (`discriminators.{i}.convs.{j}.weight_g / weight_v / bias`, `discriminators.{i}.conv_post.*`;
+`discriminators.{i}.discriminators.{j}.*`, `discriminators.{i}.out.*`), the forwards on the HIP engines
+(stts_mpd_fwd, stts_msd_fwd).  Forward only: the reference trains these with autograd; backward
+kernels are not built.
 """
 from __future__ import annotations
 
 import torch
 from torch import nn
-from torch.nn import Conv2d
+from torch.nn import Conv2d, Conv2d as _C2
 from torch.nn.utils import weight_norm
 
 LRELU_SLOPE = 0.1
@@ -75,4 +76,65 @@ def mpd_gan_losses(mpd: MultiPeriodDiscriminator, y, y_hat, dtype="fp32"):
     (losses.py:97-128) over its outputs -> (feature, generator, discriminator) float64 scalars."""
     mpd(y, y_hat, dtype=dtype)
     loss = mpd.engine(dtype).gan_losses()
+    return loss[0], loss[1], loss[2]
+
+
+class SpecDiscriminator(nn.Module):
+    """Parameter holder with the reference's layout (discriminators.py:29-45)."""
+
+    def __init__(self, fft_size=1024, shift_size=120, win_length=600, window="hann_window", use_spectral_norm=False):
+        super().__init__()
+        if use_spectral_norm or window != "hann_window":
+            raise NotImplementedError("the HIP engine implements the reference's weight-norm / hann configuration")
+        self.fft_size, self.shift_size, self.win_length = int(fft_size), int(shift_size), int(win_length)
+        self.discriminators = nn.ModuleList([
+            weight_norm(_C2(1, 32, kernel_size=(3, 9), padding=(1, 4))),
+            weight_norm(_C2(32, 32, kernel_size=(3, 9), stride=(1, 2), padding=(1, 4))),
+            weight_norm(_C2(32, 32, kernel_size=(3, 9), stride=(1, 2), padding=(1, 4))),
+            weight_norm(_C2(32, 32, kernel_size=(3, 9), stride=(1, 2), padding=(1, 4))),
+            weight_norm(_C2(32, 32, kernel_size=(3, 3), stride=(1, 1), padding=(1, 1))),
+        ])
+        self.out = weight_norm(_C2(32, 1, 3, 1, 1))
+
+
+class MultiResSpecDiscriminator(nn.Module):
+    """MultiResSpecDiscriminator (discriminators.py:65-94) on the HIP engine.
+
+    forward(y, y_hat) -> (y_d_rs, y_d_gs, fmap_rs, fmap_gs) as the reference: per resolution a score
+    [B, H*W] and six feature maps [B, C, H, W] (permuted views of the engine's [B][H][W][C] output).
+    y and y_hat go through the engine as one batch.  (The reference's forward only runs on CUDA
+    tensors: `self.window.to(y.get_device())`, :55; this one takes any device.)"""
+
+    def __init__(self, fft_sizes=(1024, 2048, 512), hop_sizes=(120, 240, 50), win_lengths=(600, 1200, 240),
+                 window="hann_window"):
+        super().__init__()
+        self.discriminators = nn.ModuleList([SpecDiscriminator(f, h, w, window)
+                                             for f, h, w in zip(fft_sizes, hop_sizes, win_lengths)])
+        self._engine = None
+
+    def engine(self, dtype="fp32"):
+        from .engine import MSDEngine
+        if self._engine is None or self._engine.dtype != dtype or self._engine.stale(self):
+            self._engine = MSDEngine(self, dtype=dtype)
+        return self._engine
+
+    def invalidate(self):
+        self._engine = None
+
+    def forward(self, y, y_hat, dtype="fp32"):
+        B = y.shape[0]
+        res = self.engine(dtype).forward(torch.cat([y, y_hat], 0))
+        y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
+        for score, fmaps in res:
+            y_d_rs.append(score[:B])
+            y_d_gs.append(score[B:])
+            fmap_rs.append([f[:B] for f in fmaps])
+            fmap_gs.append([f[B:] for f in fmaps])
+        return y_d_rs, y_d_gs, fmap_rs, fmap_gs
+
+
+def msd_gan_losses(msd: MultiResSpecDiscriminator, y, y_hat, dtype="fp32"):
+    """As mpd_gan_losses, over the MultiResSpecDiscriminator outputs."""
+    msd(y, y_hat, dtype=dtype)
+    loss = msd.engine(dtype).gan_losses()
     return loss[0], loss[1], loss[2]

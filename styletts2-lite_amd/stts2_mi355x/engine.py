@@ -14,7 +14,7 @@ import os
 import numpy as np
 import torch
 
-KIND_HIFIGAN, KIND_ISTFTNET, KIND_F0N, KIND_STYLE, KIND_MPD, KIND_VOCOS = 0, 1, 2, 3, 4, 5
+KIND_HIFIGAN, KIND_ISTFTNET, KIND_F0N, KIND_STYLE, KIND_MPD, KIND_VOCOS, KIND_MSD = 0, 1, 2, 3, 4, 5, 6
 DTYPES = {"fp32": 0, "bf16": 1}
 
 _LIB = None
@@ -64,6 +64,17 @@ def lib():
     L.stts_mpd_fwd.restype = c_int
     L.stts_mpd_losses.argtypes = [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]
     L.stts_mpd_losses.restype = c_int
+    L.stts_msd_out_elems.argtypes = [c_vp, c_int, c_int]
+    L.stts_msd_out_elems.restype = c_ll
+    L.stts_msd_fwd.argtypes = [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_ll, c_vp, c_ll, c_vp]
+    L.stts_msd_fwd.restype = c_int
+    L.stts_msd_losses.argtypes = [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]
+    L.stts_msd_losses.restype = c_int
+    L.stts_mrstft_workspace_bytes.argtypes = [c_int, c_ll, ctypes.POINTER(c_int), c_int, c_int]
+    L.stts_mrstft_workspace_bytes.restype = c_ll
+    L.stts_mrstft_loss.argtypes = [c_vp, c_vp, c_int, c_ll, c_ll, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                   ctypes.POINTER(c_int), c_int, c_int, c_int, c_vp, c_vp, c_ll, c_vp]
+    L.stts_mrstft_loss.restype = c_int
     L.stts_mel_frames.argtypes = [c_ll]
     L.stts_mel_frames.restype = c_ll
     L.stts_mel_workspace_bytes.argtypes = []
@@ -416,6 +427,72 @@ class MPDEngine(_Engine):
         loss = torch.empty(3, dtype=torch.float64, device=out.device)
         check(lib().stts_mpd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), _ptr(loss), _stream()),
               "stts_mpd_losses")
+        return loss
+
+
+def msd_geometry(T, n_fft, hop):
+    """SpecDiscriminator map sizes over T samples (plan.cpp:msd_geom): H frames, widths W[0..5]."""
+    H = 1 + T // hop
+    W = [n_fft // 2 + 1] * 2
+    for _ in range(3):
+        W.append((W[-1] - 1) // 2 + 1)
+    W.append(W[-1])
+    return H, W
+
+
+class MSDEngine(_Engine):
+    """HIP forward of Modules/discriminators.py MultiResSpecDiscriminator's SpecDiscriminator stacks
+    (reference :47-63): one batch of waveforms [B, 1, T] -> per resolution (scores [B, H*W], fmaps)."""
+
+    def __init__(self, module, dtype="fp32"):
+        super().__init__(module, dtype)
+        self.res = [(d.fft_size, d.shift_size, d.win_length) for d in module.discriminators]
+        cfg = [len(self.res)] + [v for r in self.res for v in r]
+        self.model = NativeModel(KIND_MSD, cfg, module)
+        self.model.pack(dtype)
+
+    def forward(self, x):
+        dev = self.model.device
+        in_dev = x.device
+        w = _dev_f32(x, dev)
+        if w.dim() == 3:
+            if w.shape[1] != 1:
+                raise ValueError(f"waveform must be [B, 1, T] or [B, T], got {tuple(w.shape)}")
+            w = w[:, 0]
+        B, T = w.shape
+        for n_fft, _, _ in self.res:
+            if T <= n_fft // 2:  # torch.stft's reflect pad
+                raise ValueError(f"T = {T} too short for n_fft {n_fft}")
+        w = w.contiguous()
+        n = lib().stts_msd_out_elems(self.model.h, B, T)
+        check(int(n) if n < 0 else 0, "stts_msd_out_elems")
+        out = torch.empty(int(n), dtype=torch.float32, device=dev)
+        ws, nb = self.model.workspace(self.dtype, B, T)
+        check(lib().stts_msd_fwd(self.model.h, DTYPES[self.dtype], _ptr(w), B, T, _ptr(out), int(n), _ptr(ws), nb,
+                                 _stream()), "stts_msd_fwd")
+        self.last = (out, B, T)
+        res, off = [], 0
+        for n_fft, hop, _ in self.res:
+            H, W = msd_geometry(T, n_fft, hop)
+            fmaps = []
+            for j in range(6):
+                C, Wj = (32, W[j + 1]) if j < 5 else (1, W[5])
+                k = B * H * Wj * C
+                f = out[off:off + k].view(B, H, Wj, C).permute(0, 3, 1, 2)  # -> [B, C, H, W] (a view)
+                fmaps.append(f if in_dev.type == "cuda" else f.to(in_dev))
+                off += k
+            res.append((torch.flatten(fmaps[-1], 1, -1), fmaps))  # discriminators.py:63
+        return res
+
+    def gan_losses(self):
+        """losses.py:97-128 over the last forward's outputs (B real then B generated signals)."""
+        out, B2, T = self.last
+        if B2 % 2:
+            raise ValueError("the last forward's batch is not real + generated halves")
+        scratch = torch.zeros(4 * 6 * len(self.res), dtype=torch.float64, device=out.device)
+        loss = torch.empty(3, dtype=torch.float64, device=out.device)
+        check(lib().stts_msd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), _ptr(loss), _stream()),
+              "stts_msd_losses")
         return loss
 
 
