@@ -663,8 +663,10 @@ MRSTFT = dict(fft_sizes=(1024, 2048, 512), hop_sizes=(120, 240, 50), win_lengths
 def mel_spectrogram_sr(wave, sample_rate, n_fft, win_length, hop_length, n_mels=128):
     """torchaudio.transforms.MelSpectrogram(sample_rate, n_fft, win_length, hop_length, window_fn=hann)
     at its other defaults (losses.py:43): f_min 0, f_max sr // 2, power 2, center/reflect, HTK, no norm."""
-    spec = torch.stft(wave, n_fft, hop_length, win_length, torch.hann_window(win_length), center=True,
-                      pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
+    lead = wave.shape[:-1]  # torchaudio packs the leading dims into one batch dim around torch.stft
+    spec = torch.stft(wave.reshape(-1, wave.shape[-1]), n_fft, hop_length, win_length, torch.hann_window(win_length),
+                      center=True, pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
+    spec = spec.reshape(lead + spec.shape[-2:])
     power = spec.abs().pow(2.0)
     fb = melscale_fbanks(n_fft // 2 + 1, 0.0, float(sample_rate // 2), n_mels, sample_rate)
     return torch.matmul(power.transpose(-1, -2), fb).transpose(-1, -2)
