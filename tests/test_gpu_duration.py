@@ -364,3 +364,20 @@ def test_lstm_cooperative_timeout_raises():
     y2, _ = lstm(x)  # healthy again, and the check passes
     prosody.check_pending()
     assert torch.isfinite(y2).all()
+
+
+def test_generate_vs_reference_fixture():
+    """StyleTTS2.generate on the drop-ins against the REFERENCE's own generate() output
+    (tests/golden/generate_ref.npz: same weights, token ids, dur_stats draws and SineGen noise), fp32,
+    north-star waveform tolerance 1e-3."""
+    from stts2_mi355x.inference import Synthesizer
+    from test_generate_ref_cpu import case, modules
+    g, sents, zs, nfs = case()
+    te, pp, dec = modules(int(g["n_symbols"]))
+    syn = Synthesizer(te.cuda(), pp.cuda(), dec.cuda())
+    got = syn.generate(sents, {"style": torch.from_numpy(g["s"]).cuda(), "speed": 1}, stabilize=True,
+                       z=[z.cuda() for z in zs], noise=[(lambda F, f=f: f(F).cuda()) for f in nfs])
+    assert got.shape == g["wav"].shape
+    err = float(np.abs(got - g["wav"]).max())
+    print(f"generate vs reference fixture: {got.shape[0]} samples, max-abs {err:.3e}")
+    assert err < 1e-3

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import decoder_case, make_decoder
+from helpers import golden, decoder_case, make_decoder
 from oracle import stts_oracle as orc
 
 pytestmark = pytest.mark.gpu
@@ -52,11 +52,19 @@ def test_odd_lengths_fp32(kind, T):
     out = gpu(kind, *case, "fp32")
     assert out.shape == ref.shape == (3, 1, 600 * T)
     err = np.abs(out - ref).max()
-    # T = 2: every InstanceNorm averages two frames, and near-equal pairs make the forward
-    # ill-conditioned -- the fp32 oracle itself moves by 1.5e-2 under a 1e-6 relative weight
-    # perturbation and by 4.5e-3 against an fp64 run of the same oracle (utt0=5), so the bound
-    # there is 5e-2; T >= 3 moves by < 4e-5 under the same perturbation and keeps 1e-3.
-    tol = 5e-2 if T == 2 else 1e-3
+    tol = 1e-3
+    if T == 2:
+        # every InstanceNorm averages two frames and near-equal pairs make the forward ill-conditioned.
+        # The bound is pinned by the REFERENCE's own conditioning (tests/golden/make_golden_edge.py):
+        # its output moves by spread_perturbed under a 1e-6 relative weight perturbation and by
+        # spread_fp64 against a float64 run (hifigan 3.4e-3 / 4.5e-3, istftnet 8.9e-5 / 1.8e-4);
+        # the GPU result must sit within 10x that of the reference's own output.
+        g = golden(f"{kind}_T2_B3_edge")
+        spread = max(float(g["spread_perturbed"]), float(g["spread_fp64"]))
+        tol = max(1e-3, 10 * spread)
+        err_ref = np.abs(out - g["out"]).max()
+        print(f"{kind} T=2: max-abs vs reference {err_ref:.3e} (tol {tol:.2e}), vs oracle {err:.3e}")
+        assert err_ref < tol, f"{kind} T=2: max-abs vs reference {err_ref}"
     assert err < tol, f"{kind} T={T}: max-abs {err}"
 
 
