@@ -67,7 +67,8 @@ __device__ __forceinline__ double* stats_slot(const ConvParams& p, int g) {
 // stats[b][c] += sum of slots 1..S-1, and those slots are zeroed, for b < B, c < C
 int st_stats_fold(double* stats, int B, int ld, int C, int slots, long long slot_bs, hipStream_t s);
 // which engine st_conv1d routes p to (profiling records; bench.py names the dominant kernel)
-enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2, ST_ENGINE_RESFUSED = 3, ST_ENGINE_HEAD = 4 };
+enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2, ST_ENGINE_RESFUSED = 3, ST_ENGINE_HEAD = 4,
+       ST_ENGINE_PW = 5 };
 int st_conv1d_engine(const ConvParams& p, int dtype);
 // resblock conv engine (resconv.hip): bf16, C = 32 / 64, 1-D 'same' dilated conv with the
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.
@@ -96,6 +97,11 @@ extern int g_opt_front;
 bool st_head_eligible(const ConvParams& p);
 int st_head(const ConvParams& p, int dtype, hipStream_t stream);
 extern int g_opt_head;
+// pointwise (1x1) conv engine (pwgemm.hip): bf16, K = 1, N % 64 == 0, [AdaIN] prologue, bias / residual /
+// GELU epilogue, no statistics; st_conv1d routes eligible launches to it while g_opt_pw != 0
+bool st_pw_eligible(const ConvParams& p, int dtype);
+int st_pw(const ConvParams& p, hipStream_t stream);
+extern int g_opt_pw;
 
 // fused AdaINResBlock1 iteration (resfused.hip): bf16, C = 32 (K = 3/7/11) or 64 (K = 3).
 //   y = conv2(Snake2(AdaIN2(conv1(Snake1(AdaIN1(x)))))) + x     (hifigan.py:65-74)

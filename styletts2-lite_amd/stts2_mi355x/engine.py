@@ -112,9 +112,10 @@ OPT_BIGCONV = 7
 OPT_HEAD = 8
 OPT_SKEW = 9
 OPT_FRONT = 10
+OPT_PW = 11
 # the production defaults of every STTS_OPT_* (include/stts2.h)
 OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
-                OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1, OPT_SKEW: 0, OPT_FRONT: 1}
+                OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1, OPT_SKEW: 0, OPT_FRONT: 1, OPT_PW: 1}
 
 
 def set_option(key: int, value: int) -> None:
@@ -530,7 +531,8 @@ def profile_read():
     return {"ms": t.value, "launches": n.value, "flops": f.value, "bytes": b.value}
 
 
-ENGINE_KERNELS = ("conv1d_igemm_kernel", "k_resconv", "k_bigconv", "k_resfused", "k_conv_post")  # engine ids 0..4
+ENGINE_KERNELS = ("conv1d_igemm_kernel", "k_resconv", "k_bigconv", "k_resfused", "k_conv_post",
+                  "k_pwgemm")  # engine ids 0..5
 
 
 def profile_launches():

@@ -70,7 +70,7 @@ def reference(x, w, b, gb, alpha, slope, res, scale, c):
     return y * scale
 
 
-def run_case(case, dtype):
+def run_case(case, dtype, stats=True):
     name, Cin, Cout, K, tr, st, dil, pad, op, L, pro = case
     g = torch.Generator().manual_seed(hash(name) % 1000)
     B = 2
@@ -92,7 +92,7 @@ def run_case(case, dtype):
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)  # noqa: E731
     rc = E.lib().stts_test_conv1d(E.DTYPES[dtype], P(xd), B, L, Cin, P(wd), P(bd), Cout, K, tr, st, dil, pad, op,
                                   pro, P(gbd), P(ad), ctypes.c_float(slope), P(rd), ctypes.c_float(scale), P(y), Lout,
-                                  P(st_out))
+                                  P(st_out if stats else None))
     E.check(rc)
     return ref, y.cpu(), st_out.cpu()
 
@@ -214,3 +214,30 @@ def test_bigconv_8wave_many_tiles_per_workgroup(case):
     scale = max(1.0, y0.abs().max().item())
     assert (y - y0).abs().max().item() <= 2 ** -7 * scale, case[0]
     np.testing.assert_allclose(s.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
+
+
+PW_CASES = [
+    # 1x1 convs without statistics: the pointwise GEMM engine (pwgemm.hip, bf16)
+    ("pw_sc_514_1024_nores", 514, 1024, 1, 0, 1, 1, 0, 0, 400, 0),
+    ("pw_sc_1090_512_nores", 1090, 512, 1, 0, 1, 1, 0, 0, 333, 0),
+    ("pw_vocos1_512_1536_nores", 512, 1536, 1, 0, 1, 1, 0, 0, 800, 1),
+    ("pw_vocos2_1536_512", 1536, 512, 1, 0, 1, 1, 0, 0, 257, 0),
+    ("pw_head_512_1216_nores", 512, 1216, 1, 0, 1, 1, 0, 0, 130, 0),
+    ("pw_64_affine", 96, 64, 1, 0, 1, 1, 0, 0, 77, 1),
+]
+
+
+@pytest.mark.parametrize("case", PW_CASES, ids=[c[0] for c in PW_CASES])
+def test_pw_engine(case):
+    """bf16 1x1 convs on the pointwise engine against torch fp32 (3 % of range, as the other bf16
+    engine cases) and against the igemm engine on the same launch (2^-7 of range)."""
+    try:
+        E.set_option(E.OPT_PW, 0)
+        _, y0, _ = run_case(case, "bf16", stats=False)
+        E.set_option(E.OPT_PW, 1)
+        ref, y1, _ = run_case(case, "bf16", stats=False)
+    finally:
+        E.reset_options()
+    scale = max(1.0, ref.abs().max().item())
+    assert (y1 - ref).abs().max().item() <= 3e-2 * scale, case[0]
+    assert (y1 - y0).abs().max().item() <= 2 ** -7 * scale, case[0]
