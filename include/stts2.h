@@ -280,8 +280,9 @@ const char* stts_error_string(int code);
  *                     run on the bigconv2 engine when the launch has at least half as many tiles as
  *                     CUs (else igemm: small batches); 2 = bigconv2 at any size (tests); 0 = igemm. */
 #define STTS_OPT_FRONT 10
-/*   STTS_OPT_PW       1 (default) = bf16 1x1 convs without statistics (the AdainResBlk1d shortcuts, the Vocos
- *                     pointwise Linears) run on the pointwise GEMM engine (pwgemm.hip); 0 = igemm (A/B). */
+/*   STTS_OPT_PW       1 (default) = bf16 1x1 convs (the AdainResBlk1d shortcuts, asr_res, the Vocos pointwise
+ *                     Linears) run on the short-conv GEMM engine (pwgemm.hip); 2 = the 2-tap polyphase
+ *                     upsamplers too (measured slower); 0 = conv1d_igemm (A/B). */
 #define STTS_OPT_PW 11
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */

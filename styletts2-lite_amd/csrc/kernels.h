@@ -97,8 +97,8 @@ extern int g_opt_front;
 bool st_head_eligible(const ConvParams& p);
 int st_head(const ConvParams& p, int dtype, hipStream_t stream);
 extern int g_opt_head;
-// pointwise (1x1) conv engine (pwgemm.hip): bf16, K = 1, N % 64 == 0, [AdaIN] prologue, bias / residual /
-// GELU epilogue, no statistics; st_conv1d routes eligible launches to it while g_opt_pw != 0
+// short-conv GEMM engine (pwgemm.hip): bf16, 1 tap (2 with g_opt_pw == 2), N % 64 == 0, [AdaIN / Snake /
+// LReLU] prologue, bias / residual / GELU / statistics epilogue; st_conv1d routes eligible launches to it
 bool st_pw_eligible(const ConvParams& p, int dtype);
 int st_pw(const ConvParams& p, hipStream_t stream);
 extern int g_opt_pw;

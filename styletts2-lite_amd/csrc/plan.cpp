@@ -1789,7 +1789,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_HEAD: g_opt_head = value ? 1 : 0; return 0;
     case STTS_OPT_SKEW: g_opt_skew = value; return 0;
     case STTS_OPT_FRONT: g_opt_front = (value >= 0 && value <= 2) ? value : 1; return 0;
-    case STTS_OPT_PW: g_opt_pw = value ? 1 : 0; return 0;
+    case STTS_OPT_PW: g_opt_pw = (value >= 0 && value <= 2) ? value : 1; return 0;
     default: return ST_EINVAL;
   }
 }

@@ -224,20 +224,29 @@ PW_CASES = [
     ("pw_vocos2_1536_512", 1536, 512, 1, 0, 1, 1, 0, 0, 257, 0),
     ("pw_head_512_1216_nores", 512, 1216, 1, 0, 1, 1, 0, 0, 130, 0),
     ("pw_64_affine", 96, 64, 1, 0, 1, 1, 0, 0, 77, 1),
+    # polyphase ConvTranspose1d upsamplers (2 taps, N = u * Cout): Snake / LReLU prologues
+    ("pw_ups1_u5", 256, 128, 10, 1, 5, 1, 3, 1, 31, 2),
+    ("pw_ups2_u3", 128, 64, 6, 1, 3, 1, 2, 1, 300, 2),
+    ("pw_ups3_u2", 64, 32, 4, 1, 2, 1, 1, 0, 517, 2),
+    ("pw_istft_ups0_lrelu", 512, 256, 20, 1, 10, 1, 5, 0, 40, 4),
 ]
 
 
 @pytest.mark.parametrize("case", PW_CASES, ids=[c[0] for c in PW_CASES])
 def test_pw_engine(case):
-    """bf16 1x1 convs on the pointwise engine against torch fp32 (3 % of range, as the other bf16
-    engine cases) and against the igemm engine on the same launch (2^-7 of range)."""
+    """bf16 1- / 2-tap convs on the short-conv GEMM engine against torch fp32 (3 % of range, as the other
+    bf16 engine cases) and against the igemm engine on the same launch (2^-7 of range), outputs and
+    InstanceNorm statistics."""
     try:
         E.set_option(E.OPT_PW, 0)
-        _, y0, _ = run_case(case, "bf16", stats=False)
-        E.set_option(E.OPT_PW, 1)
-        ref, y1, _ = run_case(case, "bf16", stats=False)
+        _, y0, s0 = run_case(case, "bf16")
+        E.set_option(E.OPT_PW, 2)  # 2-tap launches too
+        ref, y1, s1 = run_case(case, "bf16")
+        _, y2, _ = run_case(case, "bf16", stats=False)
     finally:
         E.reset_options()
     scale = max(1.0, ref.abs().max().item())
     assert (y1 - ref).abs().max().item() <= 3e-2 * scale, case[0]
     assert (y1 - y0).abs().max().item() <= 2 ** -7 * scale, case[0]
+    assert torch.equal(y1, y2), case[0]
+    np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-3, atol=1e-1)
