@@ -265,7 +265,8 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_BIGCONV  2 (default) = the C = 128 / 256 resblock convs run on bigconv2.hip (per-wave
  *                     LDS-DMA weight rings, one barrier per 32-channel group): 8-wave blocks, or
  *                     4-wave blocks two per CU when a launch has fewer 8-wave tiles than CUs (small
- *                     batches); C = 128 with 3 taps on bigconv.hip (measured faster); 1 =
+ *                     batches) and for C = 128 with 7 / 11 taps; C = 128 with 3 taps on bigconv.hip
+ *                     (measured faster); 1 =
  *                     bigconv.hip everywhere; 3 = bigconv2.hip, 4-wave blocks; 4 = bigconv2.hip,
  *                     8-wave blocks (A/B, tests). */
 #define STTS_OPT_BIGCONV 7

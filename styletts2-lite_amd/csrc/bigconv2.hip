@@ -792,8 +792,12 @@ int st_bigconv2(const ConvParams& p, hipStream_t stream) {
   // 4-wave blocks, two per CU, twice the tiles (profiles/r02_ab_b1.txt: C = 256 k11 75 -> 61 us)
   const int tm8 = p.Cout == 128 ? 512 : 256;
   const long long tiles8 = (long long)((p.Lq + tm8 - 1) / tm8) * p.B;
-  // (mode 4 = 8-wave blocks at any size: tests)
-  const bool two = g_opt_bigconv == 3 || (g_opt_bigconv == 2 && tiles8 < b2_num_cu());
+  // (mode 4 = 8-wave blocks at any size: tests).  Mode 2 also takes the 4-wave blocks for C = 128 with
+  // 7 / 11 taps at every size: two blocks per CU overlap one block's window transform / epilogue with
+  // the other's MFMAs, 371 -> 346 us (k7 conv1) and 445 -> 404 us (k7 conv2) at B = 32, while C = 256
+  // and C = 128 k3 are faster with 8-wave blocks / v1 (profiles/r02_ab_bigconv_modes.txt)
+  const bool two = g_opt_bigconv == 3 ||
+                   (g_opt_bigconv == 2 && (tiles8 < b2_num_cu() || (p.Cout == 128 && p.KS >= 7)));
   if (p.Cout == 128) return two ? launch_b2_c<128, 4>(p, stream) : launch_b2_c<128, 8>(p, stream);
   if (p.Cout == 256) return two ? launch_b2_c<256, 4>(p, stream) : launch_b2_c<256, 8>(p, stream);
   return ST_EINVAL;
