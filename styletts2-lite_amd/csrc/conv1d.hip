@@ -810,7 +810,7 @@ int st_conv1d_engine(const ConvParams& p, int dtype) {
   if (st_front_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return ST_ENGINE_RESCONV;
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
-  if (st_pw_eligible(q, dtype)) return ST_ENGINE_PW;
+  if (st_pw_split_eligible(q, dtype) || st_pw_eligible(q, dtype)) return ST_ENGINE_PW;
   return ST_ENGINE_IGEMM;
 }
 
@@ -826,6 +826,7 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (st_front_eligible(q, dtype)) return st_bigconv2_front(q, stream);
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return st_resconv(q, stream);
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return st_bigconv(q, stream);
+  if (st_pw_split_eligible(q, dtype)) return st_pw_split(q, stream);
   if (st_pw_eligible(q, dtype)) return st_pw(q, stream);
   if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);
   if (dtype == ST_BF16) {

@@ -57,6 +57,8 @@ struct ConvParams {
   int tg;          // taps per staged weight group (set by the launcher)
   int cps;         // 32-channel chunks per pipeline step, 1 or 2 (set by the launcher)
   int w_resident;  // weights of the column tile stay in LDS across tiles (set by the launcher)
+  float* splitk_ws;          // fp32 scratch for split-K partials of small launches (plan workspace), or null
+  long long splitk_ws_elems;
 };
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);
@@ -101,6 +103,10 @@ extern int g_opt_head;
 // LReLU] prologue, bias / residual / GELU / statistics epilogue; st_conv1d routes eligible launches to it
 bool st_pw_eligible(const ConvParams& p, int dtype);
 int st_pw(const ConvParams& p, hipStream_t stream);
+// its split-K path for small launches (tiles < CUs / 2, >= 8 chunks, 1-3 'same' taps): needs splitk_ws
+bool st_pw_split_eligible(const ConvParams& p, int dtype);
+extern int g_opt_splitk;  // STTS_OPT_SPLITK
+int st_pw_split(const ConvParams& p, hipStream_t stream);
 extern int g_opt_pw;
 
 // fused AdaINResBlock1 iteration (resfused.hip): bf16, C = 32 (K = 3/7/11) or 64 (K = 3).

@@ -564,6 +564,14 @@ struct Ctx {
   // atomics do not all land on the same few (utterance, channel) addresses (B = 1: ~200-450 us a
   // launch measured, tools/phase_profile.py with PHASE_B=1), folded after each producing launch
   int slots = 1;
+  // small batches: fp32 scratch for the split-K partials of the short-conv engine (pwgemm.hip)
+  float* splitk = nullptr;
+  long long splitk_elems = 0;
+  void alloc_splitk(long long rows_x_cols) {
+    if (B > 4) return;
+    splitk_elems = 8LL * B * rows_x_cols;  // up to 8 slices
+    splitk = reinterpret_cast<float*>(alloc((size_t)splitk_elems * 4));
+  }
   float* H = nullptr;
   const char* packed;
   char* aux;
@@ -643,6 +651,8 @@ ConvParams conv_base(Ctx& c, const WConv& w, const Buf& x, int c0) {
   p.pro = pro_none();
   p.up = 1;
   p.out_scale = 1.0f;
+  p.splitk_ws = c.splitk;
+  p.splitk_ws_elems = c.splitk_elems;
   return p;
 }
 
@@ -924,6 +934,7 @@ FrontBufs alloc_front(Ctx& c, int T) {
   f.POOL = c.frames(2 * T, ld_cat);
   f.X0 = c.frames(2 * T, 512);
   c.H = reinterpret_cast<float*>(c.alloc((size_t)c.B * m.Htot * 4));
+  c.alloc_splitk((long long)T * 1024);  // the largest front-end conv output: T x 1024 = 2T x 512
   return f;
 }
 
@@ -1311,6 +1322,7 @@ int f0n_forward(Ctx& c, const float* x, const float* s, int T, float* F0, float*
   Buf Y0 = c.frames(T, d), Y1 = c.frames(2 * T, d / 2), Y2 = c.frames(2 * T, d / 2);
   Buf H1 = c.frames(2 * T, d), SC = c.frames(T, d), POOL = c.frames(2 * T, rup8(d));
   c.H = reinterpret_cast<float*>(c.alloc((size_t)B * m.Htot * 4));
+  c.alloc_splitk((long long)T * d);  // the largest conv output of the stacks: T x d = 2T x d/2
   c.stats_begin = c.stats_off = c.off;
   RUN(st_linear(s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
   double* S0 = c.stat(d);
@@ -1790,6 +1802,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_SKEW: g_opt_skew = value; return 0;
     case STTS_OPT_FRONT: g_opt_front = (value >= 0 && value <= 2) ? value : 1; return 0;
     case STTS_OPT_PW: g_opt_pw = (value >= 0 && value <= 2) ? value : 1; return 0;
+    case STTS_OPT_SPLITK: g_opt_splitk = value ? 1 : 0; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1812,6 +1825,7 @@ int stts_get_option(int key) {
     case STTS_OPT_SKEW: return g_opt_skew;
     case STTS_OPT_FRONT: return g_opt_front;
     case STTS_OPT_PW: return g_opt_pw;
+    case STTS_OPT_SPLITK: return g_opt_splitk;
     default: return ST_EINVAL;
   }
 }

@@ -236,6 +236,198 @@ __global__ void __launch_bounds__(NT, 2) k_pwgemm(const ConvParams p, int ntm, i
   if (cur_key >= 0 && p.stats) flush(cur_b, (cur_key % ntn) * BN);
 }
 
+
+// ---------------------------------------------------------------------------- split-K (small launches)
+// At B = 1 the front-end / F0N k3 convs make 56 tiles for 256 CUs and each walks ~100 chunk steps on
+// conv1d_igemm (120-132 us a launch, profiles/r02_layers_bf16_b1.txt).  Here the chunk range is split
+// over S slices: block (tile, slice) writes its fp32 partial tile to the workspace, and k_pw_reduce sums
+// the S partials in slice order (deterministic), then applies bias, residual (row >> res_shift) x
+// out_scale, GELU, the bf16 store and the InstanceNorm statistics.
+template <int TAPS>
+__global__ void __launch_bounds__(NT) k_pwsplit(const ConvParams p, int ntm, int ntn, int S, float* __restrict__ part) {
+  constexpr int XR = BM + TAPS - 1;
+  constexpr int XU = (XR * 4 + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][XR * XP];
+  __shared__ __attribute__((aligned(16))) bf16_t Ws[2][TAPS * BN * WP];
+  extern __shared__ __attribute__((aligned(16))) float coef[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int slice = blockIdx.x % S, t = blockIdx.x / S;
+  const int tn = t % ntn, tm = (t / ntn) % ntm, b = t / (ntn * ntm);
+  const int q0 = tm * BM, n0 = tn * BN;
+  const int nch = p.nchunks, cpad = nch * 32, mode = p.pro.mode;
+  const int cb = (int)((long long)nch * slice / S), ce = (int)((long long)nch * (slice + 1) / S);
+  const int Np = (p.N + 31) & ~31;
+  if (mode) {
+    for (int c = cb * 32 + tid; c < ce * 32; c += NT) {
+      float mm = 0.f, aa = 1.f, be = 0.f, al = 1.f;
+      if (c < p.Cin) {
+        if (mode & PRO_AFFINE) adain_coeffs(p.pro, b, c, mm, aa, be);
+        if (mode & PRO_SNAKE) al = p.pro.alpha[c];
+      }
+      coef[c] = be - mm * aa;
+      coef[cpad + c] = aa;
+      coef[2 * cpad + c] = al;
+      coef[3 * cpad + c] = 1.0f / al;
+    }
+    __syncthreads();
+  }
+  const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)nch * TAPS * Np * 32 * 2));
+  const Rsrc rx = make_rsrc(reinterpret_cast<const bf16_t*>(p.x) + (size_t)b * p.x_bs,
+                            (unsigned)((size_t)p.Lin * p.x_ld * 2));
+  const int r0 = q0 - p.pad;
+  uint4 px[XU], pw[TAPS][2];
+  auto issue = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < XU; ++k) {
+      const int u = tid + k * NT, r = u >> 2, g = u & 3, gr = r0 + r;
+      px[k] = bload16(rx, (u < XR * 4 && gr >= 0 && gr < p.Lin) ? (unsigned)((gr * p.x_ld + c * 32 + 8 * g) * 2) : OOB);
+    }
+#pragma unroll
+    for (int tp = 0; tp < TAPS; ++tp)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int u = tid + k * NT, r = u >> 2, g = u & 3, n = n0 + r;
+        pw[tp][k] = bload16(rw, n < Np ? (unsigned)(((((size_t)c * TAPS + tp) * Np + n) * 32 + 8 * g) * 2) : OOB);
+      }
+  };
+  auto stage = [&](int c, int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < XU; ++k) {
+      const int u = tid + k * NT, r = u >> 2, g = u & 3, gr = r0 + r;
+      if (u >= XR * 4) continue;
+      uint4 o = px[k];
+      const int ch = c * 32 + 8 * g;
+      const bool row_ok = gr >= 0 && gr < p.Lin;
+      if (mode || ch + 8 > p.Cin || !row_ok) {
+        bf16x8 v;
+        __builtin_memcpy(&v, &o, 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float f = (float)v[j];
+          if (mode & PRO_AFFINE) f = __builtin_fmaf(f, coef[cpad + ch + j], coef[ch + j]);
+          if (mode & PRO_SNAKE) {
+            const float sn = __sinf(coef[2 * cpad + ch + j] * f);
+            f = __builtin_fmaf(sn * sn, coef[3 * cpad + ch + j], f);
+          }
+          if (mode & PRO_LRELU) f = f > 0.f ? f : f * p.pro.slope;
+          if (ch + j >= p.Cin || !row_ok) f = 0.f;
+          v[j] = (bf16_t)f;
+        }
+        __builtin_memcpy(&o, &v, 16);
+      }
+      *reinterpret_cast<uint4*>(&Xs[s][r * XP + 8 * g]) = o;
+    }
+#pragma unroll
+    for (int tp = 0; tp < TAPS; ++tp)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int u = tid + k * NT, r = u >> 2, g = u & 3, n = n0 + r;
+        *reinterpret_cast<uint4*>(&Ws[s][(tp * BN + r) * WP + 8 * (g ^ ((n >> 2) & 3))]) = pw[tp][k];
+      }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  if (ce > cb) {
+    issue(cb);
+    stage(cb, 0);
+    if (cb + 1 < ce) issue(cb + 1);
+    __syncthreads();
+    const bf16_t* xw0 = &Xs[0][(wm * 64 + l32) * XP + hi * 8];
+    const bf16_t* ww0 = &Ws[0][(wn * 64 + l32) * WP + hi * 8];
+    for (int c = cb; c < ce; ++c) {
+      const int s = (c - cb) & 1;
+      const bf16_t* xw = xw0 + s * XR * XP;
+      const bf16_t* ww = ww0 + s * TAPS * BN * WP;
+#pragma unroll
+      for (int tp = 0; tp < TAPS; ++tp)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          bf16x8 wa[2], xb[2];
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            wa[ni] = *reinterpret_cast<const bf16x8*>(ww + (tp * BN + ni * 32) * WP + kk * 16);
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+            xb[mi] = *reinterpret_cast<const bf16x8*>(xw + (mi * 32 + tp) * XP + kk * 16);
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ni], xb[mi], acc[mi][ni], 0, 0, 0);
+        }
+      if (c + 1 < ce) {
+        stage(c + 1, s ^ 1);
+        if (c + 2 < ce) issue(c + 2);
+        __syncthreads();
+      }
+    }
+  }
+  // fp32 partial tile -> part[slice][b][q][n]
+  float* pb = part + ((size_t)slice * p.B + b) * (size_t)p.Lq * p.N;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const int q = q0 + wm * 64 + mi * 32 + l32;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int nb = n0 + wn * 64 + ni * 32 + 16 * hi;
+      if (q >= p.Lq || nb >= p.N) continue;
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[mi][ni][r];
+      store16(pb + (size_t)q * p.N + nb, v);
+    }
+  }
+}
+
+// y[b][q][n] = epi(sum_s part[s][b][q][n]).  Block = 64 columns x RR rows; thread (column tx, row lane
+// ty of 4) owns rows q0 + ty + 4 i, so the loads of a row are coalesced and a thread has RR / 4
+// independent rows in flight; the statistics meet in LDS (fixed order) and leave as one atomic pair
+// per (block, column).
+constexpr int RR = 32;
+__global__ void __launch_bounds__(256) k_pw_reduce(const ConvParams p, int S, const float* __restrict__ part) {
+  __shared__ double red[2][4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + tx, b = blockIdx.z;
+  const int q0 = blockIdx.y * RR;
+  const size_t sb = (size_t)p.B * p.Lq * p.N;
+  const float* pb = part + (size_t)b * p.Lq * p.N + n;
+  bf16_t* yb = reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs;
+  const bf16_t* rb = p.res ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr;
+  const bool col = n < p.N;
+  const float bias = (p.bias && col) ? p.bias[n] : 0.f;
+  double a = 0.0, qq = 0.0;
+#pragma unroll
+  for (int i = 0; i < RR / 4; ++i) {
+    const int q = q0 + ty + 4 * i;
+    if (!col || q >= p.Lq) continue;
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += pb[s * sb + (size_t)q * p.N];
+    v += bias;
+    if (rb) v = (v + (float)rb[(size_t)(q >> p.res_shift) * p.res_ld + n]) * p.out_scale;
+    if (p.epi_gelu) v = 0.5f * v * (1.0f + erff(v * 0.7071067811865476f));
+    yb[(size_t)q * p.y_ld + n] = (bf16_t)v;
+    a += v;
+    qq += (double)v * v;
+  }
+  if (!p.stats) return;
+  red[0][ty][tx] = a;
+  red[1][ty][tx] = qq;
+  __syncthreads();
+  if (ty == 0 && col) {
+    const double sa = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
+    const double sq = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+    double* d = stats_slot(p, blockIdx.y) + ((size_t)b * p.stats_ld + n) * 2;
+    atomicAdd(d, sa);
+    atomicAdd(d + 1, sq);
+  }
+}
+
 }  // namespace
 
 int g_opt_pw = 1;
@@ -283,5 +475,57 @@ int st_pw(const ConvParams& p, hipStream_t stream) {
     hipLaunchKernelGGL(k_pwgemm<1>, dim3((unsigned)blocks), dim3(NT), lds, stream, p, ntm, ntn);
   else
     hipLaunchKernelGGL(k_pwgemm<2>, dim3((unsigned)blocks), dim3(NT), lds, stream, p, ntm, ntn);
+  return (int)hipGetLastError();
+}
+
+int g_opt_splitk = 0;
+
+bool st_pw_split_eligible(const ConvParams& p, int dtype) {
+  if (!g_opt_pw || !g_opt_splitk || dtype != ST_BF16 || !p.splitk_ws) return false;
+  if (p.KS < 1 || p.KS > 3 || p.stride != 1 || p.dil != 1 || p.row_off != 0 || p.up != 1 || p.opad != 0) return false;
+  if (p.kw != 0 && p.kw != p.KS) return false;
+  if (p.pad != (p.KS - 1) / 2 || p.Lq != p.Lin || p.Lout != p.Lq) return false;
+  if (p.N % 64 != 0 || p.Cout != p.N) return false;
+  if (p.accb || p.y_f32 || p.y_row_off || p.epi_tanh || p.epi_lrelu || p.reflect_front || p.zc_period) return false;
+  if (p.pro.mode & ~(PRO_AFFINE | PRO_SNAKE | PRO_LRELU)) return false;
+  if (p.x_ld % 8 || p.y_ld % 8) return false;
+  if (!g_num_cu_pw) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_num_cu_pw, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return false;
+  }
+  const long long tiles = (long long)((p.Lq + BM - 1) / BM) * ((p.N + BN - 1) / BN) * p.B;
+  return tiles < g_num_cu_pw / 2 && p.nchunks >= 8;  // small launches with a long K only
+}
+
+int st_pw_split(const ConvParams& p, hipStream_t stream) {
+  const int ntm = (p.Lq + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const long long tiles = (long long)ntm * ntn * p.B;
+  // slices: about two blocks per CU, at least 4 chunks each, and the partials must fit the workspace
+  int S = (int)((2LL * g_num_cu_pw + tiles - 1) / tiles);
+  S = S < 1 ? 1 : S;
+  if (S > p.nchunks / 4) S = p.nchunks / 4;
+  while (S > 1 && (long long)S * p.B * p.Lq * p.N > p.splitk_ws_elems) --S;
+  if (S < 1 || (long long)S * p.B * p.Lq * p.N > p.splitk_ws_elems) return ST_EWORKSPACE;
+  const size_t lds = p.pro.mode ? (size_t)p.nchunks * 32 * 4 * sizeof(float) : 0;
+  static bool attr = false;
+  if (!attr) {
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)k_pwsplit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)k_pwsplit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)k_pwsplit<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    attr = true;
+  }
+  if (lds > 64 * 1024) return ST_EINVAL;
+  const dim3 grid((unsigned)(tiles * S));
+  if (p.KS == 1)
+    hipLaunchKernelGGL(k_pwsplit<1>, grid, dim3(NT), lds, stream, p, ntm, ntn, S, p.splitk_ws);
+  else if (p.KS == 2)
+    hipLaunchKernelGGL(k_pwsplit<2>, grid, dim3(NT), lds, stream, p, ntm, ntn, S, p.splitk_ws);
+  else
+    hipLaunchKernelGGL(k_pwsplit<3>, grid, dim3(NT), lds, stream, p, ntm, ntn, S, p.splitk_ws);
+  ST_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_pw_reduce, dim3((p.N + 63) / 64, (p.Lq + RR - 1) / RR, p.B), dim3(256), 0, stream, p, S,
+                     (const float*)p.splitk_ws);
   return (int)hipGetLastError();
 }

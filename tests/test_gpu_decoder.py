@@ -153,6 +153,28 @@ def test_resfused_decoder_ab(cap):
     assert corr > 0.9995 and err < 5e-2
 
 
+@pytest.mark.parametrize("B,T", [(1, 400), (2, 40)])
+def test_pw_split_decoder_ab(B, T):
+    """bf16 HiFi-GAN decode at small batch with the short-conv engine (its split-K path serves the
+    front-end k3 convs and the 1x1 shortcuts: fp32 slice partials summed in slice order) on and off
+    (STTS_OPT_PW 0 = conv1d_igemm).  Same bf16 model, different summation order."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_PW, 0)
+        ref = run("hifigan", B, T, "bf16")
+        E.set_option(E.OPT_PW, 1)
+        E.set_option(E.OPT_SPLITK, 1)
+        out = run("hifigan", B, T, "bf16")
+        out2 = run("hifigan", B, T, "bf16")
+    finally:
+        E.reset_options()
+    corr = np.corrcoef(out.ravel(), ref.ravel())[0, 1]
+    err = np.abs(out - ref).max()
+    print(f"pw split-K A/B B={B} T={T}: max-abs {err:.3e} corr {corr:.7f}")
+    assert corr > 0.9995 and err < 5e-2
+    assert np.array_equal(out, out2)  # deterministic (fixed slice order, no atomics on the outputs)
+
+
 # ---------------------------------------------------------------- config 3 (BASELINE configs[2])
 _CFG3 = {}
 
