@@ -478,7 +478,7 @@ int st_pw(const ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-int g_opt_splitk = 0;
+int g_opt_splitk = 1;
 
 bool st_pw_split_eligible(const ConvParams& p, int dtype) {
   if (!g_opt_pw || !g_opt_splitk || dtype != ST_BF16 || !p.splitk_ws) return false;
