@@ -131,6 +131,29 @@ int stts_mrstft_loss(const float* x, const float* y, int B, long long L, long lo
                      const int* hops, const int* wins, int n_res, int sample_rate, int n_mels, double* loss,
                      void* workspace, long long ws_bytes, void* stream);
 
+/* Conv1d forward / backward on caller frames: the conv layers of the training step (config 5).
+ * train.py:272-327 calls loss.backward() through the decoder's and the discriminators' nn.Conv1d layers
+ * (Modules/hifigan.py:26-80, 292-294, 427-432; Modules/discriminators.py:96-156, weight norm folded):
+ * these compute y = conv1d(x, w, bias, stride, padding=pad, dilation=dil) and the gradients torch
+ * autograd gives for it.  All tensors fp32 on the device, frames layout (channels contiguous):
+ * x / dx [B][Lin][Cin], y / dy [B][Lq][Cout], w / dw [Cout][Cin][K] (nn.Conv1d layout), bias / db [Cout];
+ * Lq = (Lin + 2 pad - dil (K - 1) - 1) / stride + 1 must hold (ST_EINVAL otherwise).
+ * y and dx run on the conv engine in `dtype` (dx of a stride-1 conv = the forward conv of dy with the
+ * channel-transposed, tap-reversed weight and padding dil (K - 1) - pad; of a strided conv (dil 1) = the
+ * polyphase ConvTranspose1d of dy); dw / db always compute in fp32 (f32 MFMA over (utterance, frame)
+ * row slices, fp64 fixed-order slice sums: deterministic).  dx, dw, db may each be null.
+ * Workspace >= the matching *_workspace_bytes. */
+long long stts_conv1d_fwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride, int dil,
+                                          int pad, int Lq);
+int stts_conv1d_fwd(int dtype, const float* x, const float* w, const float* bias, int B, int Lin, int Cin, int Cout,
+                    int K, int stride, int dil, int pad, int Lq, float* y, void* workspace, long long ws_bytes,
+                    void* stream);
+long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride, int dil,
+                                          int pad, int Lq);
+int stts_conv1d_bwd(int dtype, const float* x, const float* w, const float* dy, int B, int Lin, int Cin, int Cout,
+                    int K, int stride, int dil, int pad, int Lq, float* dx, float* dw, float* db, void* workspace,
+                    long long ws_bytes, void* stream);
+
 /* MultiResSpecDiscriminator forward, <- Modules/discriminators.py:47-63 SpecDiscriminator.forward for every
  * resolution (MultiResSpecDiscriminator.forward :80-94 calls it on y and y_hat: pass both as one batch).
  * wave [B][T] fp32.  out (fp32, >= stts_msd_out_elems) receives, resolution by resolution, the 5

@@ -1,0 +1,401 @@
+// Conv1d forward / backward on caller frames: the conv layers of the training step (config 5,
+// train.py:272-327 runs loss.backward() through the decoder's and the discriminators' convs).
+//
+//   y  = conv1d(x, w, bias, stride, pad, dil)      x [B][Lin][Cin], y [B][Lq][Cout] (fp32 frames)
+//   dx = conv_transpose1d(dy, w, stride, pad)      -> conv engine (st_conv1d) in the run's dtype:
+//          stride 1: a forward conv of dy with w'[ci][co][t] = w[co][ci][K-1-t], pad' = dil(K-1) - pad
+//          stride > 1 (dil 1): the engine's polyphase ConvTranspose with the weight as it is
+//   dw[co][ci][t] = sum_(b,q) dy[b][q][co] * x[b][q*stride + t*dil - pad][ci]
+//          -> k_wgrad: fp32-in MFMA (v_mfma_f32_32x32x2_f32), the (b, q) rows split into S slices,
+//             one fp32 partial per slice, summed in slice order in fp64 (k_slice_reduce): deterministic
+//   db[co] = sum_(b,q) dy[b][q][co]   -> k_colsum partials + the same reduction
+//
+// The wgrad GEMM is M = Cout, N = Cin (per tap), K = B*Lq (up to 3 M rows for a decoder stage):
+// both operands are frames (rows = time, channels contiguous), which is exactly the f32 MFMA's
+// operand map (lane l: A[m = l&31][k = l>>5], B[k = l>>5][n = l&31]), so 32 lanes read 128
+// contiguous bytes of one row and no LDS transpose is needed.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/stts2.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int kTargetWaves = 2048;  // 8 waves per CU on 256 CUs
+
+// one wave: (32*NA co) x (32*NB ci) of tap t over rows [r0, r1) of the flattened (b, q) range
+template <int NA, int NB, int UNR>
+__global__ __launch_bounds__(64) void k_wgrad(const float* __restrict__ x, const float* __restrict__ dy, int Lin,
+                                              int Cin, int Lq, int Cout, int K, int stride, int dil, int pad,
+                                              long long R, int S, int ntco, int ntci, float* __restrict__ part) {
+  const int lane = threadIdx.x;
+  int tile = blockIdx.x;
+  const int tci = tile % ntci;
+  tile /= ntci;
+  const int tco = tile % ntco;
+  const int t = tile / ntco;
+  const int s = blockIdx.y;
+  const long long r0 = R * s / S, r1 = R * (s + 1) / S;
+  const int col = lane & 31, h = lane >> 5;
+  int co[NA], ci[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) co[i] = (tco * NA + i) * 32 + col;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) ci[j] = (tci * NB + j) * 32 + col;
+  f32x16 acc[NA][NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  long long r = r0 + h;
+  long long b = r / Lq;
+  int q = (int)(r - b * Lq);
+  const int toff = t * dil - pad;
+  for (long long rb = r0; rb < r1; rb += 2 * UNR) {
+    float a[UNR][NA], v[UNR][NB];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const bool vr = r < r1;
+      const int xr = q * stride + toff;
+      const bool vx = vr && xr >= 0 && xr < Lin;
+      const float* yrow = dy + (b * Lq + q) * (long long)Cout;
+      const float* xrow = x + (b * Lin + xr) * (long long)Cin;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) a[u][i] = (vr && co[i] < Cout) ? yrow[co[i]] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v[u][j] = (vx && ci[j] < Cin) ? xrow[ci[j]] : 0.f;
+      r += 2;
+      q += 2;
+      while (q >= Lq) {
+        q -= Lq;
+        ++b;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i], v[u][j], acc[i][j], 0, 0, 0);
+  }
+  // C/D map: column = lane & 31 (ci), row = (e & 3) + 8 (e >> 2) + 4 h (co)
+  float* pt = part + ((size_t)s * K + t) * (size_t)Cout * Cin;
+#pragma unroll
+  for (int i = 0; i < NA; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int cr = (tco * NA + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (cr >= Cout) continue;
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        if (ci[j] < Cin) pt[(size_t)cr * Cin + ci[j]] = acc[i][j][e];
+    }
+}
+
+// part[s][t][co][ci] -> out[co][ci][t] = sum over s in order (fp64)
+__global__ void k_slice_reduce(const float* __restrict__ part, int S, int K, int Cout, int Cin,
+                               float* __restrict__ out) {
+  const size_t per = (size_t)K * Cout * Cin;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per) return;
+  const int ci = (int)(i % Cin);
+  const int co = (int)((i / Cin) % Cout);
+  const int t = (int)(i / ((size_t)Cin * Cout));
+  double sum = 0.0;
+  for (int s = 0; s < S; ++s) sum += part[s * per + i];
+  out[((size_t)co * Cin + ci) * K + t] = (float)sum;
+}
+
+// column sums of dy [R][C] over row slice s: part[s][c]
+__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ dy, long long R, int C, int S,
+                                                float* __restrict__ part) {
+  __shared__ double red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int s = blockIdx.y;
+  const long long r0 = R * s / S, r1 = R * (s + 1) / S;
+  double acc = 0.0;
+  if (c < C)
+    for (long long r = r0 + rl; r < r1; r += 4) acc += dy[r * C + c];
+  red[rl][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    const int l = threadIdx.x;
+    part[(size_t)s * C + c] = (float)(((red[0][l] + red[1][l]) + red[2][l]) + red[3][l]);
+  }
+}
+
+// w [Cout][Cin][K] -> wt [Cin][Cout][K] with the taps reversed (the stride-1 dgrad weight)
+__global__ void k_flip_transpose(const float* __restrict__ w, int Cout, int Cin, int K, float* __restrict__ wt) {
+  const size_t n = (size_t)Cout * Cin * K;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int t = (int)(i % K);
+  const int co = (int)((i / K) % Cout);
+  const int ci = (int)(i / ((size_t)K * Cout));
+  wt[i] = w[((size_t)co * Cin + ci) * K + (K - 1 - t)];
+}
+
+struct Geo {
+  int B, Lin, Cin, Cout, K, stride, dil, pad, Lq;
+};
+
+inline int ldpad(int c) { return (c + 7) & ~7; }
+
+bool geo_ok(const Geo& g) {
+  if (g.B <= 0 || g.Lin <= 0 || g.Cin <= 0 || g.Cout <= 0 || g.K <= 0 || g.stride <= 0 || g.dil <= 0 || g.pad < 0)
+    return false;
+  const long long lq = ((long long)g.Lin + 2LL * g.pad - (long long)g.dil * (g.K - 1) - 1) / g.stride + 1;
+  return lq == g.Lq && g.Lq > 0;
+}
+
+struct Slices {
+  int NA, NB, ntco, ntci, S, S2;
+};
+
+Slices slices_of(const Geo& g) {
+  Slices sl;
+  sl.NA = g.Cout > 32 ? 2 : 1;
+  sl.NB = g.Cin > 32 ? 2 : 1;
+  sl.ntco = (g.Cout + 32 * sl.NA - 1) / (32 * sl.NA);
+  sl.ntci = (g.Cin + 32 * sl.NB - 1) / (32 * sl.NB);
+  const long long R = (long long)g.B * g.Lq;
+  const long long tiles = (long long)g.K * sl.ntco * sl.ntci;
+  long long S = (kTargetWaves + tiles - 1) / tiles;
+  S = std::min<long long>(S, std::max<long long>(1, R / 64));  // >= 64 rows per slice
+  sl.S = (int)std::max<long long>(1, std::min<long long>(S, 4096));
+  const int cblk = (g.Cout + 63) / 64;
+  long long S2 = (512 + cblk - 1) / cblk;
+  S2 = std::min<long long>(S2, std::max<long long>(1, R / 256));
+  sl.S2 = (int)std::max<long long>(1, std::min<long long>(S2, 1024));
+  return sl;
+}
+
+// workspace pieces (bytes, each 256-aligned)
+struct WsLayout {
+  size_t xin, wstage, bpad, packed, yout, part, part2, total;
+};
+
+inline size_t al(size_t n) { return (n + 255) & ~(size_t)255; }
+
+enum WMode { W_PLAIN = 0, W_FLIP = 1, W_TRANS = 2 };
+
+// one engine launch as the caller sees it: ci_e -> co_e channels
+struct EngineGeo {
+  int Lin, ci, co, co_p, Lout, u, transposed, stride;
+  WMode wm;
+};
+
+// the conv engine's narrow epilogue (Cout % 16 != 0) serves only N <= 32 at stride 1: other
+// channel counts run with the output channels padded to 16 (zero weight rows) and are cropped
+EngineGeo engine_geo(const Geo& g, bool fwd) {
+  EngineGeo e;
+  e.Lin = fwd ? g.Lin : g.Lq;
+  e.Lout = fwd ? g.Lq : g.Lin;
+  e.ci = fwd ? g.Cin : g.Cout;
+  e.co = fwd ? g.Cout : g.Cin;
+  e.transposed = !fwd && g.stride > 1;
+  e.u = e.transposed ? g.stride : 1;
+  e.stride = fwd ? g.stride : 1;
+  e.wm = fwd ? W_PLAIN : (e.transposed ? W_TRANS : W_FLIP);
+  const bool pad = e.co % 16 != 0 && (e.u * e.co > 32 || e.stride > 1);
+  e.co_p = pad ? (e.co + 15) & ~15 : e.co;
+  return e;
+}
+
+WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
+  const size_t esz = dtype == ST_FP32 ? 4 : 2;
+  const EngineGeo e = engine_geo(g, fwd);
+  WsLayout w;
+  memset(&w, 0, sizeof(w));
+  size_t off = 0;
+  w.xin = off;
+  off += al((size_t)g.B * e.Lin * ldpad(e.ci) * esz);
+  w.wstage = off;
+  if (e.wm != W_PLAIN || e.co_p != e.co) off += al((size_t)e.co_p * e.ci * g.K * 4);
+  w.bpad = off;
+  if (e.co_p != e.co) off += al((size_t)e.co_p * 4);
+  w.packed = off;
+  off += al(st_packed_conv_elems(e.ci, e.co_p, g.K, e.transposed, e.u) * esz);
+  w.yout = off;
+  if (dtype != ST_FP32 || e.co_p != e.co) off += al((size_t)g.B * e.Lout * e.co_p * esz);
+  if (!fwd) {
+    const Slices sl = slices_of(g);
+    w.part = off;
+    off += al((size_t)sl.S * g.K * g.Cout * g.Cin * 4);
+    w.part2 = off;
+    off += al((size_t)sl.S2 * g.Cout * 4);
+  }
+  w.total = off;
+  return w;
+}
+
+// one engine launch: y fp32 [B][Lout][co] from xf fp32 frames [B][Lin][ci].  w is the forward
+// weight [Cout][Cin][K]; wm says how the engine's weight derives from it (W_PLAIN: as is, W_FLIP:
+// channel-transposed and tap-reversed, W_TRANS: as a ConvTranspose1d weight [in][out][K]).
+int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* w, const float* bias, float* y,
+               char* ws, hipStream_t s) {
+  const EngineGeo e = engine_geo(g, fwd);
+  const WsLayout L = ws_layout(g, dtype, fwd);
+  const int K = g.K, B = g.B;
+  const int ldx = ldpad(e.ci);
+  void* xd = ws + L.xin;
+  void* wd = ws + L.packed;
+  ST_CHECK(st_frames_convert(xf, B, e.Lin, e.ci, e.ci, xd, ldx, nullptr, 0, dtype, s));
+  const float* wsrc = w;
+  if (e.wm != W_PLAIN || e.co_p != e.co) {
+    float* wt = (float*)(ws + L.wstage);
+    const size_t nst = (size_t)e.co_p * e.ci * K;
+    const size_t n = (size_t)e.co * e.ci * K;
+    if (e.wm == W_TRANS) {  // [ci][co][K] -> [ci][co_p][K]
+      ST_CHECK_HIP(hipMemsetAsync(wt, 0, nst * 4, s));
+      ST_CHECK_HIP(hipMemcpy2DAsync(wt, (size_t)e.co_p * K * 4, w, (size_t)e.co * K * 4, (size_t)e.co * K * 4, e.ci,
+                                    hipMemcpyDeviceToDevice, s));
+    } else {  // [co][ci][K] rows, then zero rows co .. co_p
+      if (e.wm == W_FLIP) {
+        hipLaunchKernelGGL(k_flip_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, g.Cout, g.Cin, K,
+                           wt);
+        ST_CHECK_HIP(hipGetLastError());
+      } else {
+        ST_CHECK_HIP(hipMemcpyAsync(wt, w, n * 4, hipMemcpyDeviceToDevice, s));
+      }
+      if (nst > n) ST_CHECK_HIP(hipMemsetAsync(wt + n, 0, (nst - n) * 4, s));
+    }
+    wsrc = wt;
+  }
+  const float* bsrc = bias;
+  if (bias && e.co_p != e.co) {
+    float* bp = (float*)(ws + L.bpad);
+    ST_CHECK_HIP(hipMemsetAsync(bp, 0, (size_t)e.co_p * 4, s));
+    ST_CHECK_HIP(hipMemcpyAsync(bp, bias, (size_t)e.co * 4, hipMemcpyDeviceToDevice, s));
+    bsrc = bp;
+  }
+  ST_CHECK(st_pack_conv(wsrc, e.ci, e.co_p, K, e.transposed, e.u, wd, dtype, s));
+  ConvParams p;
+  memset(&p, 0, sizeof(p));
+  p.x = xd;
+  p.x_bs = (long long)e.Lin * ldx;
+  p.x_ld = ldx;
+  p.Lin = e.Lin;
+  p.Cin = e.ci;
+  p.B = B;
+  p.w = wd;
+  p.nchunks = (e.ci + 31) / 32;
+  p.bias = bsrc;
+  p.Cout = e.co_p;
+  if (!e.transposed) {
+    p.KS = K;
+    p.dil = g.dil;
+    p.stride = e.stride;
+    p.pad = fwd ? g.pad : g.dil * (K - 1) - g.pad;
+    p.N = e.co_p;
+    p.up = 1;
+    p.Lq = e.Lout;
+  } else {
+    const int taps = (K + e.u - 1) / e.u;
+    p.KS = taps;
+    p.dil = 1;
+    p.stride = 1;
+    p.pad = taps - 1;
+    p.N = e.u * e.co_p;
+    p.up = e.u;
+    p.opad = g.pad;
+    p.Lq = (e.Lout - 1 + g.pad) / e.u + 1;
+  }
+  p.Lout = e.Lout;
+  const bool direct = dtype == ST_FP32 && e.co_p == e.co;
+  void* yd = direct ? (void*)y : (void*)(ws + L.yout);
+  p.y = yd;
+  p.y_bs = (long long)e.Lout * e.co_p;
+  p.y_ld = e.co_p;
+  p.out_scale = 1.f;
+  ST_CHECK(st_conv1d(p, dtype, s));
+  if (!direct) ST_CHECK(st_frames_to_f32(yd, B, e.Lout, e.co, e.co_p, y, dtype, s));
+  return 0;
+}
+
+template <int NA, int NB>
+void launch_wgrad(const Geo& g, const Slices& sl, const float* x, const float* dy, float* part, hipStream_t s) {
+  dim3 grid(g.K * sl.ntco * sl.ntci, sl.S);
+  hipLaunchKernelGGL((k_wgrad<NA, NB, 4>), grid, dim3(64), 0, s, x, dy, g.Lin, g.Cin, g.Lq, g.Cout, g.K, g.stride,
+                     g.dil, g.pad, (long long)g.B * g.Lq, sl.S, sl.ntco, sl.ntci, part);
+}
+
+}  // namespace
+
+extern "C" long long stts_conv1d_fwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride,
+                                                     int dil, int pad, int Lq) {
+  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
+  if (!geo_ok(g)) return ST_EINVAL;
+  return (long long)ws_layout(g, dtype, true).total;
+}
+
+extern "C" int stts_conv1d_fwd(int dtype, const float* x, const float* w, const float* bias, int B, int Lin, int Cin,
+                               int Cout, int K, int stride, int dil, int pad, int Lq, float* y, void* workspace,
+                               long long ws_bytes, void* stream) {
+  const long long need = stts_conv1d_fwd_workspace_bytes(dtype, B, Lin, Cin, Cout, K, stride, dil, pad, Lq);
+  if (need < 0) return (int)need;
+  if (!x || !w || !y) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
+  return run_engine(dtype, g, true, x, w, bias, y, (char*)workspace, (hipStream_t)stream);
+}
+
+extern "C" long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride,
+                                                     int dil, int pad, int Lq) {
+  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
+  if (!geo_ok(g)) return ST_EINVAL;
+  if (g.stride > 1 && g.dil > 1) return ST_EINVAL;
+  if (g.stride == 1 && g.dil * (g.K - 1) < g.pad) return ST_EINVAL;
+  return (long long)ws_layout(g, dtype, false).total;
+}
+
+extern "C" int stts_conv1d_bwd(int dtype, const float* x, const float* w, const float* dy, int B, int Lin, int Cin,
+                               int Cout, int K, int stride, int dil, int pad, int Lq, float* dx, float* dw,
+                               float* db, void* workspace, long long ws_bytes, void* stream) {
+  const long long need = stts_conv1d_bwd_workspace_bytes(dtype, B, Lin, Cin, Cout, K, stride, dil, pad, Lq);
+  if (need < 0) return (int)need;
+  if (!dy || (dx && !w) || (dw && !x)) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
+  const WsLayout L = ws_layout(g, dtype, false);
+  char* ws = (char*)workspace;
+  if (dx) ST_CHECK(run_engine(dtype, g, false, dy, w, nullptr, dx, ws, s));
+  const Slices sl = slices_of(g);
+  if (dw) {
+    float* part = (float*)(ws + L.part);
+    if (sl.NA == 2 && sl.NB == 2)
+      launch_wgrad<2, 2>(g, sl, x, dy, part, s);
+    else if (sl.NA == 2)
+      launch_wgrad<2, 1>(g, sl, x, dy, part, s);
+    else if (sl.NB == 2)
+      launch_wgrad<1, 2>(g, sl, x, dy, part, s);
+    else
+      launch_wgrad<1, 1>(g, sl, x, dy, part, s);
+    ST_CHECK_HIP(hipGetLastError());
+    const size_t n = (size_t)K * Cout * Cin;
+    hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, sl.S, K, Cout, Cin,
+                       dw);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  if (db) {
+    float* part2 = (float*)(ws + L.part2);
+    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((Cout + 63) / 64), sl.S2), dim3(256), 0, s, dy,
+                       (long long)B * Lq, Cout, sl.S2, part2);
+    ST_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, part2, sl.S2, 1, Cout,
+                       1, db);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  return 0;
+}

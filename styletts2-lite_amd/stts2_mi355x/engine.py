@@ -70,6 +70,13 @@ def lib():
     L.stts_msd_fwd.restype = c_int
     L.stts_msd_losses.argtypes = [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]
     L.stts_msd_losses.restype = c_int
+    for fn in ("stts_conv1d_fwd_workspace_bytes", "stts_conv1d_bwd_workspace_bytes"):
+        getattr(L, fn).argtypes = [c_int] * 10
+        getattr(L, fn).restype = c_ll
+    L.stts_conv1d_fwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
+    L.stts_conv1d_fwd.restype = c_int
+    L.stts_conv1d_bwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]
+    L.stts_conv1d_bwd.restype = c_int
     L.stts_mrstft_workspace_bytes.argtypes = [c_int, c_ll, ctypes.POINTER(c_int), c_int, c_int]
     L.stts_mrstft_workspace_bytes.restype = c_ll
     L.stts_mrstft_loss.argtypes = [c_vp, c_vp, c_int, c_ll, c_ll, ctypes.POINTER(c_int), ctypes.POINTER(c_int),

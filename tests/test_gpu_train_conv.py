@@ -1,0 +1,98 @@
+"""Conv1d forward / backward of the training step (config 5) on the HIP path vs torch autograd.
+
+train.py:272-327 gets its conv gradients from torch autograd, so autograd (fp64 on the CPU) is the
+reference algorithm here; tolerances are relative to the gradient's max magnitude: fp32 1e-4,
+bf16 operands (forward and dx only; dw / db are fp32 in both modes) 2e-2.  The cases are the
+conv shapes of the decoder (Modules/hifigan.py) and the discriminators (discriminators.py)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# (B, Cin, Cout, K, stride, dil, pad, Lin)
+CASES = [
+    (2, 64, 64, 7, 1, 3, 9, 300),        # resblock conv, dilation 3
+    (1, 32, 32, 11, 1, 5, 25, 1000),     # last-stage resblock, dilation 5
+    (2, 1090, 1024, 3, 1, 1, 1, 40),     # decoder front-end AdainResBlk1d conv1
+    (3, 32, 1, 7, 1, 1, 3, 257),         # conv_post
+    (2, 1, 1, 3, 2, 1, 1, 80),           # F0_conv / N_conv (stride 2, one channel)
+    (2, 32, 128, 5, 3, 1, 2, 301),       # MPD (5, 1) conv, stride 3 along time
+    (1, 512, 256, 1, 1, 1, 0, 37),       # 1x1 shortcut
+    (2, 16, 48, 4, 2, 1, 1, 99),         # even kernel, stride 2, ragged length
+    (1, 64, 64, 7, 1, 5, 15, 48000),     # long rows: many wgrad slices
+]
+
+
+def _ref(x, w, b, stride, pad, dil, gy):
+    xd, wd, bd = (t.double().requires_grad_(True) for t in (x, w, b))
+    y = torch.nn.functional.conv1d(xd, wd, bd, stride=stride, padding=pad, dilation=dil)
+    y.backward(gy.double())
+    return y.detach(), xd.grad, wd.grad, bd.grad
+
+
+def _rel(a, ref):
+    a, ref = a.detach().double().cpu(), ref.detach().double().cpu()
+    return float((a - ref).abs().max() / max(ref.abs().max().item(), 1e-30))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_d{}_p{}_L{}".format(*c))
+def test_conv1d_fwd_bwd(case, dtype):
+    from stts2_mi355x.training import conv1d, out_length
+    B, Cin, Cout, K, stride, dil, pad, Lin = case
+    if dtype == "bf16" and Lin > 10000:
+        pytest.skip("fp32 covers the long case")
+    g = torch.Generator().manual_seed(hash(case) % 2**31)
+    x = torch.randn(B, Cin, Lin, generator=g)
+    w = torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)
+    b = torch.randn(Cout, generator=g)
+    Lq = out_length(Lin, K, stride, pad, dil)
+    gy = torch.randn(B, Cout, Lq, generator=g)
+    y_ref, dx_ref, dw_ref, db_ref = _ref(x, w, b, stride, pad, dil, gy)
+    xc, wc, bc = (t.cuda().requires_grad_(True) for t in (x, w, b))
+    y = conv1d(xc, wc, bc, stride, pad, dil, dtype=dtype)
+    assert y.shape == (B, Cout, Lq)
+    y.backward(gy.cuda())
+    tol = 1e-4 if dtype == "fp32" else 2e-2
+    errs = {"y": _rel(y, y_ref), "dx": _rel(xc.grad, dx_ref), "dw": _rel(wc.grad, dw_ref), "db": _rel(bc.grad, db_ref)}
+    print(case, dtype, {k: f"{v:.2e}" for k, v in errs.items()})
+    assert errs["y"] < tol and errs["dx"] < tol
+    assert errs["dw"] < 1e-4 and errs["db"] < 1e-5  # fp32 in both modes
+
+
+def test_conv1d_bwd_deterministic_and_partial_outputs():
+    """Fixed slice order: two backward passes agree bitwise; dw-only / dx-only calls give the same
+    values as the full call."""
+    from stts2_mi355x.training import conv1d
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 64, 3000, generator=g).cuda()
+    w = (torch.randn(64, 64, 3, generator=g) * 0.1).cuda()
+    gy = torch.randn(2, 64, 3000, generator=g).cuda()
+    outs = []
+    for _ in range(2):
+        xc, wc = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        conv1d(xc, wc, None, 1, 1, 1).backward(gy)
+        outs.append((xc.grad.clone(), wc.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    wc = w.clone().requires_grad_(True)
+    conv1d(x, wc, None, 1, 1, 1).backward(gy)  # x needs no grad: dx is not computed
+    assert torch.equal(wc.grad, outs[0][1])
+    xc = x.clone().requires_grad_(True)
+    conv1d(xc, w, None, 1, 1, 1).backward(gy)
+    assert torch.equal(xc.grad, outs[0][0])
+
+
+def test_conv1d_module_dropin():
+    """training.Conv1d loads an nn.Conv1d state dict and matches its forward and parameter grads."""
+    from stts2_mi355x.training import Conv1d
+    torch.manual_seed(3)
+    ref = torch.nn.Conv1d(48, 80, 5, stride=1, padding=4, dilation=2)
+    mod = Conv1d(48, 80, 5, stride=1, padding=4, dilation=2)
+    mod.load_state_dict(ref.state_dict())
+    x = torch.randn(2, 48, 200)
+    ref(x).square().mean().backward()
+    mod.cuda()
+    mod(x.cuda()).square().mean().backward()
+    assert _rel(mod.weight.grad, ref.weight.grad) < 1e-4
+    assert _rel(mod.bias.grad, ref.bias.grad) < 1e-4

@@ -1,0 +1,36 @@
+"""Host-side checks of the training-step conv ABI (no GPU): workspace queries validate the geometry
+(Lq must be the forward's output length; dilated strided convs are refused) and the drop-in module
+refuses what the HIP path does not run."""
+import pytest
+import torch
+
+from stts2_mi355x import engine as E
+from stts2_mi355x.training import Conv1d, out_length
+
+
+def test_workspace_queries_validate_geometry():
+    L = E.lib()
+    for fn in (L.stts_conv1d_fwd_workspace_bytes, L.stts_conv1d_bwd_workspace_bytes):
+        Lq = out_length(300, 7, 1, 9, 3)
+        assert fn(0, 2, 300, 64, 64, 7, 1, 3, 9, Lq) > 0
+        assert fn(1, 2, 300, 64, 64, 7, 1, 3, 9, Lq) > 0
+        assert fn(0, 2, 300, 64, 64, 7, 1, 3, 9, Lq + 1) == -1   # ST_EINVAL
+        assert fn(2, 2, 300, 64, 64, 7, 1, 3, 9, Lq) == -2       # ST_EDTYPE
+    Lq = out_length(100, 3, 2, 2, 2)
+    assert L.stts_conv1d_bwd_workspace_bytes(0, 1, 100, 8, 8, 3, 2, 2, 2, Lq) == -1  # stride 2 with dilation 2
+    assert L.stts_conv1d_fwd_workspace_bytes(0, 1, 100, 8, 8, 3, 2, 2, 2, Lq) > 0
+
+
+def test_module_refuses_groups_and_padding_modes():
+    with pytest.raises(NotImplementedError):
+        Conv1d(8, 8, 3, groups=2)
+    with pytest.raises(NotImplementedError):
+        Conv1d(8, 8, 3, padding=1, padding_mode="reflect")
+
+
+def test_forward_without_device_fails_loudly():
+    if torch.cuda.is_available():
+        pytest.skip("CPU-only check")
+    m = Conv1d(4, 4, 3, padding=1)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m(torch.randn(1, 4, 10))
