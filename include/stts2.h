@@ -154,6 +154,30 @@ int stts_conv1d_bwd(int dtype, const float* x, const float* w, const float* dy, 
                     int K, int stride, int dil, int pad, int Lq, float* dx, float* dw, float* db, void* workspace,
                     long long ws_bytes, void* stream);
 
+/* AdaIN1d + activation forward / backward (training step), <- Modules/hifigan.py:14-24 AdaIN1d followed by
+ * Snake (:68, AdaINResBlock1) or LeakyReLU(0.2) (:385-395, AdainResBlk1d):
+ *   z = (1 + gamma[b][c]) InstanceNorm(x)[b][t][c] + beta[b][c] (eps 1e-5, biased variance);
+ *   y = act(z), act 0 identity, 1 Snake z + sin^2(alpha_c z) / alpha_c, 2 LeakyReLU(0.2).
+ * x, y, dy, dx [B][L][C] fp32 frames; gb [B][2C] = fc(s) (gamma then beta, the reference's chunk order);
+ * alpha [C] (act 1); mean_rstd [B][C][2] is written by the forward and read by the backward.
+ * The backward writes dx (nullable), dgb [B][2C] (nullable) and dalpha [C] (act 1, nullable); its
+ * column sums are fp64 row-slice partials added in fixed order.  Workspace >= stts_adain_act_workspace_bytes. */
+long long stts_adain_act_workspace_bytes(int B, int L, int C);
+int stts_adain_act_fwd(const float* x, const float* gb, const float* alpha, int act, int B, int L, int C, float* y,
+                       float* mean_rstd, void* workspace, long long ws_bytes, void* stream);
+int stts_adain_act_bwd(const float* x, const float* gb, const float* alpha, int act, const float* mean_rstd,
+                       const float* dy, int B, int L, int C, float* dx, float* dgb, float* dalpha, void* workspace,
+                       long long ws_bytes, void* stream);
+/* nn.Linear (the AdaIN style projection fc, hifigan.py:18): h [B][N] = s [B][K] W^T + bias, W [N][K];
+ * backward ds [B][K], dW [N][K], db [N] (each nullable; fp64 sums). */
+int stts_linear_fwd(const float* s, const float* W, const float* bias, int B, int K, int N, float* h, void* stream);
+int stts_linear_bwd(const float* s, const float* W, const float* dh, int B, int K, int N, float* ds, float* dW,
+                    float* db, void* stream);
+/* weight_norm backward (the training step's convs are weight-normed, hifigan.py:26-80): for w = g v / ||v||
+ * per row of v [d0][inner]: dg [d0] = <dw, v> / ||v||, dv = (g / ||v||)(dw - v <dw, v> / ||v||^2). */
+int stts_weight_norm_bwd(const float* g, const float* v, const float* dw, int d0, int inner, float* dg, float* dv,
+                         void* stream);
+
 /* MultiResSpecDiscriminator forward, <- Modules/discriminators.py:47-63 SpecDiscriminator.forward for every
  * resolution (MultiResSpecDiscriminator.forward :80-94 calls it on y and y_hat: pass both as one batch).
  * wave [B][T] fp32.  out (fp32, >= stts_msd_out_elems) receives, resolution by resolution, the 5

@@ -77,6 +77,21 @@ def lib():
     L.stts_conv1d_fwd.restype = c_int
     L.stts_conv1d_bwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]
     L.stts_conv1d_bwd.restype = c_int
+    L.stts_weight_norm.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]
+    L.stts_weight_norm.restype = c_int
+    L.stts_adain_act_workspace_bytes.argtypes = [c_int, c_int, c_int]
+    L.stts_adain_act_workspace_bytes.restype = c_ll
+    L.stts_adain_act_fwd.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_ll, c_vp]
+    L.stts_adain_act_fwd.restype = c_int
+    L.stts_adain_act_bwd.argtypes = [c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                     c_vp, c_ll, c_vp]
+    L.stts_adain_act_bwd.restype = c_int
+    L.stts_linear_fwd.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp]
+    L.stts_linear_fwd.restype = c_int
+    L.stts_linear_bwd.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]
+    L.stts_linear_bwd.restype = c_int
+    L.stts_weight_norm_bwd.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp]
+    L.stts_weight_norm_bwd.restype = c_int
     L.stts_mrstft_workspace_bytes.argtypes = [c_int, c_ll, ctypes.POINTER(c_int), c_int, c_int]
     L.stts_mrstft_workspace_bytes.restype = c_ll
     L.stts_mrstft_loss.argtypes = [c_vp, c_vp, c_int, c_ll, c_ll, ctypes.POINTER(c_int), ctypes.POINTER(c_int),

@@ -1,4 +1,6 @@
-"""Training-step conv layers on the HIP path.
+"""Training-step layers on the HIP path: conv1d, AdaIN1d + Snake /
+LeakyReLU, the style Linear, weight norm, and the AdaINResBlock1 built from them, each a
+`torch.autograd.Function` whose forward and backward both run as HIP kernels behind the C-ABI.
 
 train.py:272-327 backpropagates the discriminator and generator losses through every nn.Conv1d of
 the decoder (Modules/hifigan.py) and the discriminators (Modules/discriminators.py).  `conv1d` is
@@ -24,10 +26,6 @@ def _ws(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
 
-def _frames(t: torch.Tensor) -> torch.Tensor:
-    return t.detach().to(torch.float32).transpose(1, 2).contiguous()
-
-
 def out_length(Lin: int, K: int, stride: int, pad: int, dil: int) -> int:
     return (Lin + 2 * pad - dil * (K - 1) - 1) // stride + 1
 
@@ -35,14 +33,15 @@ def out_length(Lin: int, K: int, stride: int, pad: int, dil: int) -> int:
 class _Conv1dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, stride, pad, dil, dtype):
+        """x: frames [B, Lin, Cin] -> y frames [B, Lq, Cout]"""
         _require_device()
-        B, Cin, Lin = x.shape
+        B, Lin, Cin = x.shape
         Cout, Cin_w, K = w.shape
         if Cin_w != Cin:
             raise ValueError(f"weight {tuple(w.shape)} does not take {Cin} input channels")
         Lq = out_length(Lin, K, stride, pad, dil)
         dt = _DT[dtype]
-        xf = _frames(x)
+        xf = x.detach().to(torch.float32).contiguous()
         wc = w.detach().to(torch.float32).contiguous()
         bc = bias.detach().to(torch.float32).contiguous() if bias is not None else None
         nb = lib().stts_conv1d_fwd_workspace_bytes(dt, B, Lin, Cin, Cout, K, stride, dil, pad, Lq)
@@ -53,14 +52,14 @@ class _Conv1dFn(torch.autograd.Function):
                                     _ptr(y), _ptr(ws), int(nb), _stream()), "stts_conv1d_fwd")
         ctx.save_for_backward(xf, wc)
         ctx.geo = (B, Lin, Cin, Cout, K, stride, dil, pad, Lq, dt, bias is not None)
-        return y.transpose(1, 2)
+        return y
 
     @staticmethod
     def backward(ctx, gy):
         xf, wc = ctx.saved_tensors
         B, Lin, Cin, Cout, K, stride, dil, pad, Lq, dt, has_bias = ctx.geo
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
-        dyf = _frames(gy)
+        dyf = gy.detach().to(torch.float32).contiguous()
         dev = dyf.device
         nb = lib().stts_conv1d_bwd_workspace_bytes(dt, B, Lin, Cin, Cout, K, stride, dil, pad, Lq)
         check(int(nb) if nb < 0 else 0, "stts_conv1d_bwd_workspace_bytes")
@@ -70,13 +69,20 @@ class _Conv1dFn(torch.autograd.Function):
         db = torch.empty(Cout, dtype=torch.float32, device=dev) if (need_b and has_bias) else None
         check(lib().stts_conv1d_bwd(dt, _ptr(xf), _ptr(wc), _ptr(dyf), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
                                     _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()), "stts_conv1d_bwd")
-        return (dx.transpose(1, 2) if dx is not None else None), dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
     """torch.nn.functional.conv1d (groups 1, zero padding) with forward and backward on the HIP
     conv engines.  dtype 'bf16' runs the forward and dx with bf16 operands (fp32 accumulation);
     dw / db are always fp32."""
+    if dtype not in _DT:
+        raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
+    return conv1d_frames(x.transpose(1, 2), weight, bias, stride, padding, dilation, dtype).transpose(1, 2)
+
+
+def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
+    """conv1d on frames tensors: x [B, Lin, Cin] -> [B, Lq, Cout] (the kernels' native layout)."""
     if dtype not in _DT:
         raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
     return _Conv1dFn.apply(x, weight, bias, int(stride), int(padding), int(dilation), dtype)
@@ -94,3 +100,166 @@ class Conv1d(nn.Conv1d):
     def forward(self, x):
         return conv1d(x, self.weight, self.bias, self.stride[0], self.padding[0], self.dilation[0],
                       self.dtype_compute)
+
+
+ACT_NONE, ACT_SNAKE, ACT_LRELU = 0, 1, 2
+
+
+def _c(t):
+    return t.detach().to(torch.float32).contiguous() if t is not None else None
+
+
+class _LinearFn(torch.autograd.Function):
+    """nn.Linear on the device (stts_linear_fwd / stts_linear_bwd): s [B, K], W [N, K] -> [B, N]."""
+
+    @staticmethod
+    def forward(ctx, s, W, b):
+        _require_device()
+        B, K = s.shape
+        N = W.shape[0]
+        sc, Wc, bc = _c(s), _c(W), _c(b)
+        h = torch.empty(B, N, dtype=torch.float32, device=s.device)
+        check(lib().stts_linear_fwd(_ptr(sc), _ptr(Wc), _ptr(bc), B, K, N, _ptr(h), _stream()), "stts_linear_fwd")
+        ctx.save_for_backward(sc, Wc)
+        ctx.has_b = b is not None
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        sc, Wc = ctx.saved_tensors
+        B, K = sc.shape
+        N = Wc.shape[0]
+        dh = _c(dh)
+        ns, nw, nb = ctx.needs_input_grad
+        ds = torch.empty_like(sc) if ns else None
+        dW = torch.empty_like(Wc) if nw else None
+        db = torch.empty(N, dtype=torch.float32, device=dh.device) if (nb and ctx.has_b) else None
+        check(lib().stts_linear_bwd(_ptr(sc), _ptr(Wc), _ptr(dh), B, K, N, _ptr(ds), _ptr(dW), _ptr(db), _stream()),
+              "stts_linear_bwd")
+        return ds, dW, db
+
+
+class _AdaINActFn(torch.autograd.Function):
+    """AdaIN1d (InstanceNorm + (1 + gamma), beta) + activation on frames [B, L, C]; gb [B, 2C]."""
+
+    @staticmethod
+    def forward(ctx, x, gb, alpha, act):
+        _require_device()
+        B, L, C = x.shape
+        xc, gbc, ac = _c(x), _c(gb), _c(alpha.reshape(-1)) if alpha is not None else None
+        nb = lib().stts_adain_act_workspace_bytes(B, L, C)
+        check(int(nb) if nb < 0 else 0, "stts_adain_act_workspace_bytes")
+        ws = _ws(nb, x.device)
+        y = torch.empty_like(xc)
+        mr = torch.empty(B, C, 2, dtype=torch.float32, device=x.device)
+        check(lib().stts_adain_act_fwd(_ptr(xc), _ptr(gbc), _ptr(ac), act, B, L, C, _ptr(y), _ptr(mr), _ptr(ws),
+                                       int(nb), _stream()), "stts_adain_act_fwd")
+        ctx.save_for_backward(xc, gbc, ac if ac is not None else xc.new_empty(0), mr)
+        ctx.act, ctx.alpha_shape = act, (alpha.shape if alpha is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, gbc, ac, mr = ctx.saved_tensors
+        act = ctx.act
+        B, L, C = xc.shape
+        dy = _c(dy)
+        nx, ngb, na = ctx.needs_input_grad[:3]
+        nb = lib().stts_adain_act_workspace_bytes(B, L, C)
+        ws = _ws(nb, dy.device)
+        dx = torch.empty_like(xc) if nx else None
+        dgb = torch.empty_like(gbc) if ngb else None
+        da = torch.empty(C, dtype=torch.float32, device=dy.device) if (na and act == ACT_SNAKE) else None
+        check(lib().stts_adain_act_bwd(_ptr(xc), _ptr(gbc), _ptr(ac if act == ACT_SNAKE else None), act, _ptr(mr),
+                                       _ptr(dy), B, L, C, _ptr(dx), _ptr(dgb), _ptr(da), _ptr(ws), int(nb),
+                                       _stream()), "stts_adain_act_bwd")
+        return dx, dgb, (da.reshape(ctx.alpha_shape) if da is not None else None), None
+
+
+class _WeightNormFn(torch.autograd.Function):
+    """w = g v / ||v|| (norm over all dims but 0): stts_weight_norm / stts_weight_norm_bwd."""
+
+    @staticmethod
+    def forward(ctx, g, v):
+        _require_device()
+        gc, vc = _c(g), _c(v)
+        d0 = vc.shape[0]
+        w = torch.empty_like(vc)
+        check(lib().stts_weight_norm(_ptr(gc), _ptr(vc), d0, vc.numel() // d0, _ptr(w), _stream()),
+              "stts_weight_norm")
+        ctx.save_for_backward(gc, vc)
+        ctx.g_shape = g.shape
+        return w
+
+    @staticmethod
+    def backward(ctx, dw):
+        gc, vc = ctx.saved_tensors
+        d0 = vc.shape[0]
+        dw = _c(dw)
+        dg = torch.empty(d0, dtype=torch.float32, device=dw.device)
+        dv = torch.empty_like(vc)
+        check(lib().stts_weight_norm_bwd(_ptr(gc), _ptr(vc), _ptr(dw), d0, vc.numel() // d0, _ptr(dg), _ptr(dv),
+                                         _stream()), "stts_weight_norm_bwd")
+        return dg.reshape(ctx.g_shape), dv
+
+
+def linear(s, W, b=None):
+    return _LinearFn.apply(s, W, b)
+
+
+def adain_act(x, s, fc_weight, fc_bias, alpha=None, act=ACT_NONE):
+    """AdaIN1d(style) on frames x [B, L, C] followed by `act` (Snake needs alpha [C] or [1, C, 1])."""
+    return _AdaINActFn.apply(x, linear(s, fc_weight, fc_bias), alpha, int(act))
+
+
+def weight_norm(g, v):
+    return _WeightNormFn.apply(g, v)
+
+
+class _WNConv(nn.Module):
+    """weight_norm(nn.Conv1d) parameter layout (weight_g [Cout, 1, 1], weight_v, bias)."""
+
+    def __init__(self, cin, cout, k, dilation=1, padding=0):
+        super().__init__()
+        self.weight_g = nn.Parameter(torch.ones(cout, 1, 1))
+        self.weight_v = nn.Parameter(torch.randn(cout, cin, k) * 0.02)
+        self.bias = nn.Parameter(torch.zeros(cout))
+        self.dilation, self.padding = dilation, padding
+
+
+class _AdaIN(nn.Module):
+    def __init__(self, style_dim, C):
+        super().__init__()
+        self.fc = nn.Linear(style_dim, 2 * C)
+
+
+class AdaINResBlock1(nn.Module):
+    """Trainable Modules/hifigan.py:26-80 AdaINResBlock1 (same parameter names: convs1/convs2 weight-normed,
+    adain1/adain2 .fc, alpha1/alpha2), forward and backward on the HIP kernels:
+    for each dilation d: xt = Snake(AdaIN1(x)); xt = convs1(xt); xt = Snake(AdaIN2(xt)); xt = convs2(xt);
+    x = xt + x.  `forward(x, s)` takes x [B, C, L]; `forward_frames(x, s)` frames [B, L, C]."""
+
+    def __init__(self, channels, kernel_size=3, dilation=(1, 3, 5), style_dim=64):
+        super().__init__()
+        self.kernel_size, self.dilation = kernel_size, tuple(dilation)
+        self.convs1 = nn.ModuleList([_WNConv(channels, channels, kernel_size, d, (kernel_size * d - d) // 2)
+                                     for d in dilation])
+        self.convs2 = nn.ModuleList([_WNConv(channels, channels, kernel_size, 1, (kernel_size - 1) // 2)
+                                     for _ in dilation])
+        self.adain1 = nn.ModuleList([_AdaIN(style_dim, channels) for _ in dilation])
+        self.adain2 = nn.ModuleList([_AdaIN(style_dim, channels) for _ in dilation])
+        self.alpha1 = nn.ParameterList([nn.Parameter(torch.ones(1, channels, 1)) for _ in dilation])
+        self.alpha2 = nn.ParameterList([nn.Parameter(torch.ones(1, channels, 1)) for _ in dilation])
+
+    def forward_frames(self, x, s):
+        for c1, c2, n1, n2, a1, a2 in zip(self.convs1, self.convs2, self.adain1, self.adain2, self.alpha1,
+                                          self.alpha2):
+            xt = adain_act(x, s, n1.fc.weight, n1.fc.bias, a1, ACT_SNAKE)
+            xt = conv1d_frames(xt, weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, c1.padding, c1.dilation)
+            xt = adain_act(xt, s, n2.fc.weight, n2.fc.bias, a2, ACT_SNAKE)
+            xt = conv1d_frames(xt, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, c2.padding, c2.dilation)
+            x = xt + x
+        return x
+
+    def forward(self, x, s):
+        return self.forward_frames(x.transpose(1, 2), s).transpose(1, 2)

@@ -1,0 +1,105 @@
+"""AdaIN1d + activation, the style Linear, weight norm and a whole AdaINResBlock1 — forward and
+backward on the HIP path — against autograd through the oracle's restatement of the reference
+(oracle/stts_oracle.py adain1d / snake / adain_resblock1, fp64 on the CPU).  train.py gets these
+gradients from torch autograd, so autograd over the reference algorithm is the reference here.
+Tolerance: max |error| <= 1e-4 (layers) / 2e-4 (the six-layer resblock) of the max |reference|."""
+import sys
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import stts_oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, ref):
+    a, ref = a.detach().double().cpu(), ref.detach().double().cpu()
+    return float((a - ref).abs().max() / max(ref.abs().max().item(), 1e-30))
+
+
+@pytest.mark.parametrize("act", [0, 1, 2], ids=["none", "snake", "lrelu"])
+@pytest.mark.parametrize("B,C,L", [(2, 64, 300), (3, 100, 77), (1, 512, 4000)])
+def test_adain_act(B, C, L, act):
+    from stts2_mi355x.training import adain_act
+    g = torch.Generator().manual_seed(B * 1000 + C + act)
+    S = 128
+    x = torch.randn(B, C, L, generator=g) * 2 + 0.5
+    s = torch.randn(B, S, generator=g)
+    W = torch.randn(2 * C, S, generator=g) * 0.05
+    bfc = torch.randn(2 * C, generator=g) * 0.1
+    alpha = 0.5 + torch.rand(1, C, 1, generator=g)
+    R = torch.randn(B, C, L, generator=g)
+    # reference (fp64): AdaIN1d then the activation
+    ref = [t.double().requires_grad_(True) for t in (x, s, W, bfc, alpha)]
+    xr, sr, Wr, br, ar = ref
+    z = O.adain1d(xr, sr, {"n.fc.weight": Wr, "n.fc.bias": br}, "n")
+    y_ref = O.snake(z, ar) if act == 1 else (F.leaky_relu(z, 0.2) if act == 2 else z)
+    (y_ref * R.double()).sum().backward()
+    dev = [t.cuda().requires_grad_(True) for t in (x, s, W, bfc, alpha)]
+    xd, sd, Wd, bd, ad = dev
+    y = adain_act(xd.transpose(1, 2), sd, Wd, bd, ad if act == 1 else None, act).transpose(1, 2)
+    (y * R.cuda()).sum().backward()
+    errs = {"y": _rel(y, y_ref), "dx": _rel(xd.grad, xr.grad), "ds": _rel(sd.grad, sr.grad),
+            "dW": _rel(Wd.grad, Wr.grad), "db": _rel(bd.grad, br.grad)}
+    if act == 1:
+        errs["dalpha"] = _rel(ad.grad, ar.grad)
+    print((B, C, L, act), {k: f"{v:.1e}" for k, v in errs.items()})
+    for k, v in errs.items():
+        assert v < 1e-4, (k, v)
+
+
+def test_weight_norm_grad():
+    from stts2_mi355x.training import weight_norm
+    g0 = torch.Generator().manual_seed(1)
+    gg = torch.rand(96, 1, 1, generator=g0) + 0.5
+    v = torch.randn(96, 64, 7, generator=g0)
+    R = torch.randn(96, 64, 7, generator=g0)
+    gr, vr = gg.double().requires_grad_(True), v.double().requires_grad_(True)
+    (torch._weight_norm(vr, gr, 0) * R.double()).sum().backward()
+    gd, vd = gg.cuda().requires_grad_(True), v.cuda().requires_grad_(True)
+    w = weight_norm(gd, vd)
+    (w * R.cuda()).sum().backward()
+    assert _rel(w, torch._weight_norm(v.double(), gg.double(), 0)) < 1e-5
+    assert _rel(gd.grad, gr.grad) < 1e-5 and _rel(vd.grad, vr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("C,K,L", [(64, 7, 500), (32, 11, 1200), (128, 3, 300)])
+def test_adain_resblock1_fwd_bwd(C, K, L):
+    """One AdaINResBlock1 (dilations 1, 3, 5) end to end: output and every gradient (x, s and all 24
+    parameters) against autograd through oracle.adain_resblock1 in fp64."""
+    from stts2_mi355x.training import AdaINResBlock1
+    torch.manual_seed(C + K)
+    B, S = 2, 128
+    mod = AdaINResBlock1(C, K, (1, 3, 5), S)
+    with torch.no_grad():
+        for n, p in mod.named_parameters():
+            if "alpha" in n:
+                p.uniform_(0.6, 1.4)
+            elif "weight_g" in n:
+                p.uniform_(0.5, 1.5)
+            elif n.endswith("bias"):
+                p.normal_(0, 0.1)
+            else:
+                p.normal_(0, 0.05)
+    x = torch.randn(B, C, L)
+    s = torch.randn(B, S)
+    R = torch.randn(B, C, L)
+    sd = {"rb." + k: v.detach().double().requires_grad_(True) for k, v in mod.state_dict().items()}
+    xr, sr = x.double().requires_grad_(True), s.double().requires_grad_(True)
+    y_ref = O.adain_resblock1(xr, sr, sd, "rb", K, (1, 3, 5))
+    (y_ref * R.double()).sum().backward()
+    mod.cuda()
+    xd, sdv = x.cuda().requires_grad_(True), s.cuda().requires_grad_(True)
+    y = mod(xd, sdv)
+    (y * R.cuda()).sum().backward()
+    errs = {"y": _rel(y, y_ref), "dx": _rel(xd.grad, xr.grad), "ds": _rel(sdv.grad, sr.grad)}
+    for n, p in mod.named_parameters():
+        errs[n] = _rel(p.grad, sd["rb." + n].grad)
+    worst = max(errs, key=errs.get)
+    print((C, K, L), "worst", worst, f"{errs[worst]:.2e}", "y", f"{errs['y']:.1e}", "dx", f"{errs['dx']:.1e}")
+    for k, v in errs.items():
+        assert v < 2e-4, (k, v)

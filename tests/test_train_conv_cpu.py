@@ -34,3 +34,21 @@ def test_forward_without_device_fails_loudly():
     m = Conv1d(4, 4, 3, padding=1)
     with pytest.raises(RuntimeError, match="HIP device"):
         m(torch.randn(1, 4, 10))
+
+
+def test_training_resblock_matches_reference_layout():
+    """training.AdaINResBlock1 has the reference AdaINResBlock1's state-dict keys and shapes (the
+    inference-side params.AdaINResBlock1 is pinned to the reference names by test_native_abi)."""
+    from stts2_mi355x.params import AdaINResBlock1 as Ref
+    from stts2_mi355x.training import AdaINResBlock1
+    a = AdaINResBlock1(64, 7, (1, 3, 5), 128).state_dict()
+    b = Ref(64, 7, (1, 3, 5), 128).state_dict()
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert a[k].shape == b[k].shape, k
+
+
+def test_layer_workspace_queries():
+    L = E.lib()
+    assert L.stts_adain_act_workspace_bytes(2, 300, 64) > 0
+    assert L.stts_adain_act_workspace_bytes(0, 300, 64) == -1
