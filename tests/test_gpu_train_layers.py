@@ -3,8 +3,9 @@ backward on the HIP path — against autograd through the oracle's restatement o
 (oracle/stts_oracle.py adain1d / snake / adain_resblock1, fp64 on the CPU).  train.py gets these
 gradients from torch autograd, so autograd over the reference algorithm is the reference here.
 Tolerance: max |error| <= 1e-4 (layers) / 2e-4 (the six-layer resblock) of the max |reference|."""
-import sys
 import os
+import re
+import sys
 
 import pytest
 import torch
@@ -97,8 +98,24 @@ def test_adain_resblock1_fwd_bwd(C, K, L):
     y = mod(xd, sdv)
     (y * R.cuda()).sum().backward()
     errs = {"y": _rel(y, y_ref), "dx": _rel(xd.grad, xr.grad), "ds": _rel(sdv.grad, sr.grad)}
+    # convs1's output feeds adain2's InstanceNorm, which cancels a per-channel shift exactly and a
+    # per-channel scale up to eps: the true gradient of convs1's bias is 0 and that of weight_g
+    # nearly so, a difference of nearly equal dot products.  They are checked against their natural
+    # scale instead of their own size: the bias against the largest gradient, weight_g (= <dw, v/|v|>)
+    # against max |dw| = max |dv| |v| / g over the rows.
+    scale = max(sd["rb." + n].grad.abs().max().item() for n, _ in mod.named_parameters())
     for n, p in mod.named_parameters():
-        errs[n] = _rel(p.grad, sd["rb." + n].grad)
+        ref = sd["rb." + n].grad
+        if re.match(r"convs1\.\d+\.bias$", n):
+            assert p.grad.abs().max().item() < 1e-5 * scale, n
+            continue
+        if re.match(r"convs1\.\d+\.weight_g$", n):
+            pre = n[: -len("weight_g")]
+            v, g, dv = sd["rb." + pre + "weight_v"], sd["rb." + n], sd["rb." + pre + "weight_v"].grad
+            dw_scale = (dv.flatten(1).norm(dim=1) * v.detach().flatten(1).norm(dim=1) / g.detach().flatten()).max()
+            errs[n] = float((p.grad.detach().double().cpu() - ref).abs().max() / dw_scale)
+            continue
+        errs[n] = _rel(p.grad, ref)
     worst = max(errs, key=errs.get)
     print((C, K, L), "worst", worst, f"{errs[worst]:.2e}", "y", f"{errs['y']:.1e}", "dx", f"{errs['dx']:.1e}")
     for k, v in errs.items():

@@ -59,5 +59,37 @@ def main():
             print(json.dumps(res), flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--resblocks" not in sys.argv:
     main()
+
+
+def bench_resblocks():
+    """Forward + backward of one trainable AdaINResBlock1 (dilations 1, 3, 5) at config 5's stage shapes."""
+    from stts2_mi355x.training import AdaINResBlock1
+    for C, K, L in ((256, 3, 3100), (128, 7, 18600), (64, 11, 93000)):
+        torch.manual_seed(0)
+        mod = AdaINResBlock1(C, K, (1, 3, 5), 128).cuda()
+        x = torch.randn(2, C, L, device="cuda", requires_grad=True)
+        s = torch.randn(2, 128, device="cuda")
+        R = torch.randn(2, C, L, device="cuda")
+
+        def step():
+            mod.zero_grad(set_to_none=True)
+            x.grad = None
+            (mod(x, s) * R).sum().backward()
+        for _ in range(2):
+            step()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(5):
+            step()
+        b.record()
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / 5
+        flops = 3 * 2 * (2.0 * 2 * L * C * C * K)  # 6 convs: fwd + dx + dw
+        print(json.dumps({"resblock": f"C{C}_K{K}_L{L}_B2", "fwd_bwd_ms": round(ms, 3),
+                          "conv_tflops": round(flops / ms / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__" and "--resblocks" in sys.argv:
+    bench_resblocks()
