@@ -108,8 +108,18 @@ __global__ void k_slice_reduce(const float* __restrict__ part, int S, int K, int
   const int ci = (int)(i % Cin);
   const int co = (int)((i / Cin) % Cout);
   const int t = (int)(i / ((size_t)Cin * Cout));
+  // eight independent loads in flight, added in slice order (the latency, not the bytes, bounds
+  // a one-load-at-a-time loop)
   double sum = 0.0;
-  for (int s = 0; s < S; ++s) sum += part[s * per + i];
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = part[(size_t)(s + k) * per + i];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += v[k];
+  }
+  for (; s < S; ++s) sum += part[(size_t)s * per + i];
   out[((size_t)co * Cin + ci) * K + t] = (float)sum;
 }
 
@@ -241,14 +251,17 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
 // weight [Cout][Cin][K]; wm says how the engine's weight derives from it (W_PLAIN: as is, W_FLIP:
 // channel-transposed and tap-reversed, W_TRANS: as a ConvTranspose1d weight [in][out][K]).
 int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* w, const float* bias, float* y,
-               char* ws, hipStream_t s) {
+               char* ws, hipStream_t s, const float* res = nullptr) {
   const EngineGeo e = engine_geo(g, fwd);
   const WsLayout L = ws_layout(g, dtype, fwd);
   const int K = g.K, B = g.B;
   const int ldx = ldpad(e.ci);
   void* xd = ws + L.xin;
   void* wd = ws + L.packed;
-  ST_CHECK(st_frames_convert(xf, B, e.Lin, e.ci, e.ci, xd, ldx, nullptr, 0, dtype, s));
+  if (dtype == ST_FP32 && ldx == e.ci)
+    xd = (void*)xf;  // fp32 frames with 8-aligned rows are the engine's input as they are
+  else
+    ST_CHECK(st_frames_convert(xf, B, e.Lin, e.ci, e.ci, xd, ldx, nullptr, 0, dtype, s));
   const float* wsrc = w;
   if (e.wm != W_PLAIN || e.co_p != e.co) {
     float* wt = (float*)(ws + L.wstage);
@@ -316,6 +329,12 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   p.y_bs = (long long)e.Lout * e.co_p;
   p.y_ld = e.co_p;
   p.out_scale = 1.f;
+  if (res) {  // y = conv + res (fp32 frames [B][Lout][co], the same layout as y)
+    if (dtype != ST_FP32 || e.co_p != e.co) return ST_EINVAL;
+    p.res = res;
+    p.res_bs = (long long)e.Lout * e.co;
+    p.res_ld = e.co;
+  }
   ST_CHECK(st_conv1d(p, dtype, s));
   if (!direct) ST_CHECK(st_frames_to_f32(yd, B, e.Lout, e.co, e.co_p, y, dtype, s));
   return 0;
@@ -336,6 +355,17 @@ extern "C" long long stts_conv1d_fwd_workspace_bytes(int dtype, int B, int Lin, 
   const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
   if (!geo_ok(g)) return ST_EINVAL;
   return (long long)ws_layout(g, dtype, true).total;
+}
+
+extern "C" int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, const float* bias, const float* res,
+                                   int B, int Lin, int Cin, int Cout, int K, int stride, int dil, int pad, int Lq,
+                                   float* y, void* workspace, long long ws_bytes, void* stream) {
+  const long long need = stts_conv1d_fwd_workspace_bytes(dtype, B, Lin, Cin, Cout, K, stride, dil, pad, Lq);
+  if (need < 0) return (int)need;
+  if (!x || !w || !y) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
+  return run_engine(dtype, g, true, x, w, bias, y, (char*)workspace, (hipStream_t)stream, res);
 }
 
 extern "C" int stts_conv1d_fwd(int dtype, const float* x, const float* w, const float* bias, int B, int Lin, int Cin,

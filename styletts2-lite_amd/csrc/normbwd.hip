@@ -76,21 +76,32 @@ __global__ __launch_bounds__(256) void k_stats_part(const float* __restrict__ x,
   }
 }
 
-// mean / rstd per (b, c): mr[(b*C + c)*2 + {0, 1}]
-__global__ void k_stats_final(const double* __restrict__ part, int B, int L, int C, int S, float* __restrict__ mr) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * C) return;
+__device__ __forceinline__ double wave_sum(double v) {
+  // fixed butterfly: lane 0's result has the same association order on every run
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// mean / rstd per (b, c): mr[(b*C + c)*2 + {0, 1}]; one wave per (b, c), lanes stride the slices
+__global__ __launch_bounds__(64) void k_stats_final(const double* __restrict__ part, int L, int C, int S,
+                                                    float* __restrict__ mr) {
+  const int i = blockIdx.x;
   const int b = i / C, c = i % C;
   double s1 = 0.0, s2 = 0.0;
-  for (int s = 0; s < S; ++s) {
+  for (int s = threadIdx.x; s < S; s += 64) {
     const double* p = part + (((size_t)b * S + s) * C + c) * 2;
     s1 += p[0];
     s2 += p[1];
   }
-  const double mean = s1 / L;
-  const double var = std::max(s2 / L - mean * mean, 0.0);
-  mr[2 * i] = (float)mean;
-  mr[2 * i + 1] = (float)(1.0 / sqrt(var + kEps));
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (threadIdx.x == 0) {
+    const double mean = s1 / L;
+    const double var = fmax(s2 / L - mean * mean, 0.0);
+    mr[2 * i] = (float)mean;
+    mr[2 * i + 1] = (float)(1.0 / sqrt(var + kEps));
+  }
 }
 
 __global__ void k_adain_act_fwd(const float* __restrict__ x, const float* __restrict__ gb,
@@ -163,28 +174,34 @@ __global__ __launch_bounds__(256) void k_adain_bwd_part(const float* __restrict_
   }
 }
 
-// per channel c: dgb[b][c] = dgamma, dgb[b][C + c] = dbeta (and the fp64 sums for dx), dalpha[c]
-__global__ void k_adain_bwd_final(const double* __restrict__ part, int B, int C, int S, float* __restrict__ dgb,
-                                  double* __restrict__ sums, float* __restrict__ dalpha) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// per channel c (one wave; lanes stride the slices): dgb[b][c] = dgamma, dgb[b][C + c] = dbeta (and the
+// fp64 sums for dx), dalpha[c] summed over utterances in order
+__global__ __launch_bounds__(64) void k_adain_bwd_final(const double* __restrict__ part, int B, int C, int S,
+                                                        float* __restrict__ dgb, double* __restrict__ sums,
+                                                        float* __restrict__ dalpha) {
+  const int c = blockIdx.x;
   double da = 0.0;
   for (int b = 0; b < B; ++b) {
-    double s1 = 0.0, s2 = 0.0;
-    for (int s = 0; s < S; ++s) {
+    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    for (int s = threadIdx.x; s < S; s += 64) {
       const double* p = part + (((size_t)b * S + s) * C + c) * 3;
       s1 += p[0];
       s2 += p[1];
-      da += p[2];
+      s3 += p[2];
     }
-    sums[((size_t)b * C + c) * 2] = s1;
-    sums[((size_t)b * C + c) * 2 + 1] = s2;
-    if (dgb) {
-      dgb[(size_t)b * 2 * C + c] = (float)s2;
-      dgb[(size_t)b * 2 * C + C + c] = (float)s1;
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    da += wave_sum(s3);
+    if (threadIdx.x == 0) {
+      sums[((size_t)b * C + c) * 2] = s1;
+      sums[((size_t)b * C + c) * 2 + 1] = s2;
+      if (dgb) {
+        dgb[(size_t)b * 2 * C + c] = (float)s2;
+        dgb[(size_t)b * 2 * C + C + c] = (float)s1;
+      }
     }
   }
-  if (dalpha) dalpha[c] = (float)da;
+  if (dalpha && threadIdx.x == 0) dalpha[c] = (float)da;
 }
 
 __global__ void k_adain_bwd_dx(const float* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ gb,
@@ -293,7 +310,7 @@ extern "C" int stts_adain_act_fwd(const float* x, const float* gb, const float* 
   double* part = (double*)ws;
   hipLaunchKernelGGL(k_stats_part, dim3((C + 63) / 64, cl.S, B), dim3(256), 0, s, x, L, C, cl.S, part);
   ST_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_stats_final, dim3((B * C + 255) / 256), dim3(256), 0, s, part, B, L, C, cl.S, mean_rstd);
+  hipLaunchKernelGGL(k_stats_final, dim3(B * C), dim3(64), 0, s, part, L, C, cl.S, mean_rstd);
   ST_CHECK_HIP(hipGetLastError());
   const long long n = (long long)B * L * C;
   hipLaunchKernelGGL(k_adain_act_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, gb, alpha, mean_rstd, L,
@@ -315,7 +332,7 @@ extern "C" int stts_adain_act_bwd(const float* x, const float* gb, const float* 
   hipLaunchKernelGGL(k_adain_bwd_part, dim3((C + 63) / 64, cl.S, B), dim3(256), 0, s, x, dy, gb, alpha, mean_rstd, L,
                      C, cl.S, act, part);
   ST_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_adain_bwd_final, dim3((C + 255) / 256), dim3(256), 0, s, part, B, C, cl.S, dgb, sums,
+  hipLaunchKernelGGL(k_adain_bwd_final, dim3(C), dim3(64), 0, s, part, B, C, cl.S, dgb, sums,
                      act == 1 ? dalpha : nullptr);
   ST_CHECK_HIP(hipGetLastError());
   if (dx) {

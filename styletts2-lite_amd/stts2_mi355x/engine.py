@@ -75,6 +75,8 @@ def lib():
         getattr(L, fn).restype = c_ll
     L.stts_conv1d_fwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
     L.stts_conv1d_fwd.restype = c_int
+    L.stts_conv1d_fwd_res.argtypes = [c_int, c_vp, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
+    L.stts_conv1d_fwd_res.restype = c_int
     L.stts_conv1d_bwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]
     L.stts_conv1d_bwd.restype = c_int
     L.stts_weight_norm.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]

@@ -32,8 +32,8 @@ def out_length(Lin: int, K: int, stride: int, pad: int, dil: int) -> int:
 
 class _Conv1dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, dil, dtype):
-        """x: frames [B, Lin, Cin] -> y frames [B, Lq, Cout]"""
+    def forward(ctx, x, w, bias, stride, pad, dil, dtype, res=None):
+        """x: frames [B, Lin, Cin] -> y frames [B, Lq, Cout] (+ res, fp32 frames [B, Lq, Cout])"""
         _require_device()
         B, Lin, Cin = x.shape
         Cout, Cin_w, K = w.shape
@@ -48,8 +48,14 @@ class _Conv1dFn(torch.autograd.Function):
         check(int(nb) if nb < 0 else 0, "stts_conv1d_fwd_workspace_bytes")
         ws = _ws(nb, x.device)
         y = torch.empty(B, Lq, Cout, dtype=torch.float32, device=x.device)
-        check(lib().stts_conv1d_fwd(dt, _ptr(xf), _ptr(wc), _ptr(bc), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
-                                    _ptr(y), _ptr(ws), int(nb), _stream()), "stts_conv1d_fwd")
+        if res is not None:
+            rc = res.detach().to(torch.float32).contiguous()
+            check(lib().stts_conv1d_fwd_res(dt, _ptr(xf), _ptr(wc), _ptr(bc), _ptr(rc), B, Lin, Cin, Cout, K, stride,
+                                            dil, pad, Lq, _ptr(y), _ptr(ws), int(nb), _stream()),
+                  "stts_conv1d_fwd_res")
+        else:
+            check(lib().stts_conv1d_fwd(dt, _ptr(xf), _ptr(wc), _ptr(bc), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
+                                        _ptr(y), _ptr(ws), int(nb), _stream()), "stts_conv1d_fwd")
         ctx.save_for_backward(xf, wc)
         ctx.geo = (B, Lin, Cin, Cout, K, stride, dil, pad, Lq, dt, bias is not None)
         return y
@@ -69,7 +75,7 @@ class _Conv1dFn(torch.autograd.Function):
         db = torch.empty(Cout, dtype=torch.float32, device=dev) if (need_b and has_bias) else None
         check(lib().stts_conv1d_bwd(dt, _ptr(xf), _ptr(wc), _ptr(dyf), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
                                     _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()), "stts_conv1d_bwd")
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, (gy if ctx.needs_input_grad[7] else None)
 
 
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
@@ -81,11 +87,12 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
     return conv1d_frames(x.transpose(1, 2), weight, bias, stride, padding, dilation, dtype).transpose(1, 2)
 
 
-def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
-    """conv1d on frames tensors: x [B, Lin, Cin] -> [B, Lq, Cout] (the kernels' native layout)."""
+def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32", residual=None):
+    """conv1d on frames tensors: x [B, Lin, Cin] -> [B, Lq, Cout] (the kernels' native layout);
+    `residual` (frames [B, Lq, Cout], fp32 runs) is added in the conv epilogue."""
     if dtype not in _DT:
         raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
-    return _Conv1dFn.apply(x, weight, bias, int(stride), int(padding), int(dilation), dtype)
+    return _Conv1dFn.apply(x, weight, bias, int(stride), int(padding), int(dilation), dtype, residual)
 
 
 class Conv1d(nn.Conv1d):
@@ -257,8 +264,8 @@ class AdaINResBlock1(nn.Module):
             xt = adain_act(x, s, n1.fc.weight, n1.fc.bias, a1, ACT_SNAKE)
             xt = conv1d_frames(xt, weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, c1.padding, c1.dilation)
             xt = adain_act(xt, s, n2.fc.weight, n2.fc.bias, a2, ACT_SNAKE)
-            xt = conv1d_frames(xt, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, c2.padding, c2.dilation)
-            x = xt + x
+            x = conv1d_frames(xt, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, c2.padding, c2.dilation,
+                              residual=x)  # x = xt + x in convs2's epilogue
         return x
 
     def forward(self, x, s):
