@@ -160,6 +160,21 @@ int stts_conv1d_bwd(int dtype, const float* x, const float* w, const float* dy, 
                     int K, int stride, int dil, int pad, int Lq, float* dx, float* dw, float* db, void* workspace,
                     long long ws_bytes, void* stream);
 
+/* ConvTranspose1d forward / backward (the generator's weight-normed upsamplers, hifigan.py:292-294 /
+ * 427-432, trained by train.py's backward): y = conv_transpose1d(x, w, bias, stride, padding=pad,
+ * output_padding = Lout - ((Lin - 1) stride - 2 pad + K)), x / dx [B][Lin][Cin], y / dy [B][Lout][Cout],
+ * w / dw [Cin][Cout][K] (the nn.ConvTranspose1d layout), groups 1, dilation 1.  It is the dx of the
+ * conv1d Cout -> Cin with the same weight, so it runs on that path; its backward is that conv's
+ * forward (dx) and wgrad with the operands' roles swapped (dw, fp32), db = column sums of dy. */
+long long stts_conv_transpose1d_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride,
+                                                int pad, int Lout);
+int stts_conv_transpose1d_fwd(int dtype, const float* x, const float* w, const float* bias, int B, int Lin, int Cin,
+                              int Cout, int K, int stride, int pad, int Lout, float* y, void* workspace,
+                              long long ws_bytes, void* stream);
+int stts_conv_transpose1d_bwd(int dtype, const float* x, const float* w, const float* dy, int B, int Lin, int Cin,
+                              int Cout, int K, int stride, int pad, int Lout, float* dx, float* dw, float* db,
+                              void* workspace, long long ws_bytes, void* stream);
+
 /* AdaIN1d + activation forward / backward (training step), <- Modules/hifigan.py:14-24 AdaIN1d followed by
  * Snake (:68, AdaINResBlock1) or LeakyReLU(0.2) (:385-395, AdainResBlk1d):
  *   z = (1 + gamma[b][c]) InstanceNorm(x)[b][t][c] + beta[b][c] (eps 1e-5, biased variance);

@@ -188,6 +188,13 @@ Slices slices_of(const Geo& g) {
   return sl;
 }
 
+int colsum_slices(int C, long long R) {
+  const int cblk = (C + 63) / 64;
+  long long S2 = (512 + cblk - 1) / cblk;
+  S2 = std::min<long long>(S2, std::max<long long>(1, R / 256));
+  return (int)std::max<long long>(1, std::min<long long>(S2, 1024));
+}
+
 // workspace pieces (bytes, each 256-aligned)
 struct WsLayout {
   size_t xin, wstage, bpad, packed, yout, part, part2, total;
@@ -425,6 +432,82 @@ extern "C" int stts_conv1d_bwd(int dtype, const float* x, const float* w, const 
     ST_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, part2, sl.S2, 1, Cout,
                        1, db);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+// ConvTranspose1d(Cin_T -> Cout_T, K, stride, pad, output_padding implied by Lout) is the dx of the
+// conv1d (Cout_T -> Cin_T) with the same weight; its backward is that conv's forward (dx) and wgrad
+// with the operands' roles swapped (dw).  gc = the conv's geometry.
+namespace {
+Geo convT_geo(int B, int Lin, int Cin, int Cout, int K, int stride, int pad, int Lout) {
+  return Geo{B, Lout, Cout, Cin, K, stride, 1, pad, Lin};
+}
+size_t convT_ws(const Geo& gc, int dtype) {
+  const size_t a = ws_layout(gc, dtype, false).total, b = ws_layout(gc, dtype, true).total;
+  const int S2 = colsum_slices(gc.Cin, (long long)gc.B * gc.Lin);
+  return std::max(a, b) + al((size_t)S2 * gc.Cin * 4);
+}
+}  // namespace
+
+extern "C" long long stts_conv_transpose1d_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K,
+                                                           int stride, int pad, int Lout) {
+  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  const Geo gc = convT_geo(B, Lin, Cin, Cout, K, stride, pad, Lout);
+  if (!geo_ok(gc)) return ST_EINVAL;
+  if (stride == 1 && K - 1 < pad) return ST_EINVAL;
+  return (long long)convT_ws(gc, dtype);
+}
+
+extern "C" int stts_conv_transpose1d_fwd(int dtype, const float* x, const float* w, const float* bias, int B, int Lin,
+                                         int Cin, int Cout, int K, int stride, int pad, int Lout, float* y,
+                                         void* workspace, long long ws_bytes, void* stream) {
+  const long long need = stts_conv_transpose1d_workspace_bytes(dtype, B, Lin, Cin, Cout, K, stride, pad, Lout);
+  if (need < 0) return (int)need;
+  if (!x || !w || !y) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  const Geo gc = convT_geo(B, Lin, Cin, Cout, K, stride, pad, Lout);
+  return run_engine(dtype, gc, false, x, w, bias, y, (char*)workspace, (hipStream_t)stream);
+}
+
+extern "C" int stts_conv_transpose1d_bwd(int dtype, const float* x, const float* w, const float* dy, int B, int Lin,
+                                         int Cin, int Cout, int K, int stride, int pad, int Lout, float* dx, float* dw,
+                                         float* db, void* workspace, long long ws_bytes, void* stream) {
+  const long long need = stts_conv_transpose1d_workspace_bytes(dtype, B, Lin, Cin, Cout, K, stride, pad, Lout);
+  if (need < 0) return (int)need;
+  if (!dy || (dx && !w) || (dw && !x)) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const Geo gc = convT_geo(B, Lin, Cin, Cout, K, stride, pad, Lout);
+  char* ws = (char*)workspace;
+  if (dx) ST_CHECK(run_engine(dtype, gc, true, dy, w, nullptr, dx, ws, s));
+  if (dw) {
+    // wgrad of the conv with x := dy (Lout rows, Cout channels) and dy := x (Lin rows, Cin channels)
+    const Slices sl = slices_of(gc);
+    float* part = (float*)(ws + ws_layout(gc, dtype, false).part);
+    if (sl.NA == 2 && sl.NB == 2)
+      launch_wgrad<2, 2>(gc, sl, dy, x, part, s);
+    else if (sl.NA == 2)
+      launch_wgrad<2, 1>(gc, sl, dy, x, part, s);
+    else if (sl.NB == 2)
+      launch_wgrad<1, 2>(gc, sl, dy, x, part, s);
+    else
+      launch_wgrad<1, 1>(gc, sl, dy, x, part, s);
+    ST_CHECK_HIP(hipGetLastError());
+    const size_t n = (size_t)K * gc.Cout * gc.Cin;
+    hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, sl.S, K, gc.Cout,
+                       gc.Cin, dw);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  if (db) {
+    const long long R = (long long)B * Lout;
+    const int S2 = colsum_slices(Cout, R);
+    float* part2 = (float*)(ws + convT_ws(gc, dtype) - al((size_t)S2 * Cout * 4));
+    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((Cout + 63) / 64), S2), dim3(256), 0, s, dy, R, Cout, S2, part2);
+    ST_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, part2, S2, 1, Cout, 1,
+                       db);
     ST_CHECK_HIP(hipGetLastError());
   }
   return 0;

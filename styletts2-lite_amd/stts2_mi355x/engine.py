@@ -77,6 +77,13 @@ def lib():
     L.stts_conv1d_fwd.restype = c_int
     L.stts_conv1d_fwd_res.argtypes = [c_int, c_vp, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
     L.stts_conv1d_fwd_res.restype = c_int
+    L.stts_conv_transpose1d_workspace_bytes.argtypes = [c_int] * 9
+    L.stts_conv_transpose1d_workspace_bytes.restype = c_ll
+    L.stts_conv_transpose1d_fwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp, c_vp, c_ll, c_vp]
+    L.stts_conv_transpose1d_fwd.restype = c_int
+    L.stts_conv_transpose1d_bwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 8 + [c_vp, c_vp, c_vp, c_vp, c_ll,
+                                                                                      c_vp]
+    L.stts_conv_transpose1d_bwd.restype = c_int
     L.stts_conv1d_bwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]
     L.stts_conv1d_bwd.restype = c_int
     L.stts_weight_norm.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]

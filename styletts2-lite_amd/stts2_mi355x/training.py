@@ -109,6 +109,60 @@ class Conv1d(nn.Conv1d):
                       self.dtype_compute)
 
 
+class _ConvT1dFn(torch.autograd.Function):
+    """ConvTranspose1d on frames: x [B, Lin, Cin] -> [B, Lout, Cout], w [Cin, Cout, K]."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pad, out_pad, dtype):
+        _require_device()
+        B, Lin, Cin = x.shape
+        Cin_w, Cout, K = w.shape
+        if Cin_w != Cin:
+            raise ValueError(f"weight {tuple(w.shape)} does not take {Cin} input channels")
+        Lout = (Lin - 1) * stride - 2 * pad + K + out_pad
+        dt = _DT[dtype]
+        xf, wc, bc = _c(x), _c(w), _c(bias)
+        nb = lib().stts_conv_transpose1d_workspace_bytes(dt, B, Lin, Cin, Cout, K, stride, pad, Lout)
+        check(int(nb) if nb < 0 else 0, "stts_conv_transpose1d_workspace_bytes")
+        ws = _ws(nb, x.device)
+        y = torch.empty(B, Lout, Cout, dtype=torch.float32, device=x.device)
+        check(lib().stts_conv_transpose1d_fwd(dt, _ptr(xf), _ptr(wc), _ptr(bc), B, Lin, Cin, Cout, K, stride, pad,
+                                              Lout, _ptr(y), _ptr(ws), int(nb), _stream()),
+              "stts_conv_transpose1d_fwd")
+        ctx.save_for_backward(xf, wc)
+        ctx.geo = (B, Lin, Cin, Cout, K, stride, pad, Lout, dt, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xf, wc = ctx.saved_tensors
+        B, Lin, Cin, Cout, K, stride, pad, Lout, dt, has_bias = ctx.geo
+        nx, nw, nbias = ctx.needs_input_grad[:3]
+        dy = _c(gy)
+        nb = lib().stts_conv_transpose1d_workspace_bytes(dt, B, Lin, Cin, Cout, K, stride, pad, Lout)
+        ws = _ws(nb, dy.device)
+        dx = torch.empty_like(xf) if nx else None
+        dw = torch.empty_like(wc) if nw else None
+        db = torch.empty(Cout, dtype=torch.float32, device=dy.device) if (nbias and has_bias) else None
+        check(lib().stts_conv_transpose1d_bwd(dt, _ptr(xf), _ptr(wc), _ptr(dy), B, Lin, Cin, Cout, K, stride, pad,
+                                              Lout, _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()),
+              "stts_conv_transpose1d_bwd")
+        return dx, dw, db, None, None, None, None
+
+
+def conv_transpose1d_frames(x, weight, bias=None, stride=1, padding=0, output_padding=0, dtype="fp32"):
+    """F.conv_transpose1d (groups 1, dilation 1) on frames [B, Lin, Cin] -> [B, Lout, Cout]."""
+    if dtype not in _DT:
+        raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
+    return _ConvT1dFn.apply(x, weight, bias, int(stride), int(padding), int(output_padding), dtype)
+
+
+def conv_transpose1d(x, weight, bias=None, stride=1, padding=0, output_padding=0, dtype="fp32"):
+    """F.conv_transpose1d on [B, C, L] tensors with forward and backward on the HIP path."""
+    return conv_transpose1d_frames(x.transpose(1, 2), weight, bias, stride, padding, output_padding,
+                                   dtype).transpose(1, 2)
+
+
 ACT_NONE, ACT_SNAKE, ACT_LRELU = 0, 1, 2
 
 

@@ -96,3 +96,39 @@ def test_conv1d_module_dropin():
     mod(x.cuda()).square().mean().backward()
     assert _rel(mod.weight.grad, ref.weight.grad) < 1e-4
     assert _rel(mod.bias.grad, ref.bias.grad) < 1e-4
+
+
+# (B, Cin, Cout, K, stride, pad, out_pad, Lin): the HiFi-GAN upsamplers (hifigan.py:292-294, u = 10, 5, 3,
+# 2 over k = 20, 10, 6, 4), a ragged output_padding case and a stride-1 case
+T_CASES = [
+    (2, 512, 256, 20, 10, 5, 0, 40),
+    (1, 256, 128, 10, 5, 3, 1, 97),
+    (2, 128, 64, 6, 3, 2, 1, 300),
+    (3, 64, 32, 4, 2, 1, 0, 501),
+    (1, 48, 40, 5, 1, 2, 0, 77),
+]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", T_CASES, ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_p{}_op{}_L{}".format(*c))
+def test_conv_transpose1d_fwd_bwd(case, dtype):
+    from stts2_mi355x.training import conv_transpose1d
+    B, Cin, Cout, K, stride, pad, op, Lin = case
+    g = torch.Generator().manual_seed(hash(case) % 2**31)
+    x = torch.randn(B, Cin, Lin, generator=g)
+    w = torch.randn(Cin, Cout, K, generator=g) / np.sqrt(Cin * K / stride)
+    b = torch.randn(Cout, generator=g)
+    xd_, wd_, bd_ = (t.double().requires_grad_(True) for t in (x, w, b))
+    y_ref = torch.nn.functional.conv_transpose1d(xd_, wd_, bd_, stride=stride, padding=pad, output_padding=op)
+    gy = torch.randn(y_ref.shape, generator=g)
+    y_ref.backward(gy.double())
+    xc, wc, bc = (t.cuda().requires_grad_(True) for t in (x, w, b))
+    y = conv_transpose1d(xc, wc, bc, stride, pad, op, dtype=dtype)
+    assert y.shape == y_ref.shape
+    y.backward(gy.cuda())
+    tol = 1e-4 if dtype == "fp32" else 2e-2
+    errs = {"y": _rel(y, y_ref), "dx": _rel(xc.grad, xd_.grad), "dw": _rel(wc.grad, wd_.grad),
+            "db": _rel(bc.grad, bd_.grad)}
+    print(case, dtype, {k: f"{v:.2e}" for k, v in errs.items()})
+    assert errs["y"] < tol and errs["dx"] < tol
+    assert errs["dw"] < 1e-4 and errs["db"] < 1e-5
