@@ -148,10 +148,10 @@ long long stts_conv1d_fwd_workspace_bytes(int dtype, int B, int Lin, int Cin, in
 int stts_conv1d_fwd(int dtype, const float* x, const float* w, const float* bias, int B, int Lin, int Cin, int Cout,
                     int K, int stride, int dil, int pad, int Lq, float* y, void* workspace, long long ws_bytes,
                     void* stream);
-/* The same with a residual added in the epilogue: y = conv1d(x, w, bias) + res (res fp32 [B][Lq][Cout];
+/* The same with a residual added in the epilogue: y = (conv1d(x, w, bias) + res) * scale (res fp32 [B][Lq][Cout];
  * dtype STTS fp32 and Cout % 16 == 0 or Cout <= 32; ST_EINVAL otherwise).  AdaINResBlock1's x = xt + x
  * (hifigan.py:74) rides on convs2 this way; its gradient w.r.t. res is dy itself. */
-int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, const float* bias, const float* res, int B,
+int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, const float* bias, const float* res, float scale, int B,
                         int Lin, int Cin, int Cout, int K, int stride, int dil, int pad, int Lq, float* y,
                         void* workspace, long long ws_bytes, void* stream);
 long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride, int dil,
@@ -194,6 +194,17 @@ int stts_adain_act_bwd(const float* x, const float* gb, const float* alpha, int 
 int stts_linear_fwd(const float* s, const float* W, const float* bias, int B, int K, int N, float* h, void* stream);
 int stts_linear_bwd(const float* s, const float* W, const float* dh, int B, int K, int N, float* ds, float* dW,
                     float* db, void* stream);
+/* AdainResBlk1d's upsampling pieces (hifigan.py:350-403), frames fp32: the depthwise pool
+ * ConvTranspose1d(C, C, 3, stride 2, padding 1, output_padding 1, groups C) with w [C][3] (the folded
+ * [C][1][3] weight), x [B][Lin][C] -> y [B][2 Lin][C], its backward (dx, dw [C][3], db; fp64 row-slice
+ * sums in fixed order, workspace >= stts_pool_workspace_bytes), and the shortcut's nearest x2 upsample
+ * with its backward (dx[m] = dy[2m] + dy[2m+1]). */
+long long stts_pool_workspace_bytes(int B, int Lin, int C);
+int stts_pool_fwd(const float* x, const float* w, const float* bias, int B, int Lin, int C, float* y, void* stream);
+int stts_pool_bwd(const float* x, const float* w, const float* dy, int B, int Lin, int C, float* dx, float* dw,
+                  float* db, void* workspace, long long ws_bytes, void* stream);
+int stts_upsample2(const float* x, int B, int Lin, int C, float* y, void* stream);
+int stts_upsample2_bwd(const float* dy, int B, int Lin, int C, float* dx, void* stream);
 /* weight_norm backward (the training step's convs are weight-normed, hifigan.py:26-80): for w = g v / ||v||
  * per row of v [d0][inner]: dg [d0] = <dw, v> / ||v||, dv = (g / ||v||)(dw - v <dw, v> / ||v||^2). */
 int stts_weight_norm_bwd(const float* g, const float* v, const float* dw, int d0, int inner, float* dg, float* dv,

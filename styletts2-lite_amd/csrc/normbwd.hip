@@ -289,6 +289,123 @@ __global__ __launch_bounds__(256) void k_wn_bwd(const float* __restrict__ g, con
   }
 }
 
+// depthwise ConvTranspose1d(C, C, 3, stride 2, padding 1, output_padding 1, groups C) (AdainResBlk1d.pool,
+// hifigan.py:375-377) on frames: y[2m] = b + w1 x[m], y[2m+1] = b + w2 x[m] + w0 x[m+1] (x[Lin] = 0)
+__global__ void k_pool_fwd(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+                           int Lin, int C, float* __restrict__ y, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // over B * 2Lin * C outputs
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  const long long bo = i / C;
+  const int o = (int)(bo % (2 * Lin));
+  const long long b = bo / (2 * Lin);
+  const float* xb = x + b * Lin * C + c;
+  const int m = o >> 1;
+  float v = bias ? bias[c] : 0.f;
+  if ((o & 1) == 0) {
+    v += w[c * 3 + 1] * xb[(size_t)m * C];
+  } else {
+    v += w[c * 3 + 2] * xb[(size_t)m * C];
+    if (m + 1 < Lin) v += w[c * 3 + 0] * xb[(size_t)(m + 1) * C];
+  }
+  y[i] = v;
+}
+
+// dx[m] = w1 dy[2m] + w2 dy[2m+1] + w0 dy[2m-1]
+__global__ void k_pool_bwd_dx(const float* __restrict__ dy, const float* __restrict__ w, int Lin, int C,
+                              float* __restrict__ dx, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  const long long bm = i / C;
+  const int m = (int)(bm % Lin);
+  const long long b = bm / Lin;
+  const float* db_ = dy + b * 2 * Lin * C + c;
+  float v = w[c * 3 + 1] * db_[(size_t)(2 * m) * C] + w[c * 3 + 2] * db_[(size_t)(2 * m + 1) * C];
+  if (m > 0) v += w[c * 3 + 0] * db_[(size_t)(2 * m - 1) * C];
+  dx[i] = v;
+}
+
+// partials per (b, slice, c) of dw0 = sum dy[2m-1] x[m], dw1 = sum dy[2m] x[m], dw2 = sum dy[2m+1] x[m],
+// db = sum dy (rows m of the slice cover dy rows 2m, 2m+1)
+__global__ __launch_bounds__(256) void k_pool_bwd_part(const float* __restrict__ x, const float* __restrict__ dy,
+                                                       int Lin, int C, int S, double* __restrict__ part) {
+  __shared__ double red[4][4][64];
+  const int l = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + l, s = blockIdx.y, b = blockIdx.z;
+  const int r0 = (int)((long long)Lin * s / S), r1 = (int)((long long)Lin * (s + 1) / S);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (c < C) {
+    const float* xb = x + (size_t)b * Lin * C + c;
+    const float* gb = dy + (size_t)b * 2 * Lin * C + c;
+    for (int m = r0 + rl; m < r1; m += 4) {
+      const double xv = xb[(size_t)m * C];
+      const double g0 = gb[(size_t)(2 * m) * C], g1 = gb[(size_t)(2 * m + 1) * C];
+      if (m > 0) a0 += (double)gb[(size_t)(2 * m - 1) * C] * xv;
+      a1 += g0 * xv;
+      a2 += g1 * xv;
+      a3 += g0 + g1;
+    }
+  }
+  red[0][rl][l] = a0;
+  red[1][rl][l] = a1;
+  red[2][rl][l] = a2;
+  red[3][rl][l] = a3;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    double* p = part + (((size_t)b * S + s) * C + c) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = ((red[k][0][l] + red[k][1][l]) + red[k][2][l]) + red[k][3][l];
+  }
+}
+
+// per channel (one wave): dw[c][0..2], db[c] summed over utterances and slices in fixed order
+__global__ __launch_bounds__(64) void k_pool_bwd_final(const double* __restrict__ part, int B, int C, int S,
+                                                       float* __restrict__ dw, float* __restrict__ db) {
+  const int c = blockIdx.x;
+  double t[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = 0; b < B; ++b) {
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int s = threadIdx.x; s < S; s += 64) {
+      const double* p = part + (((size_t)b * S + s) * C + c) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] += p[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] += wave_sum(v[k]);
+  }
+  if (threadIdx.x == 0) {
+    if (dw) {
+      dw[c * 3 + 0] = (float)t[0];
+      dw[c * 3 + 1] = (float)t[1];
+      dw[c * 3 + 2] = (float)t[2];
+    }
+    if (db) db[c] = (float)t[3];
+  }
+}
+
+// nearest x2 upsample (UpSample1d 'half', hifigan.py:350-357) on frames and its backward
+__global__ void k_up2(const float* __restrict__ x, int Lin, int C, float* __restrict__ y, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  const long long bo = i / C;
+  const int o = (int)(bo % (2 * Lin));
+  const long long b = bo / (2 * Lin);
+  y[i] = x[(b * Lin + (o >> 1)) * C + c];
+}
+
+__global__ void k_up2_bwd(const float* __restrict__ dy, int Lin, int C, float* __restrict__ dx, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  const long long bm = i / C;
+  const int m = (int)(bm % Lin);
+  const long long b = bm / Lin;
+  const float* g = dy + (b * 2 * Lin + 2 * m) * C + c;
+  dx[i] = g[0] + g[C];
+}
+
 inline size_t al(size_t n) { return (n + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -372,4 +489,57 @@ extern "C" int stts_linear_bwd(const float* s_in, const float* W, const float* d
     ST_CHECK_HIP(hipGetLastError());
   }
   return 0;
+}
+
+extern "C" long long stts_pool_workspace_bytes(int B, int Lin, int C) {
+  if (B <= 0 || Lin <= 0 || C <= 0) return ST_EINVAL;
+  return (long long)al((size_t)B * cols_of(B, Lin, C).S * C * 4 * sizeof(double));
+}
+
+extern "C" int stts_pool_fwd(const float* x, const float* w, const float* bias, int B, int Lin, int C, float* y,
+                             void* stream) {
+  if (!x || !w || !y || B <= 0 || Lin <= 0 || C <= 0) return ST_EINVAL;
+  const long long n = (long long)B * 2 * Lin * C;
+  hipLaunchKernelGGL(k_pool_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, w, bias,
+                     Lin, C, y, n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int stts_pool_bwd(const float* x, const float* w, const float* dy, int B, int Lin, int C, float* dx,
+                             float* dw, float* db, void* ws, long long ws_bytes, void* stream) {
+  const long long need = stts_pool_workspace_bytes(B, Lin, C);
+  if (need < 0) return (int)need;
+  if (!dy || (dx && !w) || (dw && !x)) return ST_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (dx) {
+    const long long n = (long long)B * Lin * C;
+    hipLaunchKernelGGL(k_pool_bwd_dx, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dy, w, Lin, C, dx, n);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  if (dw || db) {
+    if (!x) return ST_EINVAL;
+    if (!ws || ws_bytes < need) return ST_EWORKSPACE;
+    const Cols cl = cols_of(B, Lin, C);
+    double* part = (double*)ws;
+    hipLaunchKernelGGL(k_pool_bwd_part, dim3((C + 63) / 64, cl.S, B), dim3(256), 0, s, x, dy, Lin, C, cl.S, part);
+    ST_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_pool_bwd_final, dim3(C), dim3(64), 0, s, part, B, C, cl.S, dw, db);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+extern "C" int stts_upsample2(const float* x, int B, int Lin, int C, float* y, void* stream) {
+  if (!x || !y || B <= 0 || Lin <= 0 || C <= 0) return ST_EINVAL;
+  const long long n = (long long)B * 2 * Lin * C;
+  hipLaunchKernelGGL(k_up2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, Lin, C, y, n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int stts_upsample2_bwd(const float* dy, int B, int Lin, int C, float* dx, void* stream) {
+  if (!dy || !dx || B <= 0 || Lin <= 0 || C <= 0) return ST_EINVAL;
+  const long long n = (long long)B * Lin * C;
+  hipLaunchKernelGGL(k_up2_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy, Lin, C, dx,
+                     n);
+  return (int)hipGetLastError();
 }

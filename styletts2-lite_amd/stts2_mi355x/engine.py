@@ -75,7 +75,18 @@ def lib():
         getattr(L, fn).restype = c_ll
     L.stts_conv1d_fwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
     L.stts_conv1d_fwd.restype = c_int
-    L.stts_conv1d_fwd_res.argtypes = [c_int, c_vp, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
+    L.stts_conv1d_fwd_res.argtypes = [c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_float] + [c_int] * 9 + [c_vp, c_vp,
+                                                                                                   c_ll, c_vp]
+    L.stts_pool_workspace_bytes.argtypes = [c_int, c_int, c_int]
+    L.stts_pool_workspace_bytes.restype = c_ll
+    L.stts_pool_fwd.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp]
+    L.stts_pool_fwd.restype = c_int
+    L.stts_pool_bwd.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]
+    L.stts_pool_bwd.restype = c_int
+    L.stts_upsample2.argtypes = [c_vp, c_int, c_int, c_int, c_vp, c_vp]
+    L.stts_upsample2.restype = c_int
+    L.stts_upsample2_bwd.argtypes = [c_vp, c_int, c_int, c_int, c_vp, c_vp]
+    L.stts_upsample2_bwd.restype = c_int
     L.stts_conv1d_fwd_res.restype = c_int
     L.stts_conv_transpose1d_workspace_bytes.argtypes = [c_int] * 9
     L.stts_conv_transpose1d_workspace_bytes.restype = c_ll

@@ -14,6 +14,9 @@ boundary (plumbing, not compute).
 """
 from __future__ import annotations
 
+import ctypes
+import math
+
 import torch
 from torch import nn
 
@@ -32,7 +35,7 @@ def out_length(Lin: int, K: int, stride: int, pad: int, dil: int) -> int:
 
 class _Conv1dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, dil, dtype, res=None):
+    def forward(ctx, x, w, bias, stride, pad, dil, dtype, res=None, scale=1.0):
         """x: frames [B, Lin, Cin] -> y frames [B, Lq, Cout] (+ res, fp32 frames [B, Lq, Cout])"""
         _require_device()
         B, Lin, Cin = x.shape
@@ -48,9 +51,11 @@ class _Conv1dFn(torch.autograd.Function):
         check(int(nb) if nb < 0 else 0, "stts_conv1d_fwd_workspace_bytes")
         ws = _ws(nb, x.device)
         y = torch.empty(B, Lq, Cout, dtype=torch.float32, device=x.device)
-        if res is not None:
-            rc = res.detach().to(torch.float32).contiguous()
-            check(lib().stts_conv1d_fwd_res(dt, _ptr(xf), _ptr(wc), _ptr(bc), _ptr(rc), B, Lin, Cin, Cout, K, stride,
+        ctx.scale = float(scale)
+        if res is not None or scale != 1.0:
+            rc = res.detach().to(torch.float32).contiguous() if res is not None else None
+            check(lib().stts_conv1d_fwd_res(dt, _ptr(xf), _ptr(wc), _ptr(bc), _ptr(rc), ctypes.c_float(scale), B, Lin,
+                                            Cin, Cout, K, stride,
                                             dil, pad, Lq, _ptr(y), _ptr(ws), int(nb), _stream()),
                   "stts_conv1d_fwd_res")
         else:
@@ -65,6 +70,8 @@ class _Conv1dFn(torch.autograd.Function):
         xf, wc = ctx.saved_tensors
         B, Lin, Cin, Cout, K, stride, dil, pad, Lq, dt, has_bias = ctx.geo
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        if ctx.scale != 1.0:
+            gy = gy * ctx.scale
         dyf = gy.detach().to(torch.float32).contiguous()
         dev = dyf.device
         nb = lib().stts_conv1d_bwd_workspace_bytes(dt, B, Lin, Cin, Cout, K, stride, dil, pad, Lq)
@@ -75,7 +82,7 @@ class _Conv1dFn(torch.autograd.Function):
         db = torch.empty(Cout, dtype=torch.float32, device=dev) if (need_b and has_bias) else None
         check(lib().stts_conv1d_bwd(dt, _ptr(xf), _ptr(wc), _ptr(dyf), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
                                     _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()), "stts_conv1d_bwd")
-        return dx, dw, db, None, None, None, None, (gy if ctx.needs_input_grad[7] else None)
+        return dx, dw, db, None, None, None, None, (gy if ctx.needs_input_grad[7] else None), None
 
 
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
@@ -87,12 +94,13 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
     return conv1d_frames(x.transpose(1, 2), weight, bias, stride, padding, dilation, dtype).transpose(1, 2)
 
 
-def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32", residual=None):
+def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32", residual=None, scale=1.0):
     """conv1d on frames tensors: x [B, Lin, Cin] -> [B, Lq, Cout] (the kernels' native layout);
-    `residual` (frames [B, Lq, Cout], fp32 runs) is added in the conv epilogue."""
+    `residual` (frames [B, Lq, Cout], fp32 runs) is added and the sum multiplied by `scale` in the
+    conv epilogue."""
     if dtype not in _DT:
         raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
-    return _Conv1dFn.apply(x, weight, bias, int(stride), int(padding), int(dilation), dtype, residual)
+    return _Conv1dFn.apply(x, weight, bias, int(stride), int(padding), int(dilation), dtype, residual, float(scale))
 
 
 class Conv1d(nn.Conv1d):
@@ -321,6 +329,106 @@ class AdaINResBlock1(nn.Module):
             x = conv1d_frames(xt, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, c2.padding, c2.dilation,
                               residual=x)  # x = xt + x in convs2's epilogue
         return x
+
+    def forward(self, x, s):
+        return self.forward_frames(x.transpose(1, 2), s).transpose(1, 2)
+
+
+class _PoolFn(torch.autograd.Function):
+    """AdainResBlk1d.pool: depthwise ConvTranspose1d(C, C, 3, 2, 1, output_padding 1) on frames."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        _require_device()
+        B, Lin, C = x.shape
+        xc, wc, bc = _c(x), _c(w).reshape(C, 3), _c(bias)
+        y = torch.empty(B, 2 * Lin, C, dtype=torch.float32, device=x.device)
+        check(lib().stts_pool_fwd(_ptr(xc), _ptr(wc), _ptr(bc), B, Lin, C, _ptr(y), _stream()), "stts_pool_fwd")
+        ctx.save_for_backward(xc, wc)
+        ctx.w_shape, ctx.has_b = w.shape, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, wc = ctx.saved_tensors
+        B, Lin, C = xc.shape
+        dy = _c(gy)
+        nx, nw, nb_ = ctx.needs_input_grad
+        dx = torch.empty_like(xc) if nx else None
+        dw = torch.empty(C, 3, dtype=torch.float32, device=dy.device) if nw else None
+        db = torch.empty(C, dtype=torch.float32, device=dy.device) if (nb_ and ctx.has_b) else None
+        nb = lib().stts_pool_workspace_bytes(B, Lin, C)
+        ws = _ws(nb, dy.device)
+        check(lib().stts_pool_bwd(_ptr(xc), _ptr(wc), _ptr(dy), B, Lin, C, _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws),
+                                  int(nb), _stream()), "stts_pool_bwd")
+        return dx, (dw.reshape(ctx.w_shape) if dw is not None else None), db
+
+
+class _Up2Fn(torch.autograd.Function):
+    """nearest x2 upsample of frames (UpSample1d 'half')."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _require_device()
+        B, Lin, C = x.shape
+        xc = _c(x)
+        y = torch.empty(B, 2 * Lin, C, dtype=torch.float32, device=x.device)
+        check(lib().stts_upsample2(_ptr(xc), B, Lin, C, _ptr(y), _stream()), "stts_upsample2")
+        ctx.shape = (B, Lin, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        B, Lin, C = ctx.shape
+        dy = _c(gy)
+        dx = torch.empty(B, Lin, C, dtype=torch.float32, device=dy.device)
+        check(lib().stts_upsample2_bwd(_ptr(dy), B, Lin, C, _ptr(dx), _stream()), "stts_upsample2_bwd")
+        return dx
+
+
+class _WNConvT(nn.Module):
+    """weight_norm(nn.ConvTranspose1d(C, C, 3, groups=C)) parameter layout (AdainResBlk1d.pool)."""
+
+    def __init__(self, C):
+        super().__init__()
+        self.weight_g = nn.Parameter(torch.ones(C, 1, 1))
+        self.weight_v = nn.Parameter(torch.randn(C, 1, 3) * 0.3)
+        self.bias = nn.Parameter(torch.zeros(C))
+
+
+class AdainResBlk1d(nn.Module):
+    """Trainable Modules/hifigan.py:359-403 AdainResBlk1d (the decoder's encode / decode blocks; same
+    parameter names), forward and backward on the HIP kernels:
+    r = conv2(LReLU(AdaIN2(conv1(pool(LReLU(AdaIN1(x)))))), sc = conv1x1(up2(x)),
+    out = (r + sc) / sqrt(2) (the sum and the scale ride in conv2's epilogue).  Dropout p = 0 (the
+    decoder's setting)."""
+
+    def __init__(self, dim_in, dim_out, style_dim=64, upsample="none"):
+        super().__init__()
+        self.upsample = upsample not in ("none", False, None)
+        self.learned_sc = dim_in != dim_out
+        self.conv1 = _WNConv(dim_in, dim_out, 3, 1, 1)
+        self.conv2 = _WNConv(dim_out, dim_out, 3, 1, 1)
+        self.norm1 = _AdaIN(style_dim, dim_in)
+        self.norm2 = _AdaIN(style_dim, dim_out)
+        if self.learned_sc:
+            self.conv1x1 = _WNConv(dim_in, dim_out, 1, 1, 0)
+            self.conv1x1.bias = None
+        if self.upsample:
+            self.pool = _WNConvT(dim_in)
+
+    def forward_frames(self, x, s):
+        r = adain_act(x, s, self.norm1.fc.weight, self.norm1.fc.bias, None, ACT_LRELU)
+        if self.upsample:
+            r = _PoolFn.apply(r, weight_norm(self.pool.weight_g, self.pool.weight_v), self.pool.bias)
+        c1, c2 = self.conv1, self.conv2
+        r = conv1d_frames(r, weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, 1)
+        r = adain_act(r, s, self.norm2.fc.weight, self.norm2.fc.bias, None, ACT_LRELU)
+        sc = _Up2Fn.apply(x) if self.upsample else x
+        if self.learned_sc:
+            sc = conv1d_frames(sc, weight_norm(self.conv1x1.weight_g, self.conv1x1.weight_v), None, 1, 0)
+        return conv1d_frames(r, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, 1, residual=sc,
+                             scale=1 / math.sqrt(2))
 
     def forward(self, x, s):
         return self.forward_frames(x.transpose(1, 2), s).transpose(1, 2)

@@ -120,3 +120,52 @@ def test_adain_resblock1_fwd_bwd(C, K, L):
     print((C, K, L), "worst", worst, f"{errs[worst]:.2e}", "y", f"{errs['y']:.1e}", "dx", f"{errs['dx']:.1e}")
     for k, v in errs.items():
         assert v < 2e-4, (k, v)
+
+
+@pytest.mark.parametrize("cin,cout,up,L", [(64, 64, False, 300), (96, 64, False, 155), (64, 32, True, 155),
+                                           (1090, 512, True, 40)])
+def test_adain_resblk1d_fwd_bwd(cin, cout, up, L):
+    """One AdainResBlk1d (the decoder's encode / decode blocks, hifigan.py:359-403), output and every
+    gradient against autograd through oracle.adain_resblk1d in fp64."""
+    from stts2_mi355x.training import AdainResBlk1d
+    torch.manual_seed(cin + cout + up)
+    B, S = 2, 128
+    mod = AdainResBlk1d(cin, cout, S, upsample=up)
+    with torch.no_grad():
+        for n, p in mod.named_parameters():
+            if "weight_g" in n:
+                p.uniform_(0.5, 1.5)
+            elif n.endswith("bias"):
+                p.normal_(0, 0.1)
+            else:
+                p.normal_(0, 0.05)
+    x = torch.randn(B, cin, L)
+    s = torch.randn(B, S)
+    Lo = 2 * L if up else L
+    R = torch.randn(B, cout, Lo)
+    sd = {"blk." + k: v.detach().double().requires_grad_(True) for k, v in mod.state_dict().items()}
+    xr, sr = x.double().requires_grad_(True), s.double().requires_grad_(True)
+    y_ref = O.adain_resblk1d(xr, sr, sd, "blk", up, cin != cout)
+    (y_ref * R.double()).sum().backward()
+    mod.cuda()
+    xd, sdv = x.cuda().requires_grad_(True), s.cuda().requires_grad_(True)
+    y = mod(xd, sdv)
+    assert y.shape == y_ref.shape
+    (y * R.cuda()).sum().backward()
+    errs = {"y": _rel(y, y_ref), "dx": _rel(xd.grad, xr.grad), "ds": _rel(sdv.grad, sr.grad)}
+    scale = max(sd["blk." + n].grad.abs().max().item() for n, _ in mod.named_parameters())
+    for n, p in mod.named_parameters():
+        ref = sd["blk." + n].grad
+        if n == "conv1.bias":  # feeds norm2's InstanceNorm: true gradient 0 (see the resblock test)
+            assert p.grad.abs().max().item() < 1e-5 * scale, n
+            continue
+        if n == "conv1.weight_g":
+            v, g, dv = sd["blk.conv1.weight_v"], sd["blk." + n], sd["blk.conv1.weight_v"].grad
+            dw_scale = (dv.flatten(1).norm(dim=1) * v.detach().flatten(1).norm(dim=1) / g.detach().flatten()).max()
+            errs[n] = float((p.grad.detach().double().cpu() - ref).abs().max() / dw_scale)
+            continue
+        errs[n] = _rel(p.grad, ref)
+    worst = max(errs, key=errs.get)
+    print((cin, cout, up, L), "worst", worst, f"{errs[worst]:.2e}", "y", f"{errs['y']:.1e}")
+    for k, v in errs.items():
+        assert v < 2e-4, (k, v)

@@ -52,3 +52,14 @@ def test_layer_workspace_queries():
     L = E.lib()
     assert L.stts_adain_act_workspace_bytes(2, 300, 64) > 0
     assert L.stts_adain_act_workspace_bytes(0, 300, 64) == -1
+
+
+@pytest.mark.parametrize("cin,cout,up", [(1090, 1024, False), (1090, 512, True), (514, 1024, False)])
+def test_training_resblk1d_matches_reference_layout(cin, cout, up):
+    from stts2_mi355x.params import AdainResBlk1d as Ref
+    from stts2_mi355x.training import AdainResBlk1d
+    a = AdainResBlk1d(cin, cout, 128, upsample=up).state_dict()
+    b = Ref(cin, cout, 128, upsample=up).state_dict()
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert a[k].shape == b[k].shape, k
