@@ -205,6 +205,10 @@ int stts_pool_bwd(const float* x, const float* w, const float* dy, int B, int Li
                   float* db, void* workspace, long long ws_bytes, void* stream);
 int stts_upsample2(const float* x, int B, int Lin, int C, float* y, void* stream);
 int stts_upsample2_bwd(const float* dy, int B, int Lin, int C, float* dx, void* stream);
+/* LeakyReLU(slope) over n fp32 values and its backward from the output y (slope > 0), as the
+ * discriminators apply it after every conv (discriminators.py:119, slope 0.1). */
+int stts_leaky_relu(const float* x, long long n, float slope, float* y, void* stream);
+int stts_leaky_relu_bwd(const float* y, const float* dy, long long n, float slope, float* dx, void* stream);
 /* weight_norm backward (the training step's convs are weight-normed, hifigan.py:26-80): for w = g v / ||v||
  * per row of v [d0][inner]: dg [d0] = <dw, v> / ||v||, dv = (g / ||v||)(dw - v <dw, v> / ||v||^2). */
 int stts_weight_norm_bwd(const float* g, const float* v, const float* dw, int d0, int inner, float* dg, float* dv,

@@ -406,6 +406,18 @@ __global__ void k_up2_bwd(const float* __restrict__ dy, int Lin, int C, float* _
   dx[i] = g[0] + g[C];
 }
 
+// LeakyReLU(slope) and its backward from the output (slope > 0 keeps the sign: y > 0 <=> x > 0)
+__global__ void k_lrelu(const float* __restrict__ x, long long n, float slope, float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = x[i] > 0.f ? x[i] : slope * x[i];
+}
+
+__global__ void k_lrelu_bwd(const float* __restrict__ y, const float* __restrict__ dy, long long n, float slope,
+                            float* __restrict__ dx) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dx[i] = y[i] > 0.f ? dy[i] : slope * dy[i];
+}
+
 inline size_t al(size_t n) { return (n + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -541,5 +553,21 @@ extern "C" int stts_upsample2_bwd(const float* dy, int B, int Lin, int C, float*
   const long long n = (long long)B * Lin * C;
   hipLaunchKernelGGL(k_up2_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy, Lin, C, dx,
                      n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int stts_leaky_relu(const float* x, long long n, float slope, float* y, void* stream) {
+  if (!x || !y || n < 0 || !(slope > 0.f)) return ST_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_lrelu, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, n, slope, y);
+  return (int)hipGetLastError();
+}
+
+extern "C" int stts_leaky_relu_bwd(const float* y, const float* dy, long long n, float slope, float* dx,
+                                   void* stream) {
+  if (!y || !dy || !dx || n < 0 || !(slope > 0.f)) return ST_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_lrelu_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y, dy, n,
+                     slope, dx);
   return (int)hipGetLastError();
 }

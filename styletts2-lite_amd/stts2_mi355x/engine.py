@@ -87,6 +87,10 @@ def lib():
     L.stts_upsample2.restype = c_int
     L.stts_upsample2_bwd.argtypes = [c_vp, c_int, c_int, c_int, c_vp, c_vp]
     L.stts_upsample2_bwd.restype = c_int
+    L.stts_leaky_relu.argtypes = [c_vp, c_ll, ctypes.c_float, c_vp, c_vp]
+    L.stts_leaky_relu.restype = c_int
+    L.stts_leaky_relu_bwd.argtypes = [c_vp, c_vp, c_ll, ctypes.c_float, c_vp, c_vp]
+    L.stts_leaky_relu_bwd.restype = c_int
     L.stts_conv1d_fwd_res.restype = c_int
     L.stts_conv_transpose1d_workspace_bytes.argtypes = [c_int] * 9
     L.stts_conv_transpose1d_workspace_bytes.restype = c_ll

@@ -432,3 +432,80 @@ class AdainResBlk1d(nn.Module):
 
     def forward(self, x, s):
         return self.forward_frames(x.transpose(1, 2), s).transpose(1, 2)
+
+
+class _LReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, slope):
+        _require_device()
+        xc = _c(x)
+        y = torch.empty_like(xc)
+        check(lib().stts_leaky_relu(_ptr(xc), xc.numel(), ctypes.c_float(slope), _ptr(y), _stream()),
+              "stts_leaky_relu")
+        ctx.save_for_backward(y)
+        ctx.slope = slope
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        dy = _c(gy)
+        dx = torch.empty_like(y)
+        check(lib().stts_leaky_relu_bwd(_ptr(y), _ptr(dy), y.numel(), ctypes.c_float(ctx.slope), _ptr(dx),
+                                        _stream()), "stts_leaky_relu_bwd")
+        return dx, None
+
+
+def leaky_relu(x, slope):
+    return _LReLUFn.apply(x, float(slope))
+
+
+class _WNConv2dK1(nn.Module):
+    """weight_norm(nn.Conv2d(cin, cout, (k, 1), (stride, 1), padding=(pad, 0))) parameter layout."""
+
+    def __init__(self, cin, cout, k, stride, pad):
+        super().__init__()
+        self.weight_g = nn.Parameter(torch.ones(cout, 1, 1, 1))
+        self.weight_v = nn.Parameter(torch.randn(cout, cin, k, 1) * 0.05)
+        self.bias = nn.Parameter(torch.zeros(cout))
+        self.k, self.stride, self.pad = k, stride, pad
+
+
+class DiscriminatorP(nn.Module):
+    """Trainable Modules/discriminators.py:96-129 DiscriminatorP (weight-norm, k 5, stride 3; same
+    parameter names), forward and backward on the HIP kernels.  Each (k, 1) Conv2d is a conv1d along
+    the H axis of every one of the `period` columns: the [B, C, H, p] map is kept as frames
+    [B * p, H, C] between layers.  forward(x [B, 1, T]) -> (score [B, H * p], fmap [B, C, H, p] x 6)
+    as the reference."""
+
+    def __init__(self, period, kernel_size=5, stride=3):
+        super().__init__()
+        self.period = period
+        ch = [1, 32, 128, 512, 1024, 1024]
+        self.convs = nn.ModuleList([_WNConv2dK1(ch[j], ch[j + 1], kernel_size, stride if j < 4 else 1, 2)
+                                    for j in range(5)])
+        self.conv_post = _WNConv2dK1(1024, 1, 3, 1, 1)
+
+    def forward(self, x):
+        b, c, t = x.shape
+        p = self.period
+        if t % p != 0:
+            x = torch.nn.functional.pad(x, (0, p - t % p), "reflect")  # discriminators.py:112-115
+            t = x.shape[-1]
+        h = x.reshape(b, c, t // p, p).permute(0, 3, 2, 1).reshape(b * p, t // p, c)  # frames [B p, H, C]
+        fmap = []
+
+        def nchw(f):
+            return f.reshape(b, p, f.shape[1], f.shape[2]).permute(0, 3, 2, 1)
+
+        for layer in self.convs:
+            w = weight_norm(layer.weight_g, layer.weight_v)
+            h = conv1d_frames(h, w.reshape(w.shape[0], w.shape[1], layer.k), layer.bias, layer.stride, layer.pad)
+            h = leaky_relu(h, 0.1)
+            fmap.append(nchw(h))
+        cp = self.conv_post
+        w = weight_norm(cp.weight_g, cp.weight_v)
+        h = conv1d_frames(h, w.reshape(1, w.shape[1], cp.k), cp.bias, 1, cp.pad)
+        out = nchw(h)
+        fmap.append(out)
+        return torch.flatten(out, 1, -1), fmap

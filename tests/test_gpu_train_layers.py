@@ -169,3 +169,42 @@ def test_adain_resblk1d_fwd_bwd(cin, cout, up, L):
     print((cin, cout, up, L), "worst", worst, f"{errs[worst]:.2e}", "y", f"{errs['y']:.1e}")
     for k, v in errs.items():
         assert v < 2e-4, (k, v)
+
+
+@pytest.mark.parametrize("period,T", [(2, 6000), (3, 4001), (11, 3000)])
+def test_discriminator_p_fwd_bwd(period, T):
+    """One MPD DiscriminatorP (discriminators.py:96-129): score, the six feature maps, and the gradients
+    of a loss over all of them w.r.t. the input and every parameter, against autograd through
+    oracle.discriminator_p in fp64."""
+    from stts2_mi355x.training import DiscriminatorP
+    torch.manual_seed(period)
+    mod = DiscriminatorP(period)
+    with torch.no_grad():
+        for n, p in mod.named_parameters():
+            if "weight_g" in n:
+                p.uniform_(0.5, 1.5)
+            elif n.endswith("bias"):
+                p.normal_(0, 0.05)
+    B = 2
+    x = torch.randn(B, 1, T) * 0.3
+    sd = {"d." + k: v.detach().double().requires_grad_(True) for k, v in mod.state_dict().items()}
+    xr = x.double().requires_grad_(True)
+    score_r, fmap_r = O.discriminator_p(xr, sd, "d", period)
+    Rs = [torch.randn(f.shape) for f in fmap_r]
+    loss_r = sum((f * r.double()).sum() for f, r in zip(fmap_r, Rs)) + score_r.square().sum()
+    loss_r.backward()
+    mod.cuda()
+    xd = x.cuda().requires_grad_(True)
+    score, fmap = mod(xd)
+    assert score.shape == score_r.shape and [f.shape for f in fmap] == [f.shape for f in fmap_r]
+    loss = sum((f * r.cuda()).sum() for f, r in zip(fmap, Rs)) + score.square().sum()
+    loss.backward()
+    errs = {"score": _rel(score, score_r), "dx": _rel(xd.grad, xr.grad)}
+    for j, (f, fr) in enumerate(zip(fmap, fmap_r)):
+        errs[f"fmap{j}"] = _rel(f, fr)
+    for n, p in mod.named_parameters():
+        errs[n] = _rel(p.grad, sd["d." + n].grad)
+    worst = max(errs, key=errs.get)
+    print((period, T), "worst", worst, f"{errs[worst]:.2e}", "dx", f"{errs['dx']:.1e}")
+    for k, v in errs.items():
+        assert v < 2e-4, (k, v)

@@ -63,3 +63,13 @@ def test_training_resblk1d_matches_reference_layout(cin, cout, up):
     assert sorted(a) == sorted(b)
     for k in a:
         assert a[k].shape == b[k].shape, k
+
+
+def test_training_discriminator_p_matches_reference_layout():
+    from stts2_mi355x.discriminators import DiscriminatorP as Ref
+    from stts2_mi355x.training import DiscriminatorP
+    a = DiscriminatorP(3).state_dict()
+    b = Ref(3).state_dict()
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert a[k].shape == b[k].shape, k
