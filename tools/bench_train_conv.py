@@ -59,7 +59,7 @@ def main():
             print(json.dumps(res), flush=True)
 
 
-if __name__ == "__main__" and "--resblocks" not in sys.argv:
+if __name__ == "__main__" and "--resblocks" not in sys.argv and "--mpd" not in sys.argv:
     main()
 
 
@@ -93,3 +93,35 @@ def bench_resblocks():
 
 if __name__ == "__main__" and "--resblocks" in sys.argv:
     bench_resblocks()
+
+
+def bench_mpd():
+    """Forward + backward of the trainable MPD (periods 2, 3, 5, 7, 11) at config 5's shape: y and y_hat
+    (2 x 93,000 samples each) as one batch of 4, loss = sum of squared scores + feature-map sums."""
+    from stts2_mi355x.training import DiscriminatorP
+    torch.manual_seed(0)
+    ds = [DiscriminatorP(p).cuda() for p in (2, 3, 5, 7, 11)]
+    x = torch.randn(4, 1, 93000, device="cuda") * 0.3
+
+    def step():
+        for d in ds:
+            d.zero_grad(set_to_none=True)
+        loss = 0
+        for d in ds:
+            score, fmap = d(x)
+            loss = loss + score.square().mean() + sum(f.mean() for f in fmap)
+        loss.backward()
+    for _ in range(2):
+        step()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(5):
+        step()
+    b.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"mpd_fwd_bwd": "5 periods, 4 x 93000 samples", "ms": round(a.elapsed_time(b) / 5, 3)}),
+          flush=True)
+
+
+if __name__ == "__main__" and "--mpd" in sys.argv:
+    bench_mpd()
