@@ -478,9 +478,10 @@ class DiscriminatorP(nn.Module):
     [B * p, H, C] between layers.  forward(x [B, 1, T]) -> (score [B, H * p], fmap [B, C, H, p] x 6)
     as the reference."""
 
-    def __init__(self, period, kernel_size=5, stride=3):
+    def __init__(self, period, kernel_size=5, stride=3, dtype_compute="fp32"):
         super().__init__()
         self.period = period
+        self.dtype_compute = dtype_compute  # 'bf16': bf16 operands for the conv forwards and dx
         ch = [1, 32, 128, 512, 1024, 1024]
         self.convs = nn.ModuleList([_WNConv2dK1(ch[j], ch[j + 1], kernel_size, stride if j < 4 else 1, 2)
                                     for j in range(5)])
@@ -500,12 +501,13 @@ class DiscriminatorP(nn.Module):
 
         for layer in self.convs:
             w = weight_norm(layer.weight_g, layer.weight_v)
-            h = conv1d_frames(h, w.reshape(w.shape[0], w.shape[1], layer.k), layer.bias, layer.stride, layer.pad)
+            h = conv1d_frames(h, w.reshape(w.shape[0], w.shape[1], layer.k), layer.bias, layer.stride, layer.pad,
+                              dtype=self.dtype_compute)
             h = leaky_relu(h, 0.1)
             fmap.append(nchw(h))
         cp = self.conv_post
         w = weight_norm(cp.weight_g, cp.weight_v)
-        h = conv1d_frames(h, w.reshape(1, w.shape[1], cp.k), cp.bias, 1, cp.pad)
+        h = conv1d_frames(h, w.reshape(1, w.shape[1], cp.k), cp.bias, 1, cp.pad, dtype=self.dtype_compute)
         out = nchw(h)
         fmap.append(out)
         return torch.flatten(out, 1, -1), fmap

@@ -208,3 +208,22 @@ def test_discriminator_p_fwd_bwd(period, T):
     print((period, T), "worst", worst, f"{errs[worst]:.2e}", "dx", f"{errs['dx']:.1e}")
     for k, v in errs.items():
         assert v < 2e-4, (k, v)
+
+
+def test_discriminator_p_bf16_close():
+    """dtype_compute='bf16' (bf16 operands in the conv forwards and dx; fp32 dw) against the fp32 run:
+    score within 3 % of its range (measured 0.8 %), input gradient within 10 % (measured 6.1 %: bf16
+    rounding compounds through the six dx layers)."""
+    from stts2_mi355x.training import DiscriminatorP
+    torch.manual_seed(7)
+    m32 = DiscriminatorP(5).cuda()
+    m16 = DiscriminatorP(5, dtype_compute="bf16").cuda()
+    m16.load_state_dict(m32.state_dict())
+    x = torch.randn(2, 1, 5000, device="cuda") * 0.3
+    outs = []
+    for m in (m32, m16):
+        xd = x.clone().requires_grad_(True)
+        score, fmap = m(xd)
+        (score.square().sum() + sum(f.sum() for f in fmap)).backward()
+        outs.append((score.detach(), xd.grad.detach()))
+    assert _rel(outs[1][0], outs[0][0]) < 3e-2 and _rel(outs[1][1], outs[0][1]) < 1e-1

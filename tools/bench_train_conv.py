@@ -100,7 +100,8 @@ def bench_mpd():
     (2 x 93,000 samples each) as one batch of 4, loss = sum of squared scores + feature-map sums."""
     from stts2_mi355x.training import DiscriminatorP
     torch.manual_seed(0)
-    ds = [DiscriminatorP(p).cuda() for p in (2, 3, 5, 7, 11)]
+    dtype = "bf16" if "--bf16" in sys.argv else "fp32"
+    ds = [DiscriminatorP(p, dtype_compute=dtype).cuda() for p in (2, 3, 5, 7, 11)]
     x = torch.randn(4, 1, 93000, device="cuda") * 0.3
 
     def step():
@@ -119,7 +120,8 @@ def bench_mpd():
         step()
     b.record()
     torch.cuda.synchronize()
-    print(json.dumps({"mpd_fwd_bwd": "5 periods, 4 x 93000 samples", "ms": round(a.elapsed_time(b) / 5, 3)}),
+    print(json.dumps({"mpd_fwd_bwd": "5 periods, 4 x 93000 samples", "dtype": dtype,
+                      "ms": round(a.elapsed_time(b) / 5, 3)}),
           flush=True)
 
 
