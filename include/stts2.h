@@ -149,7 +149,7 @@ int stts_conv1d_fwd(int dtype, const float* x, const float* w, const float* bias
                     int K, int stride, int dil, int pad, int Lq, float* y, void* workspace, long long ws_bytes,
                     void* stream);
 /* The same with a residual added in the epilogue: y = (conv1d(x, w, bias) + res) * scale (res fp32 [B][Lq][Cout];
- * dtype STTS fp32 and Cout % 16 == 0 or Cout <= 32; ST_EINVAL otherwise).  AdaINResBlock1's x = xt + x
+ * dtype STTS fp32 and Cout % 16 == 0 or Cout <= 32; ST_EINVAL otherwise, and for res = NULL with scale != 1).  AdaINResBlock1's x = xt + x
  * (hifigan.py:74) rides on convs2 this way; its gradient w.r.t. res is dy itself. */
 int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, const float* bias, const float* res, float scale, int B,
                         int Lin, int Cin, int Cout, int K, int stride, int dil, int pad, int Lq, float* y,

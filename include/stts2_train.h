@@ -1,0 +1,143 @@
+/*
+ * stts2_train.h — training-step (BASELINE config 5) entry points of libstts2.so, beyond the layer
+ * forward / backward pairs already in stts2.h (conv1d, ConvTranspose1d, AdaIN1d + activation, Linear,
+ * weight norm, pool, LeakyReLU).
+ *
+ * The reference's fine-tune step (train.py:267-327) runs, per batch: the decoder forward
+ * (Modules/hifigan.py:446-475), DiscriminatorLoss (losses.py:170-190) + backward + AdamW on the MPD /
+ * MSD (Modules/discriminators.py), then MultiResolutionSTFTLoss (losses.py:58-94) + GeneratorLoss
+ * (:149-168) + backward + AdamW on the decoder (optimizers.py:65-73).  Everything below is one piece of
+ * that autograd graph that stts2.h does not already cover; stts2_mi355x/training.py, losses.py and
+ * optim.py string them together as torch.autograd.Functions.
+ *
+ * Conventions as stts2.h: DEVICE pointers to contiguous fp32 data, sizes as ints, `stream` a
+ * hipStream_t (0 = default), caller-owned memory and workspaces, asynchronous, 0 = ok, >0 hipError_t,
+ * <0 STTS_E*.  Every reduction is a fixed-order sum (fp64 partials, added in order): results are
+ * bitwise reproducible run to run.  `go` arguments are DEVICE pointers to the autograd upstream
+ * gradient of a scalar loss (read by the kernel, so no host synchronisation is needed).
+ */
+#ifndef STTS2_TRAIN_H
+#define STTS2_TRAIN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Snake with a learned per-channel alpha, the Generator's stage activations (hifigan.py:329, :343):
+ * y = x + (1 / alpha_c) sin^2(alpha_c x) on frames x, y, dy, dx [B][L][C], alpha [C].  Backward: dx
+ * and dalpha [C] (each nullable); workspace >= stts_snake_workspace_bytes(B, L, C). */
+long long stts_snake_workspace_bytes(int B, int L, int C);
+int stts_snake_fwd(const float* x, const float* alpha, int B, int L, int C, float* y, void* stream);
+int stts_snake_bwd(const float* x, const float* alpha, const float* dy, int B, int L, int C, float* dx,
+                   float* dalpha, void* ws, long long ws_bytes, void* stream);
+
+/* tanh over n values (hifigan.py:345 after conv_post) and its backward from the output. */
+int stts_tanh_fwd(const float* x, long long n, float* y, void* stream);
+int stts_tanh_bwd(const float* y, const float* dy, long long n, float* dx, void* stream);
+
+/* y = (xs[0] + xs[1] + ... + xs[k-1]) / div over n values, added left to right: `x + x_source`
+ * (hifigan.py:334, div 1) and the resblock average `xs / num_kernels` (:337-342).  `xs` is a HOST array
+ * of k <= 8 device pointers.  stts_div: y = x / div (the backward of the average). */
+int stts_sum_div(const float* const* xs, int k, long long n, float div, float* y, void* stream);
+int stts_div(const float* x, long long n, float div, float* y, void* stream);
+
+/* SourceModuleHnNSF for training (hifigan.py:221-268): f0_curve [B][n] (the Decoder's F0_curve; the
+ * Generator upsamples it x scale, :323) -> sw [B][n*scale][9] = the SineGen output sine_waves * uv + noise
+ * (computed under no_grad in the reference, :262-263) and har [B][n*scale] = tanh(l_linear(sw)) (:264).
+ * noise [B][n*scale][9] = the randn_like draw of :213, or NULL for the counter RNG keyed by
+ * (seed, utt_offset + b, sample, harmonic) as stts_decoder_fwd.  Backward: dW [9] and db [1] of l_linear
+ * from dhar (the only parameters with a gradient there).  Workspace >= stts_source_workspace_bytes(B, n). */
+long long stts_source_workspace_bytes(int B, int n);
+int stts_source_fwd(const float* f0_curve, const float* lw, const float* lb, const float* noise,
+                    unsigned long long seed, long long utt_offset, int B, int n, int scale, float* sw, float* har,
+                    void* ws, long long ws_bytes, void* stream);
+int stts_source_bwd(const float* sw, const float* har, const float* dhar, int B, long long L, float* dW, float* db,
+                    void* ws, long long ws_bytes, void* stream);
+
+/* Decoder.forward's train-mode F0 / N smoothing (hifigan.py:447-455):
+ * y = conv1d(x, ones(1, 1, k), padding k // 2) / k per row of x [B][n], k odd; and its backward. */
+int stts_box_smooth_fwd(const float* x, int B, int n, int k, float* y, void* stream);
+int stts_box_smooth_bwd(const float* dy, int B, int n, int k, float* dx, void* stream);
+
+/* A (3, kw) Conv2d over (frames, bins) (SpecDiscriminator, discriminators.py:39-47) as a 1-D conv
+ * along the bins over 3 C channels: x3[s][h][w][c * 3 + dh] = y[s][h + dh - 1][w][c] (0 outside
+ * [0, H)), so the reference's [Cout][C][3][kw] weight is the [Cout][3C][kw] conv1d weight.  Backward:
+ * dy[s][h][w][c] = sum_dh dx3[s][h - dh + 1][w][c * 3 + dh]. */
+int stts_time_expand3(const float* y, int S, int H, int W, int C, float* x3, void* stream);
+int stts_time_expand3_bwd(const float* dx3, int S, int H, int W, int C, float* dy, void* stream);
+
+/* |torch.stft(x, n_fft, hop, win, hann(win), center, reflect, onesided)| (discriminators.py:11-27,
+ * :53): wave [S][ld] (L > n_fft / 2 samples) -> mag [S][F][nb] (F = 1 + L / hop, nb = n_fft / 2 + 1:
+ * the reference's [S, 1, F, nb] image) and spec [S][F][nb][2] (re, im, kept for the backward).
+ * Backward: dwave [S][L] = the stft adjoint (per frame an inverse FFT in LDS, window, then a fixed-order
+ * overlap-add gather that folds the reflect padding back) of dspec = dmag * spec / |spec|
+ * (0 where |spec| = 0, as torch.abs).  n_fft a power of two <= 2048.
+ * Workspace >= stts_stft_mag_workspace_bytes(S, L, n_fft, win, hop). */
+long long stts_stft_mag_workspace_bytes(int S, long long L, int n_fft, int win, int hop);
+int stts_stft_mag_fwd(const float* wave, int S, long long L, long long ld, int n_fft, int win, int hop, float* mag,
+                      float* spec, void* stream);
+int stts_stft_mag_bwd(const float* spec, const float* dmag, int S, long long L, int n_fft, int win, int hop,
+                      float* dwave, void* ws, long long ws_bytes, void* stream);
+
+/* MultiResolutionSTFTLoss backward (losses.py:24-94; stts_mrstft_loss is the forward): dx [B][L]
+ * = go * d loss / d x for x the predicted signal (train.py:281 stft_loss(y_rec, wav)) and y the target.
+ * Per resolution: log-mel of y, ||y_mag||_1, then per frame of x the FFT, mel, d|mag| = -sign(y - x) /
+ * (n_res ||y_mag||_1), the log / filterbank / power adjoints and the inverse FFT; the frames are
+ * overlap-added in fixed order.  The int arrays are HOST pointers.
+ * Workspace >= stts_mrstft_bwd_workspace_bytes(B, L, n_ffts, hops, wins, n_res, n_mels). */
+long long stts_mrstft_bwd_workspace_bytes(int B, long long L, const int* n_ffts, const int* hops, const int* wins,
+                                          int n_res, int n_mels);
+int stts_mrstft_loss_bwd(const float* x, const float* y, int B, long long L, long long ld, const int* n_ffts,
+                         const int* hops, const int* wins, int n_res, int sample_rate, int n_mels, const float* go,
+                         float* dx, void* ws, long long ws_bytes, void* stream);
+
+/* GAN loss terms: the sums GeneratorLoss / DiscriminatorLoss form (losses.py:97-190).  A term reads
+ * two equally laid out tensors a, b of n values (a = the real side, b = the generated side):
+ *   STTS_GAN_FEATURE  2 mean|a - b|                    feature_loss (:97-103, fmap_r, fmap_g)
+ *   STTS_GAN_GEN      mean((1 - b)^2)                  generator_loss (:120-128, b = D(y_hat))
+ *   STTS_GAN_DISC     mean((1 - a)^2) + mean(b^2)      discriminator_loss (:106-117)
+ *   STTS_GAN_TPRLS    tau - relu(tau - mean(((a - b) - m)^2 over a < b + m)),  m = median(a - b)
+ *                     (the lower median, as torch.median), tau = 0.04: discriminator_TPRLS_loss(dr, dg)
+ *                     with (a, b) = (dr, dg) and generator_TPRLS_loss(dr, dg) with (a, b) = (dg, dr)
+ *                     (:131-147; the latter's loop swaps the names).
+ * stts_gan_loss: loss (device, 1 double) = the sum of the terms in order; it also leaves per-term
+ * results (median, selected count, mean) in the workspace for the backward.  stts_gan_loss_bwd (after
+ * the forward, same terms and workspace): da[i] / db[i] (device, n values each, nullable) = go * the
+ * term's gradient w.r.t. a / b (torch's: sign(0) = 0; the median's gradient shared evenly by the
+ * elements equal to it; relu'(0) = 0).  `terms`, `da`, `db` are HOST arrays; n_terms <= 256.
+ * Workspace >= stts_gan_workspace_bytes(n_terms). */
+typedef struct {
+  const float* a;
+  const float* b;
+  long long n;
+  int kind;
+} stts_gan_term;
+#define STTS_GAN_FEATURE 0
+#define STTS_GAN_GEN 1
+#define STTS_GAN_DISC 2
+#define STTS_GAN_TPRLS 3
+long long stts_gan_workspace_bytes(int n_terms);
+int stts_gan_loss(const stts_gan_term* terms, int n_terms, double* loss, void* ws, long long ws_bytes, void* stream);
+int stts_gan_loss_bwd(const stts_gan_term* terms, float* const* da, float* const* db, int n_terms, const float* go,
+                      const void* ws, long long ws_bytes, void* stream);
+
+/* AdamW step (torch.optim.AdamW, single-tensor arithmetic order, amsgrad off), as build_optimizer makes it
+ * (optimizers.py:65-73: betas (0.0, 0.99), eps 1e-9, weight_decay 1e-4): for every tensor
+ *   p *= 1 - lr wd;  m = lerp(m, g, 1 - beta1);  v = v beta2 + (1 - beta2) g g;
+ *   p += (-lr / (1 - beta1^step)) m / (sqrt(v) / sqrt(1 - beta2^step) + eps)
+ * with `step` the tensor's step count after the increment (1 on the first call).  `tensors` is a HOST
+ * array; any number of tensors (one launch per 32). */
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  long long n;
+} stts_adamw_tensor;
+int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, long long step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STTS2_TRAIN_H */

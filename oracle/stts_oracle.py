@@ -94,18 +94,19 @@ def sine_source(f0_curve, sd, p, upsample_scale: int, noise):
     rand_ini (hifigan.py:126-129) is added to sample 0 only and the ÷upsample_scale linear
     downsample reads samples 300j+149/150 only, so it never reaches the output (measured
     diff 0.0); it is omitted.  Returns har [B, L, 1] (pre-transpose)."""
-    f0 = F.interpolate(f0_curve[:, None], scale_factor=upsample_scale).transpose(1, 2)  # nearest, [B,L,1]
-    fn = torch.multiply(f0, torch.FloatTensor([[range(1, 10)]]))
-    rad_values = (fn / 24000) % 1
-    rad_values = F.interpolate(rad_values.transpose(1, 2), scale_factor=1 / upsample_scale,
-                               mode="linear").transpose(1, 2)
-    phase = torch.cumsum(rad_values, dim=1) * 2 * np.pi
-    phase = F.interpolate(phase.transpose(1, 2) * upsample_scale, scale_factor=upsample_scale,
-                          mode="linear").transpose(1, 2)
-    sine_waves = torch.sin(phase) * 0.1
-    uv = (f0 > 10).type(torch.float32)
-    noise_amp = uv * 0.003 + (1 - uv) * 0.1 / 3
-    sine_waves = sine_waves * uv + noise_amp * noise
+    with torch.no_grad():  # SourceModuleHnNSF.forward runs l_sin_gen under no_grad (hifigan.py:262-263)
+        f0 = F.interpolate(f0_curve[:, None], scale_factor=upsample_scale).transpose(1, 2)  # nearest, [B,L,1]
+        fn = torch.multiply(f0, torch.FloatTensor([[range(1, 10)]]))
+        rad_values = (fn / 24000) % 1
+        rad_values = F.interpolate(rad_values.transpose(1, 2), scale_factor=1 / upsample_scale,
+                                   mode="linear").transpose(1, 2)
+        phase = torch.cumsum(rad_values, dim=1) * 2 * np.pi
+        phase = F.interpolate(phase.transpose(1, 2) * upsample_scale, scale_factor=upsample_scale,
+                              mode="linear").transpose(1, 2)
+        sine_waves = torch.sin(phase) * 0.1
+        uv = (f0 > 10).type(torch.float32)
+        noise_amp = uv * 0.003 + (1 - uv) * 0.1 / 3
+        sine_waves = sine_waves * uv + noise_amp * noise
     return torch.tanh(F.linear(sine_waves, _t(sd, p + ".l_linear.weight"), _t(sd, p + ".l_linear.bias")))
 
 
@@ -171,8 +172,23 @@ def decoder_frontend(asr, F0_curve, N, s, sd):
     return x
 
 
-def decoder_hifigan(asr, F0_curve, N, s, sd, cfg, noise, taps=None):
-    """reference hifigan.py:446-475 (Decoder.forward, eval)."""
+def train_smooth(F0_curve, N, F0_down, N_down):
+    """Decoder.forward's train-mode branch (hifigan.py:447-455): box-smooth F0_curve over F0_down frames
+    and N over N_down frames (0 = off); the reference draws F0_down from [0, 3, 7] and N_down from
+    [0, 3, 7, 15] with random.randint."""
+    if F0_down:
+        F0_curve = F.conv1d(F0_curve.unsqueeze(1), torch.ones(1, 1, F0_down, dtype=F0_curve.dtype),
+                            padding=F0_down // 2).squeeze(1) / F0_down
+    if N_down:
+        N = F.conv1d(N.unsqueeze(1), torch.ones(1, 1, N_down, dtype=N.dtype), padding=N_down // 2).squeeze(1) / N_down
+    return F0_curve, N
+
+
+def decoder_hifigan(asr, F0_curve, N, s, sd, cfg, noise, taps=None, smooth=None):
+    """reference hifigan.py:446-475 (Decoder.forward; eval, or the train-mode smoothing with
+    smooth = (F0_down, N_down))."""
+    if smooth is not None:
+        F0_curve, N = train_smooth(F0_curve, N, *smooth)
     x = decoder_frontend(asr, F0_curve, N, s, sd)
     if taps is not None:
         taps["frontend"] = x
@@ -728,3 +744,127 @@ def gan_losses(y_d_rs, y_d_gs, fmap_rs, fmap_gs):
     gen = sum(torch.mean((1 - dg) ** 2) for dg in y_d_gs)
     disc = sum(torch.mean((1 - dr) ** 2) + torch.mean(dg ** 2) for dr, dg in zip(y_d_rs, y_d_gs))
     return fm, gen, disc
+
+
+# ----------------------------------------------------------------------- the assembled training step (config 5)
+TAU = 0.04
+
+
+def discriminator_tprls_loss(disc_real_outputs, disc_generated_outputs):
+    """losses.py:131-138 discriminator_TPRLS_loss."""
+    loss = 0
+    for dr, dg in zip(disc_real_outputs, disc_generated_outputs):
+        m_DG = torch.median((dr - dg))
+        L_rel = torch.mean((((dr - dg) - m_DG) ** 2)[dr < dg + m_DG])
+        loss += TAU - F.relu(TAU - L_rel)
+    return loss
+
+
+def generator_tprls_loss(disc_real_outputs, disc_generated_outputs):
+    """losses.py:140-147 generator_TPRLS_loss (its loop names the real outputs dg and the generated dr)."""
+    loss = 0
+    for dg, dr in zip(disc_real_outputs, disc_generated_outputs):
+        m_DG = torch.median((dr - dg))
+        L_rel = torch.mean((((dr - dg) - m_DG) ** 2)[dr < dg + m_DG])
+        loss += TAU - F.relu(TAU - L_rel)
+    return loss
+
+
+def feature_loss(fmap_r, fmap_g):
+    """losses.py:97-103."""
+    loss = 0
+    for dr, dg in zip(fmap_r, fmap_g):
+        for rl, gl in zip(dr, dg):
+            loss += torch.mean(torch.abs(rl - gl))
+    return loss * 2
+
+
+def generator_loss(disc_outputs):
+    """losses.py:120-128 (the loss only)."""
+    loss = 0
+    for dg in disc_outputs:
+        loss += torch.mean((1 - dg) ** 2)
+    return loss
+
+
+def discriminator_loss(disc_real_outputs, disc_generated_outputs):
+    """losses.py:106-117 (the loss only)."""
+    loss = 0
+    for dr, dg in zip(disc_real_outputs, disc_generated_outputs):
+        loss += torch.mean((1 - dr) ** 2) + torch.mean(dg ** 2)
+    return loss
+
+
+def generator_loss_all(y, y_hat, mpd_sd, msd_sd):
+    """GeneratorLoss.forward (losses.py:156-168)."""
+    y_df_hat_r, y_df_hat_g, fmap_f_r, fmap_f_g = mpd(y, y_hat, mpd_sd)
+    y_ds_hat_r, y_ds_hat_g, fmap_s_r, fmap_s_g = msd(y, y_hat, msd_sd)
+    loss_fm_f = feature_loss(fmap_f_r, fmap_f_g)
+    loss_fm_s = feature_loss(fmap_s_r, fmap_s_g)
+    loss_gen_f = generator_loss(y_df_hat_g)
+    loss_gen_s = generator_loss(y_ds_hat_g)
+    loss_rel = generator_tprls_loss(y_df_hat_r, y_df_hat_g) + generator_tprls_loss(y_ds_hat_r, y_ds_hat_g)
+    return (loss_gen_s + loss_gen_f + loss_fm_s + loss_fm_f + loss_rel).mean()
+
+
+def discriminator_loss_all(y, y_hat, mpd_sd, msd_sd):
+    """DiscriminatorLoss.forward (losses.py:177-190)."""
+    y_df_hat_r, y_df_hat_g, _, _ = mpd(y, y_hat, mpd_sd)
+    loss_disc_f = discriminator_loss(y_df_hat_r, y_df_hat_g)
+    y_ds_hat_r, y_ds_hat_g, _, _ = msd(y, y_hat, msd_sd)
+    loss_disc_s = discriminator_loss(y_ds_hat_r, y_ds_hat_g)
+    loss_rel = discriminator_tprls_loss(y_df_hat_r, y_df_hat_g) + discriminator_tprls_loss(y_ds_hat_r, y_ds_hat_g)
+    return (loss_disc_s + loss_disc_f + loss_rel).mean()
+
+
+def adamw_update(p, g, m, v, step, lr, betas=(0.0, 0.99), eps=1e-9, weight_decay=1e-4):
+    """torch.optim.AdamW's single-tensor update (torch/optim/adam.py _single_tensor_adam with decoupled
+    weight decay, amsgrad off), as optimizers.py:65-73 builds it; in place on p, m, v (fp32 tensors);
+    `step` counts this update (1 first)."""
+    beta1, beta2 = betas
+    p.mul_(1 - lr * weight_decay)
+    m.lerp_(g, 1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    bias_correction1 = 1 - beta1 ** step
+    bias_correction2 = 1 - beta2 ** step
+    denom = (v.sqrt() / (bias_correction2 ** 0.5)).add_(eps)
+    p.addcdiv_(m, denom, value=-(lr / bias_correction1))
+
+
+def train_step(dec_sd, mpd_sd, msd_sd, cfg, asr, F0_curve, N, s, wav, noise, lr_dec=1e-5, lr_disc=1e-4,
+               lambda_mel=5.0, lambda_gen=1.0, smooth=None):
+    """train.py:267-327 restricted to the decoder and the discriminators (BASELINE config 5): the decoder
+    forward (eval, as train.py:190 leaves it, or the train-mode smoothing), then
+      d_loss = DiscriminatorLoss(wav, y_rec.detach()); backward; AdamW on the MPD and MSD   (:272-276)
+      g_loss = lambda_mel MultiResolutionSTFTLoss(y_rec, wav) + lambda_gen GeneratorLoss(wav, y_rec);
+      backward; AdamW on the decoder                                                        (:278-325)
+    Every state dict is a {name: fp32 tensor}; parameters are updated in place (new leaves), so the
+    caller passes copies.  Returns (y_rec, losses dict, grads dict {"dec" / "mpd" / "msd" / "inputs": {...}})."""
+    leaf = lambda sd: {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}  # noqa: E731
+    dsd, psd, ssd = leaf(dec_sd), leaf(mpd_sd), leaf(msd_sd)
+    ins = {k: v.detach().clone().requires_grad_(True) for k, v in
+           (("asr", asr), ("F0_curve", F0_curve), ("N", N), ("s", s))}
+    y_rec = decoder_hifigan(ins["asr"], ins["F0_curve"], ins["N"], ins["s"], dsd, cfg, noise, smooth=smooth)
+    d_loss = discriminator_loss_all(wav, y_rec.detach(), psd, ssd)
+    d_loss.backward()
+    grads = {"mpd": {k: v.grad for k, v in psd.items()}, "msd": {k: v.grad for k, v in ssd.items()}}
+    with torch.no_grad():
+        for sd_ in (psd, ssd):
+            for k, v in sd_.items():
+                adamw_update(v, v.grad, torch.zeros_like(v), torch.zeros_like(v), 1, lr_disc)
+                v.grad = None
+    loss_mel = mrstft_loss(y_rec, wav)
+    loss_gen_all = generator_loss_all(wav, y_rec, psd, ssd)
+    g_loss = lambda_mel * loss_mel + lambda_gen * loss_gen_all
+    g_loss.backward()
+    grads["dec"] = {k: v.grad for k, v in dsd.items()}
+    grads["inputs"] = {k: v.grad for k, v in ins.items()}
+    with torch.no_grad():
+        for k, v in dsd.items():
+            if v.grad is not None:
+                adamw_update(v, v.grad, torch.zeros_like(v), torch.zeros_like(v), 1, lr_dec)
+    losses = {"d_loss": d_loss.item(), "loss_mel": loss_mel.item(), "loss_gen_all": loss_gen_all.item(),
+              "g_loss": g_loss.item()}
+    params = {"dec": {k: v.detach() for k, v in dsd.items()}, "mpd": {k: v.detach() for k, v in psd.items()},
+              "msd": {k: v.detach() for k, v in ssd.items()}}
+    return y_rec.detach(), losses, grads, params

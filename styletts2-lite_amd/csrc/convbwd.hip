@@ -370,6 +370,9 @@ extern "C" int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, co
   const long long need = stts_conv1d_fwd_workspace_bytes(dtype, B, Lin, Cin, Cout, K, stride, dil, pad, Lq);
   if (need < 0) return (int)need;
   if (!x || !w || !y) return ST_EINVAL;
+  // the engines apply out_scale in their residual epilogue only: a scale without a residual would be
+  // silently dropped (and the autograd backward would still scale dy), so it is refused
+  if (!res && scale != 1.0f) return ST_EINVAL;
   if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
   const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
   return run_engine(dtype, g, true, x, w, bias, y, (char*)workspace, (hipStream_t)stream, res, scale);

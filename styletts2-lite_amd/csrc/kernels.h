@@ -260,7 +260,9 @@ int st_stft_mag_x3(const float* x, int S, long long L, long long ld, int n_fft, 
                    hipStream_t s);
 // x3[s][h][w][c * 3 + dh] = y[s][h + dh - 1][w][c], 0 outside [0, H)
 int st_time_expand(const void* y, int S, int H, int W, int C, void* x3, int dtype, hipStream_t s);
-// sums[0] += sum |y - x|, sums[1] += sum |y|   (SpectralConvergengeLoss numerator / denominator)
-int st_sc_sums(const float* xm, const float* ym, long long n, double* sums, hipStream_t s);
-// loss[0] = mean_r sums[2r] / sums[2r + 1]
-int st_sc_final(const double* sums, int nres, double* loss, hipStream_t s);
+// SpectralConvergengeLoss numerator / denominator partials of one resolution: part[blk][0] = sum |y - x|,
+// part[blk][1] = sum |y| over a fixed split of the n elements (st_sc_part_bytes(1) bytes per resolution)
+int st_sc_sums(const float* xm, const float* ym, long long n, double* part, hipStream_t s);
+// loss[0] = mean_r (sum of r's part[.][0]) / (sum of r's part[.][1]), partials added in block order
+int st_sc_final(const double* part, int nres, double* loss, hipStream_t s);
+long long st_sc_part_bytes(int nres);

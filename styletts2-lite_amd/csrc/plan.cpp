@@ -1698,8 +1698,8 @@ int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double*
   return st_mpd_losses(out, sg, scratch, loss, (hipStream_t)stream);
 }
 
-// MultiResolutionSTFTLoss (losses.py:55-94): workspace = the per-resolution sums + one resolution's
-// log-mels of both signals (resolutions run one after the other on the stream)
+// MultiResolutionSTFTLoss (losses.py:55-94): workspace = the per-resolution partial sums (fixed-order
+// reduction) + one resolution's log-mels of both signals (resolutions run one after the other on the stream)
 long long stts_mrstft_workspace_bytes(int B, long long L, const int* hops, int n_res, int n_mels) {
   if (B <= 0 || L <= 0 || !hops || n_res <= 0 || n_res > 16 || n_mels <= 0) return ST_EINVAL;
   long long f = 0;
@@ -1707,7 +1707,7 @@ long long stts_mrstft_workspace_bytes(int B, long long L, const int* hops, int n
     if (hops[r] <= 0) return ST_EINVAL;
     f = std::max(f, st_stft_frames(L, hops[r]));
   }
-  return 256 + 2LL * B * n_mels * f * 4;
+  return ((st_sc_part_bytes(n_res) + 255) & ~255LL) + 2LL * B * n_mels * f * 4;
 }
 
 int stts_mrstft_loss(const float* x, const float* y, int B, long long L, long long ld, const int* n_ffts,
@@ -1718,17 +1718,17 @@ int stts_mrstft_loss(const float* x, const float* y, int B, long long L, long lo
   if (need < 0) return (int)need;
   if (!ws || ws_bytes < need) return ST_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
-  double* sums = reinterpret_cast<double*>(ws);
-  ST_CHECK_HIP(hipMemsetAsync(sums, 0, 2 * n_res * sizeof(double), s));
-  float* mx = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + 256);
+  double* part = reinterpret_cast<double*>(ws);
+  const long long pb = (st_sc_part_bytes(n_res) + 255) & ~255LL;
+  float* mx = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + pb);
   for (int r = 0; r < n_res; ++r) {
     const long long F = st_stft_frames(L, hops[r]);
     float* my = mx + (size_t)B * n_mels * F;
     ST_CHECK(st_logmel(x, B, L, ld, n_ffts[r], wins[r], hops[r], n_mels, (float)sample_rate, mx, s));
     ST_CHECK(st_logmel(y, B, L, ld, n_ffts[r], wins[r], hops[r], n_mels, (float)sample_rate, my, s));
-    ST_CHECK(st_sc_sums(mx, my, (long long)B * n_mels * F, sums + 2 * r, s));
+    ST_CHECK(st_sc_sums(mx, my, (long long)B * n_mels * F, part + (size_t)r * st_sc_part_bytes(1) / 8, s));
   }
-  return st_sc_final(sums, n_res, loss, s);
+  return st_sc_final(part, n_res, loss, s);
 }
 
 long long stts_msd_out_elems(const stts_model* m, int B, int T) {

@@ -1,9 +1,13 @@
 """Drop-in MultiPeriodDiscriminator (Modules/discriminators.py:96-156) and MultiResSpecDiscriminator
 (:29-94) for the training step: same constructors, sub-module names and
 state-dict keys (`discriminators.{i}.convs.{j}.weight_g / weight_v / bias`, `discriminators.{i}.conv_post.*`;
-`discriminators.{i}.discriminators.{j}.*`, `discriminators.{i}.out.*`), the forwards on the HIP engines
-(stts_mpd_fwd, stts_msd_fwd).  Forward only: the reference trains these with autograd; backward
-kernels are not built.
+`discriminators.{i}.discriminators.{j}.*`, `discriminators.{i}.out.*`).
+
+Two paths behind one forward(y, y_hat):
+  * autograd needed (grad enabled and a parameter or an input requires grad, as in train.py's D and G
+    steps): the layer-by-layer HIP forward / backward of training.py (discriminator_p_forward,
+    spec_discriminator_forward), gradients for the parameters and the inputs;
+  * otherwise the fused forward engines (stts_mpd_fwd, stts_msd_fwd), packed weights, fp32 or bf16.
 """
 from __future__ import annotations
 
@@ -48,6 +52,7 @@ class MultiPeriodDiscriminator(nn.Module):
         super().__init__()
         self.discriminators = nn.ModuleList([DiscriminatorP(p) for p in periods])
         self._engine = None
+        self.dtype_compute = "fp32"  # default dtype of forward() ('bf16': bf16 conv operands, fp32 accumulation)
 
     def engine(self, dtype="fp32"):
         from .engine import MPDEngine
@@ -58,7 +63,12 @@ class MultiPeriodDiscriminator(nn.Module):
     def invalidate(self):
         self._engine = None
 
-    def forward(self, y, y_hat, dtype="fp32"):
+    def forward(self, y, y_hat, dtype=None):
+        dtype = dtype or self.dtype_compute
+        if _needs_graph(self, y, y_hat):
+            from .training import discriminator_p_forward
+            return _train_forward(lambda d, x: discriminator_p_forward(d, x, d.period, dtype), self.discriminators,
+                                  y, y_hat)
         B = y.shape[0]
         res = self.engine(dtype).forward(torch.cat([y, y_hat], 0))
         y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
@@ -70,11 +80,45 @@ class MultiPeriodDiscriminator(nn.Module):
         return y_d_rs, y_d_gs, fmap_rs, fmap_gs
 
 
+def _needs_graph(module, y, y_hat):
+    """True when the caller will differentiate the outputs (train.py's D and G steps)."""
+    if not torch.is_grad_enabled():
+        return False
+    return any(t.requires_grad for t in (y, y_hat) if isinstance(t, torch.Tensor)) or \
+        any(p.requires_grad for p in module.parameters())
+
+
+def _train_forward(run, discs, y, y_hat):
+    """The reference's per-discriminator loop (discriminators.py:143-156 / :80-94) on the autograd path.  y and
+    y_hat go through one batched call when they need the same graph (the D step: neither requires grad);
+    otherwise separately, the side without a gradient under no_grad when no parameter needs one."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    y, y_hat = y.to(device=dev, dtype=torch.float32), y_hat.to(device=dev, dtype=torch.float32)
+    B = y.shape[0]
+    params_grad = any(p.requires_grad for d in discs for p in d.parameters())
+    y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
+    for d in discs:
+        if y.requires_grad == y_hat.requires_grad:
+            score, fmaps = run(d, torch.cat([y, y_hat], 0))
+            r, fr = score[:B], [f[:B] for f in fmaps]
+            g, fg = score[B:], [f[B:] for f in fmaps]
+        else:
+            with torch.set_grad_enabled(params_grad or y.requires_grad):
+                r, fr = run(d, y)
+            g, fg = run(d, y_hat)
+        y_d_rs.append(r)
+        y_d_gs.append(g)
+        fmap_rs.append(fr)
+        fmap_gs.append(fg)
+    return y_d_rs, y_d_gs, fmap_rs, fmap_gs
+
+
 def mpd_gan_losses(mpd: MultiPeriodDiscriminator, y, y_hat, dtype="fp32"):
     """One MPD forward of (y, y_hat) and, on the device, the reference's
     feature_loss(fmap_rs, fmap_gs), generator_loss(y_d_gs)[0] and discriminator_loss(y_d_rs, y_d_gs)[0]
     (losses.py:97-128) over its outputs -> (feature, generator, discriminator) float64 scalars."""
-    mpd(y, y_hat, dtype=dtype)
+    with torch.no_grad():  # the fused forward engine (its outputs feed the device loss sums)
+        mpd(y, y_hat, dtype=dtype)
     loss = mpd.engine(dtype).gan_losses()
     return loss[0], loss[1], loss[2]
 
@@ -111,6 +155,7 @@ class MultiResSpecDiscriminator(nn.Module):
         self.discriminators = nn.ModuleList([SpecDiscriminator(f, h, w, window)
                                              for f, h, w in zip(fft_sizes, hop_sizes, win_lengths)])
         self._engine = None
+        self.dtype_compute = "fp32"  # default dtype of forward() ('bf16': bf16 conv operands, fp32 accumulation)
 
     def engine(self, dtype="fp32"):
         from .engine import MSDEngine
@@ -121,7 +166,12 @@ class MultiResSpecDiscriminator(nn.Module):
     def invalidate(self):
         self._engine = None
 
-    def forward(self, y, y_hat, dtype="fp32"):
+    def forward(self, y, y_hat, dtype=None):
+        dtype = dtype or self.dtype_compute
+        if _needs_graph(self, y, y_hat):
+            from .training import spec_discriminator_forward
+            return _train_forward(lambda d, x: spec_discriminator_forward(d, x, dtype), self.discriminators, y,
+                                  y_hat)
         B = y.shape[0]
         res = self.engine(dtype).forward(torch.cat([y, y_hat], 0))
         y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
@@ -135,6 +185,7 @@ class MultiResSpecDiscriminator(nn.Module):
 
 def msd_gan_losses(msd: MultiResSpecDiscriminator, y, y_hat, dtype="fp32"):
     """As mpd_gan_losses, over the MultiResSpecDiscriminator outputs."""
-    msd(y, y_hat, dtype=dtype)
+    with torch.no_grad():  # the fused forward engine (its outputs feed the device loss sums)
+        msd(y, y_hat, dtype=dtype)
     loss = msd.engine(dtype).gan_losses()
     return loss[0], loss[1], loss[2]

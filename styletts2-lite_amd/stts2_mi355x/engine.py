@@ -191,6 +191,16 @@ def check(rc: int, what: str = "stts"):
         raise RuntimeError(f"{what} failed: {msg} (code {rc})")
 
 
+def forward_only(module, what):
+    """The HIP path of `module` has no backward: refuse to run where the caller would differentiate the
+    output (grad mode on and a parameter requiring grad), instead of returning a tensor without a graph
+    whose gradients would silently be lost.  Inference runs under torch.no_grad() (inference.py:234)."""
+    if torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters()):
+        raise NotImplementedError(
+            f"{what}: the HIP path is forward-only (no backward kernels for this module); call it under "
+            "torch.no_grad() as inference.py does, or freeze its parameters (requires_grad_(False))")
+
+
 def _require_device():
     if not torch.cuda.is_available():
         raise RuntimeError("stts2_mi355x needs a HIP device (MI355X / gfx950); no CPU fallback exists")

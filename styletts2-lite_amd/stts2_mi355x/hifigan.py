@@ -6,6 +6,12 @@ Same constructor signature, same sub-module names and state-dict keys (678 keys,
 (reference inference.py:104-111, 158-168).  `forward(asr, F0_curve, N, s)` runs the
 whole decoder as HIP kernels for gfx950 through the C-ABI library
 (`include/stts2.h`, `stts_decoder_fwd`); there is no PyTorch compute fallback.
+
+When the caller will differentiate the output (grad enabled and a parameter or an input requires grad:
+train.py:267 under the G step's backward, :318), the forward instead runs the layer-by-layer HIP
+forward / backward of training.decoder_forward, which returns a graph: every parameter, asr, F0_curve,
+N and s get their gradients.  In .train() mode the F0 / N smoothing of hifigan.py:447-455 is applied on
+both paths (Python's random, as the reference).
 """
 from __future__ import annotations
 
@@ -59,7 +65,7 @@ class Generator(nn.Module):
 
 
 class Decoder(nn.Module):
-    """reference hifigan.py:416-475; forward = HIP decoder (eval semantics)."""
+    """reference hifigan.py:416-475; forward = the fused HIP decoder, or the autograd path (module docstring)."""
 
     decoder_type = "hifigan"
 
@@ -100,4 +106,13 @@ class Decoder(nn.Module):
         None draws it on the device from a counter RNG keyed by (seed, utt_offset + b, sample,
         harmonic); seed None takes one draw from torch's default generator (torch.manual_seed
         governs it and successive calls differ, as the reference's draws do)."""
+        from . import training
+        if torch.is_grad_enabled() and (any(p.requires_grad for p in self.parameters()) or any(
+                isinstance(t, torch.Tensor) and t.requires_grad for t in (asr, F0_curve, N, s))):
+            return training.decoder_forward(self, asr, F0_curve, N, s, noise=noise, seed=seed, utt_offset=utt_offset,
+                                            dtype=dtype)
+        if self.training:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            F0_curve, N = training.train_smooth(torch.as_tensor(F0_curve).to(dev, torch.float32),
+                                                torch.as_tensor(N).to(dev, torch.float32))
         return self.engine(dtype).forward(asr, F0_curve, N, s, noise=noise, seed=seed, utt_offset=utt_offset)

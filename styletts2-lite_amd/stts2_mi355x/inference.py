@@ -111,8 +111,9 @@ def get_style(style_encoder, audio, sr=24000, split_dur=3, dtype="fp32"):
         audio = audio[:MAX_REF_SAMPLES]
 
     def enc(chunks):
-        mel = wave_preprocess_batch(torch.from_numpy(np.stack(chunks)))
-        return style_encoder(mel.unsqueeze(1), dtype=dtype)
+        with torch.no_grad():  # as get_styles (inference.py:194)
+            mel = wave_preprocess_batch(torch.from_numpy(np.stack(chunks)))
+            return style_encoder(mel.unsqueeze(1), dtype=dtype)
 
     if split_dur > 0 and len(audio) / sr >= 4:
         jump = int(sr * split_dur)

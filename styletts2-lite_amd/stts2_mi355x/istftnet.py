@@ -122,4 +122,6 @@ class Decoder(nn.Module):
         return self._engine
 
     def forward(self, asr, F0_curve, N, s, noise=None, seed=None, utt_offset: int = 0, dtype: str = "fp32"):
+        from .engine import forward_only
+        forward_only(self, "istftnet.Decoder")
         return self.engine(dtype).forward(asr, F0_curve, N, s, noise=noise, seed=seed, utt_offset=utt_offset)

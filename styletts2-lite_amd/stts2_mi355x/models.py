@@ -66,6 +66,8 @@ class ProsodyPredictor(nn.Module):
     def forward(self, texts, style, text_lengths, alignment, m=None):
         """reference models.py:417-446: texts = TextEncoder output [B, d_hid, T], style [B, style_dim],
         alignment [B, T, F] -> (duration logits [B, T, max_dur], en [B, d_hid + style_dim, F])."""
+        from .engine import forward_only
+        forward_only(self, "ProsodyPredictor")
         dev = self.F0_proj.weight.device
         texts, style, alignment = (t.to(dev, torch.float32) for t in (texts, style, alignment))
         with torch.no_grad():
@@ -78,6 +80,8 @@ class ProsodyPredictor(nn.Module):
 
     def F0Ntrain(self, x, s, dtype="fp32"):
         """x = en [B, d_hid+style_dim, T], s [B, style_dim] -> (F0 [B,2T], N [B,2T])."""
+        from .engine import forward_only
+        forward_only(self, "ProsodyPredictor.F0Ntrain")
         dev = self.F0_proj.weight.device
         in_dev = x.device
         with torch.no_grad():
@@ -139,4 +143,6 @@ class StyleEncoder(nn.Module):
 
     def forward(self, x, dtype="fp32"):
         """mel [B,1,80,F] -> style [B, style_dim]."""
+        from .engine import forward_only
+        forward_only(self, "StyleEncoder")
         return self.engine(dtype).forward(x)

@@ -1,0 +1,128 @@
+"""Optimizers of the training step (optimizers.py:11-73) with the update on the device as one HIP kernel
+per 32 tensors (stts_adamw_step, include/stts2_train.h).
+
+* `AdamW(params, lr, betas, eps, weight_decay)`: torch.optim.AdamW's arithmetic (single-tensor order, amsgrad
+  off, decoupled weight decay) and its state layout (`step`, `exp_avg`, `exp_avg_sq` per parameter), so
+  `state_dict()` / `load_state_dict()` interoperate with torch.optim.AdamW checkpoints.
+* `MultiOptimizer`, `define_scheduler`, `build_optimizer`: the reference's wrappers (optimizers.py:11-73),
+  building this AdamW with betas (0.0, 0.99), eps 1e-9, weight decay 1e-4 and OneCycleLR schedulers.
+"""
+from __future__ import annotations
+
+import ctypes
+from functools import reduce
+
+import torch
+
+from .engine import _require_device, _stream, check
+from .training import _tl
+
+
+class _AdamWTensor(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_longlong)]
+
+
+class AdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError("amsgrad (the reference does not use it, optimizers.py:66)")
+        if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"invalid AdamW hyper-parameters lr={lr} betas={betas} eps={eps}")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        _require_device()
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            # tensors of one group that share a step count go in one call (a freshly added parameter starts at 1)
+            batches = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("AdamW does not support sparse gradients")
+                if p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous():
+                    raise RuntimeError("HIP AdamW: contiguous fp32 parameters on the device")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                g = p.grad if p.grad.is_contiguous() and p.grad.dtype == torch.float32 else \
+                    p.grad.float().contiguous()
+                batches.setdefault(int(st["step"].item()), []).append((p, g, st["exp_avg"], st["exp_avg_sq"]))
+            for step, items in batches.items():
+                arr = (_AdamWTensor * len(items))()
+                for i, (p, g, m, v) in enumerate(items):
+                    arr[i] = _AdamWTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel())
+                check(_tl().stts_adamw_step(arr, len(items), ctypes.c_float(group["lr"]), ctypes.c_float(beta1),
+                                            ctypes.c_float(beta2), ctypes.c_float(group["eps"]),
+                                            ctypes.c_float(group["weight_decay"]), step, _stream()),
+                      "stts_adamw_step")
+        return loss
+
+
+class MultiOptimizer:
+    """optimizers.py:11-51."""
+
+    def __init__(self, optimizers={}, schedulers={}):
+        self.optimizers = optimizers
+        self.schedulers = schedulers
+        self.keys = list(optimizers.keys())
+        self.param_groups = reduce(lambda x, y: x + y, [v.param_groups for v in self.optimizers.values()])
+
+    def state_dict(self):
+        return [(key, self.optimizers[key].state_dict()) for key in self.keys]
+
+    def load_state_dict(self, state_dict):
+        for key, val in state_dict:
+            try:
+                self.optimizers[key].load_state_dict(val)
+            except Exception:
+                print("Unloaded %s" % key)
+
+    def step(self, key=None, scaler=None):
+        keys = [key] if key is not None else self.keys
+        for k in keys:
+            if scaler is not None:
+                scaler.step(self.optimizers[k])
+                scaler.update()
+            else:
+                self.optimizers[k].step()
+
+    def zero_grad(self, key=None):
+        if key is not None:
+            self.optimizers[key].zero_grad()
+        else:
+            for k in self.keys:
+                self.optimizers[k].zero_grad()
+
+    def scheduler(self, *args, key=None):
+        if key is not None:
+            self.schedulers[key].step(*args)
+        else:
+            for k in self.keys:
+                self.schedulers[k].step(*args)
+
+
+def define_scheduler(optimizer, params):
+    """optimizers.py:53-63."""
+    return torch.optim.lr_scheduler.OneCycleLR(
+        optimizer, max_lr=params.get("max_lr", 2e-4), epochs=params.get("epochs", 200),
+        steps_per_epoch=params.get("steps_per_epoch", 1000), pct_start=params.get("pct_start", 0.0),
+        div_factor=1, final_div_factor=1)
+
+
+def build_optimizer(parameters_dict, scheduler_params_dict, lr):
+    """optimizers.py:65-73 with this module's AdamW."""
+    optim = {key: AdamW(params, lr=lr, weight_decay=1e-4, betas=(0.0, 0.99), eps=1e-9)
+             for key, params in parameters_dict.items()}
+    schedulers = {key: define_scheduler(opt, scheduler_params_dict[key]) for key, opt in optim.items()}
+    return MultiOptimizer(optim, schedulers)

@@ -213,6 +213,8 @@ class LSTM(nn.LSTM):
     """
 
     def forward(self, x, hx=None, lengths=None):
+        from .engine import forward_only
+        forward_only(self, "LSTM")
         if hx is not None:
             raise NotImplementedError("HIP LSTM: only the zero initial state the reference uses (hx=None)")
         if not (self.bidirectional and self.batch_first and self.num_layers == 1 and self.bias
@@ -300,6 +302,8 @@ class TextEncoder(nn.Module):
         return cache[1]
 
     def forward(self, x, input_lengths, m=None):
+        from .engine import forward_only
+        forward_only(self, "TextEncoder")
         if x.dim() != 2:
             raise ValueError(f"tokens must be [B, T], got {tuple(x.shape)}")
         dev = self.embedding.weight.device
@@ -342,6 +346,8 @@ class AdaLayerNorm(nn.Module):
         self.fc = nn.Linear(style_dim, channels * 2)
 
     def forward(self, x, s, lengths=None, extra=None):
+        from .engine import forward_only
+        forward_only(self, "AdaLayerNorm")
         """x [B,T,C] (any strides), s [B,style_dim] -> [B,T,C(+E)]; rows t >= lengths are zero."""
         gb = linear_frames(s.unsqueeze(0), self.fc.weight.detach(), self.fc.bias.detach())[0]
         return row_norm(x, self.channels, 1, gamma=gb, gb_sb=gb.stride(0), eps=self.eps, lengths=lengths,
@@ -364,6 +370,8 @@ class DurationEncoder(nn.Module):
         self.dropout, self.d_model, self.sty_dim = dropout, d_model, sty_dim
 
     def forward(self, x, style, text_lengths, m=None):
+        from .engine import forward_only
+        forward_only(self, "DurationEncoder")
         _on_device(x, "DurationEncoder"), _on_device(style, "DurationEncoder style")
         B, C, T = x.shape
         if C != self.d_model or tuple(style.shape) != (B, self.sty_dim):

@@ -23,6 +23,46 @@ from torch import nn
 from .engine import _ptr, _require_device, _stream, check, lib
 
 _DT = {"fp32": 0, "bf16": 1}
+_TRAIN_READY = False
+
+
+def _tl():
+    """lib() with the argument types of the training-step entry points (include/stts2_train.h)."""
+    global _TRAIN_READY
+    L = lib()
+    if _TRAIN_READY:
+        return L
+    vp, i, ll, f, ull = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_ulonglong
+    sig = {
+        "stts_snake_workspace_bytes": ([i, i, i], ll),
+        "stts_snake_fwd": ([vp, vp, i, i, i, vp, vp], i),
+        "stts_snake_bwd": ([vp, vp, vp, i, i, i, vp, vp, vp, ll, vp], i),
+        "stts_tanh_fwd": ([vp, ll, vp, vp], i),
+        "stts_tanh_bwd": ([vp, vp, ll, vp, vp], i),
+        "stts_sum_div": ([vp, i, ll, f, vp, vp], i),
+        "stts_div": ([vp, ll, f, vp, vp], i),
+        "stts_source_workspace_bytes": ([i, i], ll),
+        "stts_source_fwd": ([vp, vp, vp, vp, ull, ll, i, i, i, vp, vp, vp, ll, vp], i),
+        "stts_source_bwd": ([vp, vp, vp, i, ll, vp, vp, vp, ll, vp], i),
+        "stts_box_smooth_fwd": ([vp, i, i, i, vp, vp], i),
+        "stts_box_smooth_bwd": ([vp, i, i, i, vp, vp], i),
+        "stts_time_expand3": ([vp, i, i, i, i, vp, vp], i),
+        "stts_time_expand3_bwd": ([vp, i, i, i, i, vp, vp], i),
+        "stts_stft_mag_workspace_bytes": ([i, ll, i, i, i], ll),
+        "stts_stft_mag_fwd": ([vp, i, ll, ll, i, i, i, vp, vp, vp], i),
+        "stts_stft_mag_bwd": ([vp, vp, i, ll, i, i, i, vp, vp, ll, vp], i),
+        "stts_mrstft_bwd_workspace_bytes": ([i, ll, vp, vp, vp, i, i], ll),
+        "stts_mrstft_loss_bwd": ([vp, vp, i, ll, ll, vp, vp, vp, i, i, i, vp, vp, vp, ll, vp], i),
+        "stts_gan_workspace_bytes": ([i], ll),
+        "stts_gan_loss": ([vp, i, vp, vp, ll, vp], i),
+        "stts_gan_loss_bwd": ([vp, vp, vp, i, vp, vp, ll, vp], i),
+        "stts_adamw_step": ([vp, i, f, f, f, f, f, ll, vp], i),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes, fn.restype = args, res
+    _TRAIN_READY = True
+    return L
 
 
 def _ws(nbytes: int, device) -> torch.Tensor:
@@ -52,7 +92,15 @@ class _Conv1dFn(torch.autograd.Function):
         ws = _ws(nb, x.device)
         y = torch.empty(B, Lq, Cout, dtype=torch.float32, device=x.device)
         ctx.scale = float(scale)
-        if res is not None or scale != 1.0:
+        if res is not None and dt != 0:
+            # the residual epilogue of stts_conv1d_fwd_res is fp32-only: bf16 runs add it in a second pass
+            check(lib().stts_conv1d_fwd(dt, _ptr(xf), _ptr(wc), _ptr(bc), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
+                                        _ptr(y), _ptr(ws), int(nb), _stream()), "stts_conv1d_fwd")
+            rc = res.detach().to(torch.float32).contiguous()
+            xs = (ctypes.c_void_p * 2)(y.data_ptr(), rc.data_ptr())
+            check(_tl().stts_sum_div(xs, 2, y.numel(), ctypes.c_float(1.0 / scale), _ptr(y), _stream()),
+                  "stts_sum_div")
+        elif res is not None or scale != 1.0:
             rc = res.detach().to(torch.float32).contiguous() if res is not None else None
             check(lib().stts_conv1d_fwd_res(dt, _ptr(xf), _ptr(wc), _ptr(bc), _ptr(rc), ctypes.c_float(scale), B, Lin,
                                             Cin, Cout, K, stride,
@@ -100,6 +148,8 @@ def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="
     conv epilogue."""
     if dtype not in _DT:
         raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
+    if residual is None and scale != 1.0:
+        raise ValueError("conv1d_frames: `scale` applies to the residual sum; pass a residual or scale 1")
     return _Conv1dFn.apply(x, weight, bias, int(stride), int(padding), int(dilation), dtype, residual, float(scale))
 
 
@@ -321,17 +371,23 @@ class AdaINResBlock1(nn.Module):
         self.alpha2 = nn.ParameterList([nn.Parameter(torch.ones(1, channels, 1)) for _ in dilation])
 
     def forward_frames(self, x, s):
-        for c1, c2, n1, n2, a1, a2 in zip(self.convs1, self.convs2, self.adain1, self.adain2, self.alpha1,
-                                          self.alpha2):
-            xt = adain_act(x, s, n1.fc.weight, n1.fc.bias, a1, ACT_SNAKE)
-            xt = conv1d_frames(xt, weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, c1.padding, c1.dilation)
-            xt = adain_act(xt, s, n2.fc.weight, n2.fc.bias, a2, ACT_SNAKE)
-            x = conv1d_frames(xt, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, c2.padding, c2.dilation,
-                              residual=x)  # x = xt + x in convs2's epilogue
-        return x
+        return resblock1_frames(self, x, s)
 
     def forward(self, x, s):
         return self.forward_frames(x.transpose(1, 2), s).transpose(1, 2)
+
+
+def resblock1_frames(m, x, s, dtype="fp32"):
+    """AdaINResBlock1.forward (hifigan.py:65-74) on frames x [B, L, C] for any module with the reference's
+    parameter layout (training.AdaINResBlock1 or the decoder's params.AdaINResBlock1):
+    for each dilation: xt = Snake(AdaIN1(x)); xt = convs1(xt); xt = Snake(AdaIN2(xt)); x = convs2(xt) + x."""
+    for c1, c2, n1, n2, a1, a2 in zip(m.convs1, m.convs2, m.adain1, m.adain2, m.alpha1, m.alpha2):
+        xt = adain_act(x, s, n1.fc.weight, n1.fc.bias, a1, ACT_SNAKE)
+        xt = conv1d_frames(xt, weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, c1.padding, c1.dilation, dtype)
+        xt = adain_act(xt, s, n2.fc.weight, n2.fc.bias, a2, ACT_SNAKE)
+        x = conv1d_frames(xt, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, c2.padding, c2.dilation, dtype,
+                          residual=x)  # x = xt + x in convs2's epilogue
+    return x
 
 
 class _PoolFn(torch.autograd.Function):
@@ -418,20 +474,29 @@ class AdainResBlk1d(nn.Module):
             self.pool = _WNConvT(dim_in)
 
     def forward_frames(self, x, s):
-        r = adain_act(x, s, self.norm1.fc.weight, self.norm1.fc.bias, None, ACT_LRELU)
-        if self.upsample:
-            r = _PoolFn.apply(r, weight_norm(self.pool.weight_g, self.pool.weight_v), self.pool.bias)
-        c1, c2 = self.conv1, self.conv2
-        r = conv1d_frames(r, weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, 1)
-        r = adain_act(r, s, self.norm2.fc.weight, self.norm2.fc.bias, None, ACT_LRELU)
-        sc = _Up2Fn.apply(x) if self.upsample else x
-        if self.learned_sc:
-            sc = conv1d_frames(sc, weight_norm(self.conv1x1.weight_g, self.conv1x1.weight_v), None, 1, 0)
-        return conv1d_frames(r, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, 1, residual=sc,
-                             scale=1 / math.sqrt(2))
+        return adain_resblk1d_frames(self, x, s)
 
     def forward(self, x, s):
         return self.forward_frames(x.transpose(1, 2), s).transpose(1, 2)
+
+
+def adain_resblk1d_frames(m, x, s, dtype="fp32"):
+    """AdainResBlk1d.forward (hifigan.py:384-403, dropout p = 0) on frames x [B, L, C_in] for any module with
+    the reference's parameter layout (training.AdainResBlk1d or params.AdainResBlk1d):
+    out = (conv2(LReLU(AdaIN2(conv1(pool(LReLU(AdaIN1(x))))))) + conv1x1(up2(x))) / sqrt(2), the sum and the
+    scale in conv2's epilogue."""
+    up = m.upsample if isinstance(getattr(m, "upsample", None), bool) else m.upsample_type != "none"
+    r = adain_act(x, s, m.norm1.fc.weight, m.norm1.fc.bias, None, ACT_LRELU)
+    if up:
+        r = _PoolFn.apply(r, weight_norm(m.pool.weight_g, m.pool.weight_v), m.pool.bias)
+    c1, c2 = m.conv1, m.conv2
+    r = conv1d_frames(r, weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, 1, dtype=dtype)
+    r = adain_act(r, s, m.norm2.fc.weight, m.norm2.fc.bias, None, ACT_LRELU)
+    sc = _Up2Fn.apply(x) if up else x
+    if m.learned_sc:
+        sc = conv1d_frames(sc, weight_norm(m.conv1x1.weight_g, m.conv1x1.weight_v), None, 1, 0, dtype=dtype)
+    return conv1d_frames(r, weight_norm(c2.weight_g, c2.weight_v), c2.bias, 1, 1, dtype=dtype, residual=sc,
+                         scale=1 / math.sqrt(2))
 
 
 class _LReLUFn(torch.autograd.Function):
@@ -511,3 +576,374 @@ class DiscriminatorP(nn.Module):
         out = nchw(h)
         fmap.append(out)
         return torch.flatten(out, 1, -1), fmap
+
+
+# ====================================================================== the assembled training step (config 5)
+# train.py:267-327: the decoder forward (Modules/hifigan.py:446-475) with its parameters' gradients, the
+# discriminators (Modules/discriminators.py) with theirs, the losses (losses.py) and AdamW (optimizers.py).
+# Every Function below runs its forward and backward as HIP kernels (include/stts2_train.h).
+
+def _f32(t):
+    return t.detach().to(torch.float32).contiguous()
+
+
+class _SnakeFn(torch.autograd.Function):
+    """Snake with a learned alpha (the Generator's stage activations, hifigan.py:329, :343) on frames."""
+
+    @staticmethod
+    def forward(ctx, x, alpha):
+        _require_device()
+        B, L, C = x.shape
+        xc, ac = _f32(x), _f32(alpha.reshape(-1))
+        y = torch.empty_like(xc)
+        check(_tl().stts_snake_fwd(_ptr(xc), _ptr(ac), B, L, C, _ptr(y), _stream()), "stts_snake_fwd")
+        ctx.save_for_backward(xc, ac)
+        ctx.a_shape = alpha.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, ac = ctx.saved_tensors
+        B, L, C = xc.shape
+        nx, na = ctx.needs_input_grad
+        dyc = _f32(dy)
+        dx = torch.empty_like(xc) if nx else None
+        da = torch.empty(C, dtype=torch.float32, device=dyc.device) if na else None
+        nb = _tl().stts_snake_workspace_bytes(B, L, C)
+        ws = _ws(nb, dyc.device)
+        check(_tl().stts_snake_bwd(_ptr(xc), _ptr(ac), _ptr(dyc), B, L, C, _ptr(dx), _ptr(da), _ptr(ws), int(nb),
+                                   _stream()), "stts_snake_bwd")
+        return dx, (da.reshape(ctx.a_shape) if da is not None else None)
+
+
+def snake(x, alpha):
+    return _SnakeFn.apply(x, alpha)
+
+
+class _TanhFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        _require_device()
+        xc = _f32(x)
+        y = torch.empty_like(xc)
+        check(_tl().stts_tanh_fwd(_ptr(xc), xc.numel(), _ptr(y), _stream()), "stts_tanh_fwd")
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dyc = _f32(dy)
+        dx = torch.empty_like(y)
+        check(_tl().stts_tanh_bwd(_ptr(y), _ptr(dyc), y.numel(), _ptr(dx), _stream()), "stts_tanh_bwd")
+        return dx
+
+
+def tanh(x):
+    return _TanhFn.apply(x)
+
+
+class _SumDivFn(torch.autograd.Function):
+    """(x0 + x1 + ...) / div, added left to right (x + x_source, hifigan.py:334; xs / num_kernels, :342)."""
+
+    @staticmethod
+    def forward(ctx, div, *xs):
+        _require_device()
+        xc = [_f32(x) for x in xs]
+        for x in xc[1:]:
+            if x.shape != xc[0].shape:
+                raise ValueError(f"sum of tensors of shapes {[tuple(t.shape) for t in xc]}")
+        y = torch.empty_like(xc[0])
+        arr = (ctypes.c_void_p * len(xc))(*[x.data_ptr() for x in xc])
+        check(_tl().stts_sum_div(arr, len(xc), y.numel(), ctypes.c_float(div), _ptr(y), _stream()), "stts_sum_div")
+        ctx.div, ctx.n = float(div), len(xc)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.div == 1.0:
+            g = dy
+        else:
+            dyc = _f32(dy)
+            g = torch.empty_like(dyc)
+            check(_tl().stts_div(_ptr(dyc), dyc.numel(), ctypes.c_float(ctx.div), _ptr(g), _stream()), "stts_div")
+        return (None,) + tuple(g if need else None for need in ctx.needs_input_grad[1:])
+
+
+def sum_div(xs, div=1.0):
+    return _SumDivFn.apply(float(div), *xs)
+
+
+class _SourceFn(torch.autograd.Function):
+    """SourceModuleHnNSF (hifigan.py:221-268): f0_curve [B, n] -> har [B, n*scale]; gradients for l_linear."""
+
+    @staticmethod
+    def forward(ctx, f0_curve, lw, lb, noise, seed, utt_offset, scale):
+        _require_device()
+        B, n = f0_curve.shape
+        L = n * scale
+        fc, wc, bc = _f32(f0_curve), _f32(lw.reshape(-1)), _f32(lb.reshape(-1))
+        nz = _f32(noise) if noise is not None else None
+        if nz is not None and tuple(nz.shape) != (B, L, 9):
+            raise ValueError(f"noise {tuple(nz.shape)}: expected {(B, L, 9)}")
+        sw = torch.empty(B, L, 9, dtype=torch.float32, device=fc.device)
+        har = torch.empty(B, L, dtype=torch.float32, device=fc.device)
+        nb = _tl().stts_source_workspace_bytes(B, n)
+        ws = _ws(nb, fc.device)
+        check(_tl().stts_source_fwd(_ptr(fc), _ptr(wc), _ptr(bc), _ptr(nz), ctypes.c_ulonglong(int(seed) & (2**64 - 1)),
+                                    int(utt_offset), B, n, int(scale), _ptr(sw), _ptr(har), _ptr(ws), int(nb),
+                                    _stream()), "stts_source_fwd")
+        ctx.save_for_backward(sw, har)
+        ctx.shapes = (lw.shape, lb.shape, n)
+        return har
+
+    @staticmethod
+    def backward(ctx, dhar):
+        sw, har = ctx.saved_tensors
+        lw_shape, lb_shape, n = ctx.shapes
+        B, L = har.shape
+        nw, nbias = ctx.needs_input_grad[1:3]
+        if not (nw or nbias):
+            return (None,) * 7
+        d = _f32(dhar)
+        dW = torch.empty(9, dtype=torch.float32, device=d.device)
+        db = torch.empty(1, dtype=torch.float32, device=d.device)
+        nbytes = _tl().stts_source_workspace_bytes(B, n)
+        ws = _ws(nbytes, d.device)
+        check(_tl().stts_source_bwd(_ptr(sw), _ptr(har), _ptr(d), B, L, _ptr(dW), _ptr(db), _ptr(ws), int(nbytes),
+                                    _stream()), "stts_source_bwd")
+        return None, (dW.reshape(lw_shape) if nw else None), (db.reshape(lb_shape) if nbias else None), None, None, \
+            None, None
+
+
+class _BoxFn(torch.autograd.Function):
+    """conv1d(x, ones(1, 1, k), padding k // 2) / k per row (the train-mode smoothing, hifigan.py:453-455)."""
+
+    @staticmethod
+    def forward(ctx, x, k):
+        _require_device()
+        xc = _f32(x)
+        B, n = xc.shape
+        y = torch.empty_like(xc)
+        check(_tl().stts_box_smooth_fwd(_ptr(xc), B, n, int(k), _ptr(y), _stream()), "stts_box_smooth_fwd")
+        ctx.k = int(k)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        d = _f32(dy)
+        B, n = d.shape
+        dx = torch.empty_like(d)
+        check(_tl().stts_box_smooth_bwd(_ptr(d), B, n, ctx.k, _ptr(dx), _stream()), "stts_box_smooth_bwd")
+        return dx, None
+
+
+def box_smooth(x, k):
+    return _BoxFn.apply(x, int(k))
+
+
+def train_smooth(F0_curve, N, rng=None):
+    """Decoder.forward's train-mode branch (hifigan.py:447-455): F0_down from [0, 3, 7] and N_down from
+    [0, 3, 7, 15], drawn with Python's `random.randint` in the reference's order (so random.seed governs
+    them), then the box smoothing on the device."""
+    import random as _random
+    r = rng or _random
+    F0_down = [0, 3, 7][r.randint(0, 2)]
+    N_down = [0, 3, 7, 15][r.randint(0, 3)]
+    if F0_down:
+        F0_curve = box_smooth(F0_curve, F0_down)
+    if N_down:
+        N = box_smooth(N, N_down)
+    return F0_curve, N
+
+
+class _TimeExpandFn(torch.autograd.Function):
+    """x3[s][h][w][c*3 + dh] = y[s][h + dh - 1][w][c]: a (3, kw) Conv2d as a 1-D conv over 3C channels."""
+
+    @staticmethod
+    def forward(ctx, y):
+        _require_device()
+        yc = _f32(y)
+        S, H, W, C = yc.shape
+        x3 = torch.empty(S, H, W, 3 * C, dtype=torch.float32, device=yc.device)
+        check(_tl().stts_time_expand3(_ptr(yc), S, H, W, C, _ptr(x3), _stream()), "stts_time_expand3")
+        ctx.shape = (S, H, W, C)
+        return x3
+
+    @staticmethod
+    def backward(ctx, dx3):
+        S, H, W, C = ctx.shape
+        d = _f32(dx3)
+        dy = torch.empty(S, H, W, C, dtype=torch.float32, device=d.device)
+        check(_tl().stts_time_expand3_bwd(_ptr(d), S, H, W, C, _ptr(dy), _stream()), "stts_time_expand3_bwd")
+        return dy
+
+
+class _StftMagFn(torch.autograd.Function):
+    """|torch.stft(x, n_fft, hop, win, hann(win))| (discriminators.py:11-27) as the [S, F, nb] image."""
+
+    @staticmethod
+    def forward(ctx, wave, n_fft, hop, win):
+        _require_device()
+        w = _f32(wave)
+        S, L = w.shape
+        F_ = 1 + L // hop
+        nb = n_fft // 2 + 1
+        mag = torch.empty(S, F_, nb, dtype=torch.float32, device=w.device)
+        spec = torch.empty(S, F_, nb, 2, dtype=torch.float32, device=w.device)
+        check(_tl().stts_stft_mag_fwd(_ptr(w), S, L, L, n_fft, win, hop, _ptr(mag), _ptr(spec), _stream()),
+              "stts_stft_mag_fwd")
+        ctx.save_for_backward(spec)
+        ctx.geo = (S, L, n_fft, win, hop)
+        return mag
+
+    @staticmethod
+    def backward(ctx, dmag):
+        (spec,) = ctx.saved_tensors
+        S, L, n_fft, win, hop = ctx.geo
+        d = _f32(dmag)
+        dw = torch.empty(S, L, dtype=torch.float32, device=d.device)
+        nb = _tl().stts_stft_mag_workspace_bytes(S, L, n_fft, win, hop)
+        check(int(nb) if nb < 0 else 0, "stts_stft_mag_workspace_bytes")
+        ws = _ws(nb, d.device)
+        check(_tl().stts_stft_mag_bwd(_ptr(spec), _ptr(d), S, L, n_fft, win, hop, _ptr(dw), _ptr(ws), int(nb),
+                                      _stream()), "stts_stft_mag_bwd")
+        return dw, None, None, None
+
+
+def stft_mag(wave, n_fft, hop, win):
+    return _StftMagFn.apply(wave, int(n_fft), int(hop), int(win))
+
+
+# ---------------------------------------------------------------------- decoder (Modules/hifigan.py)
+def _wn_w(layer):
+    return weight_norm(layer.weight_g, layer.weight_v)
+
+
+def generator_forward(g, x, s, f0_curve, noise=None, seed=0, utt_offset=0, dtype="fp32"):
+    """Generator.forward (hifigan.py:321-347) on frames x [B, 2T, 512] for a module with the reference's
+    parameter layout (stts2_mi355x.hifigan.Generator) -> waveform frames [B, L, 1]."""
+    rates, kernels = g.upsample_rates, g.upsample_kernel_sizes
+    nk = g.num_kernels
+    scale = int(g.upsample_scale)
+    har = _SourceFn.apply(f0_curve, g.m_source.l_linear.weight, g.m_source.l_linear.bias, noise, seed, utt_offset,
+                          scale).unsqueeze(-1)  # frames [B, L, 1]
+    B = har.shape[0]
+    for i, (u, k) in enumerate(zip(rates, kernels)):
+        x = snake(x, g.alphas[i])
+        nc = g.noise_convs[i]
+        S, P = int(nc.stride), int(nc.padding)
+        if S > 1 and nc.weight.shape[-1] == 2 * S and 2 * P == S:
+            # Conv1d(1, C, 2S, stride S, padding S/2) (hifigan.py:296-299) as a 2-tap stride-1 conv over
+            # S-sample frames: frame r = samples [r S - P, r S - P + S), w'[c][j][t] = w[c][0][t S + j]
+            fr = torch.nn.functional.pad(har[..., 0], (P, S - P)).reshape(B, -1, S)
+            w2 = nc.weight.reshape(nc.weight.shape[0], 2, S).transpose(1, 2)
+            x_src = conv1d_frames(fr, w2, nc.bias, 1, 0, 1, dtype)
+        else:
+            x_src = conv1d_frames(har, nc.weight, nc.bias, nc.stride, nc.padding, 1, dtype)
+        x_src = resblock1_frames(g.noise_res[i], x_src, s, dtype)
+        up = g.ups[i]
+        x = conv_transpose1d_frames(x, _wn_w(up), up.bias, up.stride, up.padding, up.output_padding, dtype)
+        x = sum_div([x, x_src])
+        rs = [resblock1_frames(g.resblocks[i * nk + j], x, s, dtype) for j in range(nk)]
+        x = sum_div(rs, nk)
+    x = snake(x, g.alphas[len(rates)])
+    cp = g.conv_post
+    x = conv1d_frames(x, _wn_w(cp), cp.bias, 1, cp.padding, 1, dtype)
+    return tanh(x)
+
+
+def decoder_forward(dec, asr, F0_curve, N, s, noise=None, seed=None, utt_offset=0, dtype="fp32"):
+    """Decoder.forward (hifigan.py:446-475) with autograd through HIP kernels: asr [B, 512, T], F0_curve and
+    N [B, 2T], s [B, style_dim] -> [B, 1, 600 T].  `dec` is stts2_mi355x.hifigan.Decoder (reference
+    parameter names); in .train() mode the F0 / N smoothing of :447-455 is applied first (Python's random,
+    as the reference).  Activations stay in frames [B, L, C] end to end."""
+    _require_device()
+    if dtype not in _DT:
+        raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if noise is None else 0
+    if dec.training:
+        F0_curve, N = train_smooth(F0_curve, N)
+    B, _, T = asr.shape
+    if F0_curve.shape[-1] != 2 * T or N.shape[-1] != 2 * T:
+        raise ValueError(f"F0_curve / N {tuple(F0_curve.shape)} / {tuple(N.shape)}: expected [B, {2 * T}]")
+    F0 = conv1d_frames(F0_curve.unsqueeze(-1), _wn_w(dec.F0_conv), dec.F0_conv.bias, 2, 1, 1, dtype)  # [B, T, 1]
+    Nc = conv1d_frames(N.unsqueeze(-1), _wn_w(dec.N_conv), dec.N_conv.bias, 2, 1, 1, dtype)
+    asr_f = asr.transpose(1, 2)  # frames [B, T, 512]
+    x = torch.cat([asr_f, F0, Nc], dim=2)
+    x = adain_resblk1d_frames(dec.encode, x, s, dtype)
+    ar = dec.asr_res[0]
+    asr_res = conv1d_frames(asr_f, _wn_w(ar), ar.bias, 1, 0, 1, dtype)
+    res = True
+    for block in dec.decode:
+        if res:
+            x = torch.cat([x, asr_res, F0, Nc], dim=2)
+        x = adain_resblk1d_frames(block, x, s, dtype)
+        if block.upsample_type != "none":
+            res = False
+    y = generator_forward(dec.generator, x, s, F0_curve, noise, seed, utt_offset, dtype)  # [B, L, 1]
+    return y.reshape(B, 1, -1)
+
+
+# ---------------------------------------------------------------------- discriminators
+def _k1_geom(layer):
+    """(k, stride, pad) of a (k, 1) Conv2d: the reference's nn.Conv2d or training._WNConv2dK1."""
+    if hasattr(layer, "kernel_size"):
+        return layer.kernel_size[0], layer.stride[0], layer.padding[0]
+    return layer.k, layer.stride, layer.pad
+
+
+def discriminator_p_forward(m, x, period, dtype="fp32"):
+    """DiscriminatorP.forward (discriminators.py:110-129) for a module with the reference's parameter layout:
+    x [B, 1, T] -> (score [B, H*p], fmap: 6 maps [B, C, H, p], permuted views of frames [B*p, H, C])."""
+    b, c, t = x.shape
+    p = period
+    if t % p != 0:
+        x = torch.nn.functional.pad(x, (0, p - t % p), "reflect")  # discriminators.py:112-115
+        t = x.shape[-1]
+    h = x.reshape(b, c, t // p, p).permute(0, 3, 2, 1).reshape(b * p, t // p, c)
+    fmap = []
+
+    def nchw(f):
+        return f.reshape(b, p, f.shape[1], f.shape[2]).permute(0, 3, 2, 1)
+
+    for layer in m.convs:
+        k, st, pad = _k1_geom(layer)
+        w = _wn_w(layer)
+        h = conv1d_frames(h, w.reshape(w.shape[0], w.shape[1], k), layer.bias, st, pad, dtype=dtype)
+        h = leaky_relu(h, 0.1)
+        fmap.append(nchw(h))
+    cp = m.conv_post
+    k, st, pad = _k1_geom(cp)
+    w = _wn_w(cp)
+    h = conv1d_frames(h, w.reshape(1, w.shape[1], k), cp.bias, st, pad, dtype=dtype)
+    out = nchw(h)
+    fmap.append(out)
+    return torch.flatten(out, 1, -1), fmap
+
+
+def spec_discriminator_forward(m, y, dtype="fp32"):
+    """SpecDiscriminator.forward (discriminators.py:49-63) for the reference's parameter layout: y [B, 1, T]
+    -> (score [B, F*W5], fmap: 6 maps [B, C, F, W], permuted views of frames [B, F, W, C]).  The |STFT|
+    image is [B, F frames, nb bins]; each (3, kw) Conv2d is a 1-D conv along the bins over the 3 C
+    time-expanded channels (x3[..., c*3 + dh] = row h + dh - 1), so the weight [Cout, C, 3, kw] is the
+    [Cout, 3C, kw] conv1d weight as it lies in memory."""
+    y = y.reshape(y.shape[0], -1)
+    S = y.shape[0]
+    h = stft_mag(y, m.fft_size, m.shift_size, m.win_length).unsqueeze(-1)  # [S, F, nb, 1]
+    Fr = h.shape[1]
+    fmap = []
+    layers = list(m.discriminators) + [m.out]
+    for j, layer in enumerate(layers):
+        x3 = _TimeExpandFn.apply(h)  # [S, F, W, 3C]
+        W3 = x3.shape[2]
+        w = _wn_w(layer)
+        co, ci, kh, kw = w.shape
+        out = conv1d_frames(x3.reshape(S * Fr, W3, 3 * ci), w.reshape(co, ci * kh, kw), layer.bias,
+                            layer.stride[1], layer.padding[1], dtype=dtype)
+        if j < len(layers) - 1:
+            out = leaky_relu(out, 0.1)
+        h = out.reshape(S, Fr, out.shape[1], co)
+        fmap.append(h.permute(0, 3, 1, 2))
+    return h.reshape(S, -1), fmap

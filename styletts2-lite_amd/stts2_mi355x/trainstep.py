@@ -1,0 +1,78 @@
+"""One fine-tune step of the decoder against the discriminators, as train.py:267-327 runs it (BASELINE
+config 5), over the drop-in modules: the HIP decoder (hifigan.Decoder, autograd path), the MPD / MSD
+(discriminators.py), the losses (losses.py) and AdamW (optim.py).
+
+    step = TrainStep(decoder, mpd, msd)
+    losses = step(en, F0_fake, N_fake, s, wav)   # en [B, 512, T], F0 / N [B, 2T], s [B, style_dim], wav [B, 1, 600 T]
+
+does, in the reference's order:
+    y_rec = decoder(en, F0_fake, N_fake, s)                                     (train.py:267)
+    zero_grad; d_loss = dl(wav.detach(), y_rec.detach()).mean(); backward;
+    AdamW step on msd, mpd                                                       (:272-276)
+    zero_grad; loss_mel = stft_loss(y_rec, wav); loss_gen_all = gl(wav, y_rec).mean();
+    g_loss = lambda_mel loss_mel + lambda_gen loss_gen_all; backward; AdamW on the decoder   (:278-325)
+The other modules of train.py (text aligner, predictor, style encoder) are outside this path: their
+outputs come in as tensors, and their gradients (en.grad, F0.grad, N.grad, s.grad) are left on the inputs
+when those require grad.  `freeze_d_in_g` (default) turns off requires_grad of the discriminator parameters
+during the G step: the reference computes those gradients and discards them (its next iteration starts
+with zero_grad before they are used), so skipping them changes no update.
+"""
+from __future__ import annotations
+
+import torch
+
+from .losses import DiscriminatorLoss, GeneratorLoss, MultiResolutionSTFTLoss
+from .optim import AdamW
+
+
+class TrainStep:
+    def __init__(self, decoder, mpd, msd, lr_dec=1e-5, lr_disc=1e-4, lambda_mel=5.0, lambda_gen=1.0, dtype="fp32",
+                 freeze_d_in_g=True, capture=False):
+        self.decoder, self.mpd, self.msd = decoder, mpd, msd
+        self.capture = capture  # keep copies of the gradients each optimizer step consumed (tests)
+        self.captured = {}
+        self.dtype = dtype
+        mpd.dtype_compute = msd.dtype_compute = dtype
+        self.gl, self.dl = GeneratorLoss(mpd, msd), DiscriminatorLoss(mpd, msd)
+        self.stft_loss = MultiResolutionSTFTLoss()
+        mk = lambda m, lr: AdamW(m.parameters(), lr=lr, weight_decay=1e-4, betas=(0.0, 0.99), eps=1e-9)  # noqa: E731
+        self.opt = {"decoder": mk(decoder, lr_dec), "mpd": mk(mpd, lr_disc), "msd": mk(msd, lr_disc)}
+        self.lambda_mel, self.lambda_gen = float(lambda_mel), float(lambda_gen)
+        self.freeze_d_in_g = freeze_d_in_g
+
+    def zero_grad(self):
+        for o in self.opt.values():
+            o.zero_grad()
+
+    def __call__(self, en, F0, N, s, wav, noise=None, seed=None):
+        y_rec = self.decoder(en, F0, N, s, noise=noise, seed=seed, dtype=self.dtype)
+        self.zero_grad()
+        d_loss = self.dl(wav.detach(), y_rec.detach()).mean()
+        d_loss.backward()
+        if self.capture:
+            for tag, m in (("mpd", self.mpd), ("msd", self.msd)):
+                self.captured[tag] = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+        self.opt["msd"].step()
+        self.opt["mpd"].step()
+        self.zero_grad()
+        frozen = []
+        if self.freeze_d_in_g:
+            for m in (self.mpd, self.msd):
+                for p in m.parameters():
+                    if p.requires_grad:
+                        p.requires_grad_(False)
+                        frozen.append(p)
+        try:
+            loss_mel = self.stft_loss(y_rec, wav)
+            loss_gen_all = self.gl(wav, y_rec).mean()
+            g_loss = self.lambda_mel * loss_mel + self.lambda_gen * loss_gen_all
+            g_loss.backward()
+        finally:
+            for p in frozen:
+                p.requires_grad_(True)
+        if self.capture:
+            self.captured["dec"] = {k: p.grad.detach().clone() for k, p in self.decoder.named_parameters()
+                                    if p.grad is not None}
+        self.opt["decoder"].step()
+        return {"y_rec": y_rec.detach(), "d_loss": d_loss.detach(), "loss_mel": loss_mel.detach(),
+                "loss_gen_all": loss_gen_all.detach(), "g_loss": g_loss.detach()}

@@ -152,4 +152,6 @@ class Decoder(nn.Module):
     def forward(self, asr, F0_curve, N, s, dtype: str = "fp32"):
         """asr [B,512,T], F0_curve [B,2T], N [B,2T], s [B,style_dim] -> [B,1,2T*hop] (float32).
         The Vocos decoder has no harmonic source, so it draws no noise."""
+        from .engine import forward_only
+        forward_only(self, "vocos.Decoder")
         return self.engine(dtype).forward(asr, F0_curve, N, s)

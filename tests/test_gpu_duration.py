@@ -10,6 +10,13 @@ from stts2_mi355x import synth
 from stts2_mi355x.prosody import LSTM, matmul
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _inference():
+    """These modules' HIP paths are forward-only (engine.forward_only): run as inference.py does."""
+    with torch.no_grad():
+        yield
 TOL = 1e-4
 
 

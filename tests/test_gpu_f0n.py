@@ -9,6 +9,13 @@ from stts2_mi355x import synth
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _inference():
+    """These modules' HIP paths are forward-only (engine.forward_only): run as inference.py does."""
+    with torch.no_grad():
+        yield
+
+
 def predictor():
     from stts2_mi355x.models import ProsodyPredictor
     return fill_module(ProsodyPredictor(style_dim=128, d_hid=512, nlayers=3, max_dur=50, dropout=0.2)).eval().cuda()

@@ -9,6 +9,13 @@ from stts2_mi355x import synth
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _inference():
+    """These modules' HIP paths are forward-only (engine.forward_only): run as inference.py does."""
+    with torch.no_grad():
+        yield
+
+
 @pytest.mark.parametrize("Fr,B", [(80, 2), (241, 1)])
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_style_encoder(Fr, B, dtype):

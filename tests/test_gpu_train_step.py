@@ -1,0 +1,425 @@
+"""GPU parity of the assembled training step (BASELINE config 5) through the C-ABI:
+
+* each new HIP autograd piece (Snake with learned alpha, tanh, branch sums, the source module, the
+  train-mode smoothing, the MSD time expansion, |STFT|, the GAN loss terms incl. TPRLS, the
+  multi-resolution mel loss, AdamW) against torch autograd of the oracle / torch in fp64 on the CPU;
+* the whole decoder's parameter and input gradients, and the MPD / MSD gradients, against autograd
+  through the oracle (fp32, CPU), which tests/test_train_oracle_cpu.py pins bit-exactly to the
+  reference's own autograd;
+* one D + G step (train.py:267-327 with AdamW) against the reference fixture tests/golden/
+  train_step_B2_T8.npz (made by tests/golden/make_golden_train.py from the reference modules);
+* the full config-5 shape (B = 2 x 93,000 samples) against the oracle's step.
+
+Tolerances: fp32 gradients within 1e-4 of the tensor's max |g| (floored at 1e-3 of the largest max |g| of
+the module: parameters whose true gradient is ~0, e.g. a conv bias feeding an InstanceNorm, carry only
+rounding noise); the mel loss is parity-unpinned upstream (torchaudio is absent: DESIGN §6e).
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import HIFI_CFG, fill_module, golden, make_decoder
+from oracle import stts_oracle as orc
+from stts2_mi355x import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b, floor=0.0):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), floor, 1e-30))
+
+
+def _waves(B, L, seed):
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_golden_mpd import waves
+    return torch.from_numpy(waves(B, L, seed))
+
+
+def _train_inputs(B, T):
+    asr, f0, n, s = (torch.from_numpy(a) for a in synth.decoder_inputs(B, T, tag="train"))
+    L = 600 * T
+    return asr, f0, n, s, _waves(B, L, 7), torch.from_numpy(synth.source_noise(B, L, tag="train_noise"))
+
+
+def _discs():
+    from stts2_mi355x.discriminators import MultiPeriodDiscriminator, MultiResSpecDiscriminator
+    return fill_module(MultiPeriodDiscriminator(), "mpd."), fill_module(MultiResSpecDiscriminator(), "msd.")
+
+
+def _sd(m):
+    return {k: v.detach().clone().cpu() for k, v in m.state_dict().items()}
+
+
+def _check_grads(ours, ref, tol=1e-4, what=""):
+    gmax = max(float(g.abs().max()) for g in ref.values() if g is not None)
+    worst = (0.0, None)
+    for k, g in ref.items():
+        if g is None:
+            assert ours.get(k) is None, k
+            continue
+        assert ours.get(k) is not None, f"{what}: no gradient for {k}"
+        e = _rel(ours[k], g, floor=1e-3 * gmax)
+        worst = max(worst, (e, k))
+    print(f"{what}: worst gradient error {worst[0]:.2e} ({worst[1]}), {len(ref)} tensors, max |g| {gmax:.3e}")
+    assert worst[0] < tol, worst
+
+
+# ------------------------------------------------------------------ the pieces
+def test_snake_tanh_sum():
+    from stts2_mi355x import training as T
+    torch.manual_seed(0)
+    x = torch.randn(2, 300, 48, dtype=torch.float64)
+    a = (0.5 + torch.rand(1, 48, 1, dtype=torch.float64))
+    gy = torch.randn(2, 300, 48, dtype=torch.float64)
+    xd, ad = x.float().cuda().requires_grad_(True), a.float().cuda().requires_grad_(True)
+    y = T.snake(xd, ad)
+    y.backward(gy.float().cuda())
+    xr, ar = x.clone().requires_grad_(True), a.clone().requires_grad_(True)
+    yr = orc.snake(xr.transpose(1, 2), ar).transpose(1, 2)
+    yr.backward(gy)
+    assert _rel(y.detach(), yr.detach()) < 1e-6
+    assert _rel(xd.grad, xr.grad) < 1e-5 and _rel(ad.grad, ar.grad) < 1e-5
+    # tanh, sum / average
+    t = torch.randn(1000, device="cuda", requires_grad=True)
+    T.tanh(t).sum().backward()
+    tr = t.detach().cpu().double().requires_grad_(True)
+    torch.tanh(tr).sum().backward()
+    assert _rel(t.grad, tr.grad) < 1e-6
+    xs = [torch.randn(5, 7, device="cuda", requires_grad=True) for _ in range(3)]
+    out = T.sum_div(xs, 3)
+    c = [v.detach().cpu() for v in xs]
+    assert torch.equal(out.detach().cpu(), ((c[0] + c[1]) + c[2]) / 3)  # the reference's CPU rounding (a true division)
+    out.sum().backward()
+    assert all(torch.allclose(v.grad, torch.full_like(v, 1 / 3)) for v in xs)
+
+
+@pytest.mark.parametrize("k", [3, 7, 15])
+def test_box_smooth(k):
+    from stts2_mi355x import training as T
+    torch.manual_seed(k)
+    x = torch.randn(3, 50, dtype=torch.float64)
+    g = torch.randn(3, 50, dtype=torch.float64)
+    xd = x.float().cuda().requires_grad_(True)
+    y = T.box_smooth(xd, k)
+    y.backward(g.float().cuda())
+    xr = x.clone().requires_grad_(True)
+    yr, _ = orc.train_smooth(xr, xr, k, 0)
+    yr.backward(g)
+    assert _rel(y.detach(), yr.detach()) < 1e-6 and _rel(xd.grad, xr.grad) < 1e-6
+
+
+def test_source_module_grads():
+    from stts2_mi355x import training as T
+    B, n = 2, 16
+    _, f0, _, _ = synth.decoder_inputs(B, n // 2, tag="train")
+    f0 = torch.from_numpy(f0)
+    L = 300 * n
+    noise = torch.from_numpy(synth.source_noise(B, L, tag="src"))
+    W = torch.randn(1, 9) * 0.3
+    b = torch.randn(1) * 0.1
+    gy = torch.randn(B, L)
+    Wd, bd = W.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    har = T._SourceFn.apply(f0.cuda(), Wd, bd, noise.cuda(), 0, 0, 300)
+    har.backward(gy.cuda())
+    Wr, br = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = orc.sine_source(f0, {"m.l_linear.weight": Wr, "m.l_linear.bias": br}, "m", 300, noise)[..., 0]
+    ref.backward(gy)
+    assert _rel(har.detach(), ref.detach()) < 1e-5
+    assert _rel(Wd.grad, Wr.grad) < 1e-4 and _rel(bd.grad, br.grad) < 1e-4
+
+
+def test_time_expand():
+    from stts2_mi355x import training as T
+    torch.manual_seed(1)
+    y = torch.randn(2, 9, 13, 5, dtype=torch.float64)
+    g = torch.randn(2, 9, 13, 15, dtype=torch.float64)
+    yd = y.float().cuda().requires_grad_(True)
+    x3 = T._TimeExpandFn.apply(yd)
+    x3.backward(g.float().cuda())
+    yr = y.clone().requires_grad_(True)
+    pad = torch.nn.functional.pad(yr, (0, 0, 0, 0, 1, 1))
+    ref = torch.stack([pad[:, dh:dh + 9] for dh in range(3)], dim=-1).reshape(2, 9, 13, 15)
+    ref.backward(g)
+    assert _rel(x3.detach(), ref.detach()) < 1e-7 and _rel(yd.grad, yr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("res", orc.MSD_RES)
+@pytest.mark.parametrize("L", [4800, 4801])
+def test_stft_mag_grads(res, L):
+    from stts2_mi355x import training as T
+    n_fft, hop, win = res
+    torch.manual_seed(L)
+    x = torch.randn(3, L, dtype=torch.float64)
+    xd = x.float().cuda().requires_grad_(True)
+    mag = T.stft_mag(xd, n_fft, hop, win)
+    g = torch.randn(mag.shape, dtype=torch.float64)
+    mag.backward(g.float().cuda())
+    xr = x.clone().requires_grad_(True)
+    ref = torch.stft(xr, n_fft, hop, win, torch.hann_window(win, dtype=torch.float64), return_complex=True)
+    ref = ref.abs().transpose(1, 2)
+    ref.backward(g)
+    assert _rel(mag.detach(), ref.detach()) < 1e-5
+    assert _rel(xd.grad, xr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("scale", [0.01, 3.0])  # TPRLS active (L_rel < tau) / inactive
+def test_gan_terms(scale):
+    from stts2_mi355x import losses as Lo
+    torch.manual_seed(int(scale * 100))
+    # fp32, as the reference computes: the TPRLS mask `dr < dg + m` decides the median element itself by
+    # the rounding of dg + m, so the checker must see the same fp32 values
+    shapes = [(2, 37), (2, 101), (2, 640)]
+    dr = [torch.randn(s) * scale for s in shapes]
+    dg = [torch.randn(s) * scale for s in shapes]
+    fr = [[torch.randn(2, 8, 11, 3), torch.randn(2, 1, 11, 3)]]
+    fg = [[torch.randn(2, 8, 11, 3), torch.randn(2, 1, 11, 3)]]
+
+    def both(fn_ours, fn_ref, *lists):
+        flat = [t for lst in lists for t in (lst if isinstance(lst[0], torch.Tensor) else [u for v in lst for u in v])]
+        dev = [t.float().cuda().requires_grad_(True) for t in flat]
+        ref = [t.clone().requires_grad_(True) for t in flat]
+
+        def rebuild(ts):
+            out, i = [], 0
+            for lst in lists:
+                if isinstance(lst[0], torch.Tensor):
+                    out.append(ts[i:i + len(lst)])
+                    i += len(lst)
+                else:
+                    grp = []
+                    for v in lst:
+                        grp.append(ts[i:i + len(v)])
+                        i += len(v)
+                    out.append(grp)
+            return out
+        lo = fn_ours(*rebuild(dev))
+        lr = fn_ref(*rebuild(ref))
+        lo.backward()
+        lr.backward()
+        assert abs(float(lo.detach()) - float(lr.detach())) <= 1e-5 * max(1.0, abs(float(lr.detach())))
+        for a, b in zip(dev, ref):
+            assert _rel(a.grad, b.grad, floor=1e-12) < 1e-5
+        return float(lr)
+
+    both(lambda r, g: Lo.discriminator_loss(r, g)[0], orc.discriminator_loss, dr, dg)
+    both(lambda g: Lo.generator_loss(g)[0], orc.generator_loss, dg)
+    both(Lo.feature_loss, orc.feature_loss, fr, fg)
+    v1 = both(Lo.discriminator_TPRLS_loss, orc.discriminator_tprls_loss, dr, dg)
+    v2 = both(Lo.generator_TPRLS_loss, orc.generator_tprls_loss, dr, dg)
+    if scale < 1:
+        assert v1 < 3 * orc.TAU and v2 < 3 * orc.TAU  # the relu is active: the gradients are not zero
+
+
+def test_mrstft_loss_grad():
+    from stts2_mi355x.losses import MultiResolutionSTFTLoss
+    x = _waves(2, 4800, 3)[:, 0] * 0.7
+    y = _waves(2, 4800, 4)[:, 0]
+    xd = x.cuda().requires_grad_(True)
+    loss = MultiResolutionSTFTLoss()(xd, y.cuda())
+    loss.backward()
+    xr = x.clone().requires_grad_(True)
+    lr = orc.mrstft_loss(xr, y)
+    lr.backward()
+    assert abs(float(loss) - float(lr)) < 1e-5 * abs(float(lr))
+    print("mrstft grad rel err", _rel(xd.grad, xr.grad))
+    assert _rel(xd.grad, xr.grad) < 1e-3
+
+
+def test_adamw_matches_torch():
+    from stts2_mi355x.optim import AdamW
+    torch.manual_seed(5)
+    shapes = [(1000,), (33, 7), (1,), (4097,)]
+    ps = [torch.randn(s) for s in shapes]
+    pd = [p.clone().cuda().requires_grad_(True) for p in ps]
+    pc = [p.clone().requires_grad_(True) for p in ps]
+    od = AdamW(pd, lr=1e-4, betas=(0.0, 0.99), eps=1e-9, weight_decay=1e-4)
+    oc = torch.optim.AdamW(pc, lr=1e-4, betas=(0.0, 0.99), eps=1e-9, weight_decay=1e-4, foreach=False)
+    for it in range(3):
+        gs = [torch.randn(s) * 10 ** (-it) for s in shapes]
+        for a, b, g in zip(pd, pc, gs):
+            a.grad, b.grad = g.cuda(), g.clone()
+        od.step()
+        oc.step()
+    for a, b in zip(pd, pc):
+        d = (a.detach().cpu() - b.detach()).abs().max().item()
+        assert d <= 2e-7 * max(1.0, b.abs().max().item()), d
+    sd = od.state_dict()
+    assert sd["state"][0]["step"].item() == 3 and set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+
+
+# ------------------------------------------------------------------ whole modules vs the oracle's autograd
+def test_decoder_grads_vs_oracle():
+    B, T = 2, 8
+    dec, _ = make_decoder("hifigan")
+    sd = _sd(dec)
+    asr, f0, n, s, _, noise = _train_inputs(B, T)
+    r = torch.from_numpy(synth.normal("dec_probe", (B, 1, 600 * T))).float()
+    dec = dec.cuda().eval()
+    ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
+    y = dec(*ins, noise=noise.cuda())
+    (y * r.cuda()).sum().backward()
+    # the oracle, fp32 autograd
+    leaf = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ir = [t.clone().requires_grad_(True) for t in (asr, f0, n, s)]
+    yr = orc.decoder_hifigan(*ir, leaf, HIFI_CFG, noise)
+    (yr * r).sum().backward()
+    assert _rel(y.detach(), yr.detach()) < 1e-4
+    _check_grads({k: p.grad for k, p in dec.named_parameters()}, {k: v.grad for k, v in leaf.items()},
+                 what="decoder params")
+    _check_grads({i: t.grad for i, t in enumerate(ins)}, {i: t.grad for i, t in enumerate(ir)}, what="decoder inputs")
+
+
+def test_decoder_train_mode_smoothing():
+    """.train() applies hifigan.py:447-455 with Python's random: replay the same draws into the oracle."""
+    B, T = 1, 8
+    dec, _ = make_decoder("hifigan")
+    sd = _sd(dec)
+    asr, f0, n, s, _, noise = _train_inputs(B, T)
+    dec = dec.cuda().train()
+    for seed in (1, 2, 3):
+        random.seed(seed)
+        with torch.no_grad():
+            y = dec(asr.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=noise.cuda())
+        random.seed(seed)
+        smooth = ([0, 3, 7][random.randint(0, 2)], [0, 3, 7, 15][random.randint(0, 3)])
+        ref = orc.decoder_hifigan(asr, f0, n, s, sd, HIFI_CFG, noise, smooth=smooth)
+        print("smoothing", smooth, _rel(y, ref))
+        assert _rel(y.cpu(), ref) < 1e-4
+    # with autograd: the smoothing sits in the graph (d F0_curve passes through the box filter)
+    random.seed(7)
+    f0d = f0.cuda().requires_grad_(True)
+    y = dec(asr.cuda(), f0d, n.cuda(), s.cuda(), noise=noise.cuda())
+    y.sum().backward()
+    random.seed(7)
+    smooth = ([0, 3, 7][random.randint(0, 2)], [0, 3, 7, 15][random.randint(0, 3)])
+    f0r = f0.clone().requires_grad_(True)
+    orc.decoder_hifigan(asr, f0r, n, s, sd, HIFI_CFG, noise, smooth=smooth).sum().backward()
+    assert _rel(f0d.grad, f0r.grad) < 1e-4
+
+
+def test_discriminator_grads_vs_oracle():
+    from stts2_mi355x.losses import DiscriminatorLoss
+    mpd, msd = _discs()
+    psd, ssd = _sd(mpd), _sd(msd)
+    y = _waves(2, 4801, 0)
+    yh = _waves(2, 4801, 1)
+    mpd, msd = mpd.cuda(), msd.cuda()
+    loss = DiscriminatorLoss(mpd, msd)(y.cuda(), yh.cuda())
+    loss.backward()
+    lp = {k: v.clone().requires_grad_(True) for k, v in psd.items()}
+    ls = {k: v.clone().requires_grad_(True) for k, v in ssd.items()}
+    lr = orc.discriminator_loss_all(y, yh, lp, ls)
+    lr.backward()
+    assert abs(float(loss) - float(lr)) < 1e-4 * abs(float(lr))
+    _check_grads({k: p.grad for k, p in mpd.named_parameters()}, {k: v.grad for k, v in lp.items()}, what="mpd")
+    _check_grads({k: p.grad for k, p in msd.named_parameters()}, {k: v.grad for k, v in ls.items()}, what="msd")
+
+
+def test_generator_loss_input_grad_vs_oracle():
+    """GeneratorLoss w.r.t. y_hat through both discriminators (the G step's path into the decoder)."""
+    from stts2_mi355x.losses import GeneratorLoss
+    mpd, msd = _discs()
+    psd, ssd = _sd(mpd), _sd(msd)
+    y = _waves(2, 4800, 0)
+    yh = _waves(2, 4800, 1)
+    mpd, msd = mpd.cuda().requires_grad_(False), msd.cuda().requires_grad_(False)
+    yhd = yh.cuda().requires_grad_(True)
+    loss = GeneratorLoss(mpd, msd)(y.cuda(), yhd)
+    loss.backward()
+    yhr = yh.clone().requires_grad_(True)
+    lr = orc.generator_loss_all(y, yhr, psd, ssd)
+    lr.backward()
+    assert abs(float(loss) - float(lr)) < 1e-4 * abs(float(lr))
+    print("generator loss d/dy_hat rel err", _rel(yhd.grad, yhr.grad))
+    assert _rel(yhd.grad, yhr.grad) < 1e-4
+
+
+# ------------------------------------------------------------------ the assembled step
+def _summary_check(ours, fx, tag, floor_frac=1e-3, tol=1e-4):
+    names = [str(k) for k in fx[f"{tag}.names"]]
+    gmax = float(fx[f"{tag}.maxabs"].max())
+    worst = (0.0, "")
+    for i, k in enumerate(names):
+        g = ours[k].detach().double().cpu().reshape(-1)
+        scale = max(float(fx[f"{tag}.maxabs"][i]), floor_frac * gmax)
+        e_val = float((g[torch.from_numpy(fx[f"{tag}.idx"][i])] - torch.from_numpy(fx[f"{tag}.val"][i])).abs().max())
+        e_l2 = abs(float(g.norm()) - float(fx[f"{tag}.l2"][i])) / max(float(fx[f"{tag}.l2"][i]), scale)
+        worst = max(worst, (e_val / scale, k), (e_l2, k + " (l2)"))
+    print(f"{tag}: worst {worst[0]:.2e} at {worst[1]} ({len(names)} tensors)")
+    assert worst[0] < tol, worst
+
+
+def test_train_step_vs_reference_fixture():
+    """One D + G step with AdamW (train.py:267-327) against the reference's own autograd and torch AdamW."""
+    from stts2_mi355x.trainstep import TrainStep
+    fx = golden("train_step_B2_T8")
+    B, T = int(fx["B"]), int(fx["T"])
+    dec, _ = make_decoder("hifigan")
+    mpd, msd = _discs()
+    p0 = {k: v.detach().clone() for k, v in dec.state_dict().items()}
+    m0 = {k: v.detach().clone() for k, v in mpd.state_dict().items()}
+    dec, mpd, msd = dec.cuda().eval(), mpd.cuda().train(), msd.cuda().train()
+    asr, f0, n, s, wav, noise = _train_inputs(B, T)
+    ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
+    step = TrainStep(dec, mpd, msd, capture=True)
+    out = step(*ins, wav.cuda(), noise=noise.cuda())
+    torch.cuda.synchronize()
+    assert _rel(out["y_rec"], fx["y_rec"]) < 1e-4
+    for k in ("d_loss", "loss_mel", "loss_gen_all", "g_loss"):
+        assert abs(float(out[k]) - float(fx[k])) <= 1e-4 * abs(float(fx[k])), (k, float(out[k]), float(fx[k]))
+    _summary_check(step.captured["mpd"], fx, "grad.mpd")
+    _summary_check(step.captured["msd"], fx, "grad.msd")
+    _summary_check(step.captured["dec"], fx, "grad.dec")
+    for i, k in enumerate(("asr", "F0_curve", "N", "s")):
+        e = _rel(ins[i].grad, fx["grad_in." + k])
+        print("input grad", k, e)
+        assert e < 1e-4
+    # the AdamW updates (first step: ~ -lr sign(g) - lr wd p) where the gradient is well above rounding
+    # (tolerance: 2 fp32 ulps of the parameter; the update itself is ~ lr = 1e-5 / 1e-4)
+    names = [str(k) for k in fx["grad.dec.names"]]
+    sd1 = dec.state_dict()
+    for i, k in enumerate(names):
+        ix = torch.from_numpy(fx["grad.dec.idx"][i])
+        old = p0[k].double().reshape(-1)[ix]
+        d = sd1[k].cpu().double().reshape(-1)[ix] - old
+        sig = np.abs(fx["grad.dec.val"][i]) > 1e-3 * float(fx["grad.dec.maxabs"][i])
+        tol = 2.4e-7 * np.abs(old.numpy()) + 1e-12
+        assert (np.abs(d.numpy() - fx["grad.dec.delta"][i]) <= tol)[sig].all(), k
+    md = mpd.state_dict()
+    for i, k in enumerate(sorted(m0)):
+        ix = torch.from_numpy(np.minimum((synth.hash_u01("probe_idx." + k, 24) * m0[k].numel()).astype(np.int64),
+                                         m0[k].numel() - 1))
+        old = m0[k].double().reshape(-1)[ix]
+        d = md[k].cpu().double().reshape(-1)[ix] - old
+        tol = 2.4e-7 * np.abs(old.numpy()) + 1e-12
+        ok = np.abs(d.numpy() - fx["mpd.delta"][i]) <= tol
+        assert ok.mean() >= 0.9, k  # entries whose gradient sits at rounding level may take the other sign
+
+
+def test_train_step_config5_shape():
+    """The config-5 shape (B = 2 segments of 155 frames = 93,000 samples, train.py:235 max_len 310) vs the
+    oracle's step on the CPU."""
+    from stts2_mi355x.trainstep import TrainStep
+    B, T = 2, 155
+    dec, _ = make_decoder("hifigan")
+    mpd, msd = _discs()
+    sds = (_sd(dec), _sd(mpd), _sd(msd))
+    asr, f0, n, s, wav, noise = _train_inputs(B, T)
+    dec, mpd, msd = dec.cuda().eval(), mpd.cuda().train(), msd.cuda().train()
+    ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
+    step = TrainStep(dec, mpd, msd, capture=True)
+    out = step(*ins, wav.cuda(), noise=noise.cuda())
+    torch.cuda.synchronize()
+    y_o, l_o, g_o, _ = orc.train_step(*sds, HIFI_CFG, asr, f0, n, s, wav, noise)
+    assert _rel(out["y_rec"].cpu(), y_o) < 1e-4
+    for k in ("d_loss", "loss_mel", "loss_gen_all"):
+        print(k, float(out[k]), l_o[k])
+        assert abs(float(out[k]) - l_o[k]) <= 1e-3 * abs(l_o[k]), k
+    _check_grads(step.captured["mpd"], g_o["mpd"], tol=1e-3, what="config5 mpd")
+    _check_grads(step.captured["msd"], g_o["msd"], tol=1e-3, what="config5 msd")
+    _check_grads(step.captured["dec"], g_o["dec"], tol=1e-3, what="config5 decoder")

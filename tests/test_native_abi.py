@@ -1,6 +1,7 @@
-"""CPU tests of the C-ABI library: it loads, exports every symbol include/stts2.h declares,
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/*.h declares,
 and its model plans name exactly the reference state-dict keys (no GPU compute here)."""
 import ctypes
+import glob
 import os
 import re
 
@@ -14,15 +15,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "stts2.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(stts_[a-z0-9_]+)\s*\(", src)))
+    out = set()
+    for h in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))):
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        out |= set(re.findall(r"\b(stts_[a-z0-9_]+)\s*\(", src))
+    return sorted(out)
 
 
 def test_library_exports_all_declared_symbols():
     L = E.lib()
     syms = declared_symbols()
-    assert len(syms) >= 14
+    assert len(syms) >= 14 + 20  # stts2.h + stts2_train.h
     for s in syms:
         assert hasattr(L, s), f"libstts2.so does not export {s}"
 

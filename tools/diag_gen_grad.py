@@ -1,0 +1,49 @@
+"""Diagnostic: d GeneratorLoss / d y_hat per loss component (HIP vs the oracle's fp32 autograd)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd"), os.path.join(ROOT, "tests"),
+                os.path.join(ROOT, "tests", "golden")]
+import torch  # noqa: E402
+
+from helpers import fill_module  # noqa: E402
+from make_golden_mpd import waves  # noqa: E402
+from oracle import stts_oracle as orc  # noqa: E402
+from stts2_mi355x import losses as Lo  # noqa: E402
+from stts2_mi355x.discriminators import MultiPeriodDiscriminator, MultiResSpecDiscriminator  # noqa: E402
+
+mpd, msd = fill_module(MultiPeriodDiscriminator(), "mpd."), fill_module(MultiResSpecDiscriminator(), "msd.")
+psd = {k: v.detach().clone() for k, v in mpd.state_dict().items()}
+ssd = {k: v.detach().clone() for k, v in msd.state_dict().items()}
+mpd, msd = mpd.cuda().requires_grad_(False), msd.cuda().requires_grad_(False)
+y, yh = torch.from_numpy(waves(2, 4800, 0)), torch.from_numpy(waves(2, 4800, 1))
+for name, disc, sdict, odisc in (("mpd", mpd, psd, orc.mpd), ("msd", msd, ssd, orc.msd)):
+    for comp in ("feat", "gen", "tprls"):
+        yd = yh.cuda().requires_grad_(True)
+        r, g, fr, fg = disc(y.cuda(), yd)
+        if comp == "feat":
+            l = Lo.feature_loss(fr, fg)
+        elif comp == "gen":
+            l = Lo.generator_loss(g)[0]
+        else:
+            l = Lo.generator_TPRLS_loss(r, g)
+        l.backward()
+        yr = yh.clone().requires_grad_(True)
+        r2, g2, fr2, fg2 = odisc(y, yr, sdict)
+        if comp == "feat":
+            l2 = orc.feature_loss(fr2, fg2)
+        elif comp == "gen":
+            l2 = orc.generator_loss(g2)
+        else:
+            l2 = orc.generator_tprls_loss(r2, g2)
+        l2.backward()
+        e = (yd.grad.cpu() - yr.grad).abs().max().item() / yr.grad.abs().max().item()
+        print(f"{name} {comp}: loss {float(l.detach()):.6f} vs {float(l2.detach()):.6f}  grad rel err {e:.2e}")
+        if comp == "tprls":
+            for i, (a, b) in enumerate(zip(r2, g2)):
+                d = b - a
+                m = torch.median(d)
+                sel = (b < a + m)
+                Lr = (((d - m) ** 2)[sel]).mean().item()
+                print(f"   disc {i}: n {d.numel()} n_sel {int(sel.sum())} L_rel {Lr:.4f} (active {Lr < 0.04})")
