@@ -114,7 +114,8 @@ int stts_mpd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, floa
 /* GAN losses over stts_mpd_fwd's output for a batch of 2B = B real then B generated waveforms,
  * <- losses.py:97-128 feature_loss(fmap_r, fmap_g), generator_loss(y_d_gs)[0] and
  * discriminator_loss(y_d_rs, y_d_gs)[0] over the MultiPeriodDiscriminator outputs.  loss (device,
- * 3 doubles) = {feature, generator, discriminator}; scratch (device) >= 4 * 6 * n_periods doubles. */
+ * 3 doubles) = {feature, generator, discriminator}; scratch (device) >= 64 * 4 * 6 * n_periods doubles
+ * (per-block partial sums, added in block order: the result is bitwise reproducible). */
 int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
                     void* stream);
 
@@ -223,7 +224,8 @@ int stts_weight_norm_bwd(const float* g, const float* v, const float* dw, int d0
 long long stts_msd_out_elems(const stts_model* m, int B, int T);
 int stts_msd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, float* out, long long out_elems,
                  void* workspace, long long ws_bytes, void* stream);
-/* The GAN losses of stts_mpd_losses over stts_msd_fwd's output (losses.py:97-128 with the MSD outputs). */
+/* The GAN losses of stts_mpd_losses over stts_msd_fwd's output (losses.py:97-128 with the MSD outputs);
+ * scratch >= 64 * 4 * 6 * n_resolutions doubles. */
 int stts_msd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
                     void* stream);
 

@@ -95,6 +95,9 @@ def sine_source(f0_curve, sd, p, upsample_scale: int, noise):
     downsample reads samples 300j+149/150 only, so it never reaches the output (measured
     diff 0.0); it is omitted.  Returns har [B, L, 1] (pre-transpose)."""
     with torch.no_grad():  # SourceModuleHnNSF.forward runs l_sin_gen under no_grad (hifigan.py:262-263)
+        # (always in fp32, the reference's dtype: an fp64 run of the oracle, the training tests' truth,
+        # keeps the reference's fp32 phase quantisation, SURVEY App. B)
+        f0_curve, noise = f0_curve.float(), noise.float()
         f0 = F.interpolate(f0_curve[:, None], scale_factor=upsample_scale).transpose(1, 2)  # nearest, [B,L,1]
         fn = torch.multiply(f0, torch.FloatTensor([[range(1, 10)]]))
         rad_values = (fn / 24000) % 1
@@ -107,7 +110,8 @@ def sine_source(f0_curve, sd, p, upsample_scale: int, noise):
         uv = (f0 > 10).type(torch.float32)
         noise_amp = uv * 0.003 + (1 - uv) * 0.1 / 3
         sine_waves = sine_waves * uv + noise_amp * noise
-    return torch.tanh(F.linear(sine_waves, _t(sd, p + ".l_linear.weight"), _t(sd, p + ".l_linear.bias")))
+    w = _t(sd, p + ".l_linear.weight")
+    return torch.tanh(F.linear(sine_waves.to(w.dtype), w, _t(sd, p + ".l_linear.bias")))
 
 
 # ----------------------------------------------------------------------------------
@@ -680,11 +684,12 @@ def mel_spectrogram_sr(wave, sample_rate, n_fft, win_length, hop_length, n_mels=
     """torchaudio.transforms.MelSpectrogram(sample_rate, n_fft, win_length, hop_length, window_fn=hann)
     at its other defaults (losses.py:43): f_min 0, f_max sr // 2, power 2, center/reflect, HTK, no norm."""
     lead = wave.shape[:-1]  # torchaudio packs the leading dims into one batch dim around torch.stft
-    spec = torch.stft(wave.reshape(-1, wave.shape[-1]), n_fft, hop_length, win_length, torch.hann_window(win_length),
+    spec = torch.stft(wave.reshape(-1, wave.shape[-1]), n_fft, hop_length, win_length,
+                      torch.hann_window(win_length, dtype=wave.dtype),
                       center=True, pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
     spec = spec.reshape(lead + spec.shape[-2:])
     power = spec.abs().pow(2.0)
-    fb = melscale_fbanks(n_fft // 2 + 1, 0.0, float(sample_rate // 2), n_mels, sample_rate)
+    fb = melscale_fbanks(n_fft // 2 + 1, 0.0, float(sample_rate // 2), n_mels, sample_rate).to(power.dtype)
     return torch.matmul(power.transpose(-1, -2), fb).transpose(-1, -2)
 
 
@@ -712,7 +717,7 @@ def spec_discriminator(y, sd, prefix, fft_size, hop, win):
     """SpecDiscriminator.forward (Modules/discriminators.py:47-63): |torch.stft| image [B, 1, frames,
     bins] -> 4 Conv2d (3, 9) [strides (1,1), (1,2) x 3] + LReLU(0.1) -> Conv2d (3, 3) + LReLU -> out."""
     y = y.squeeze(1)
-    y = torch.stft(y, fft_size, hop, win, torch.hann_window(win), return_complex=True)  # stft() :11-27
+    y = torch.stft(y, fft_size, hop, win, torch.hann_window(win, dtype=y.dtype), return_complex=True)  # stft() :11-27
     y = torch.abs(y).transpose(2, 1).unsqueeze(1)
     fmap = []
     for j in range(5):

@@ -726,9 +726,12 @@ int st_period_frames(const float* wave, int B, int Tn, int p, int L0, void* dst,
 // output holds the real half then the generated half (same element order), so
 //   feature_loss = 2 sum_blocks mean|r - g|,  generator_loss = sum_periods mean((1 - g)^2),
 //   discriminator_loss = sum_periods mean((1 - r)^2) + mean(g^2)   (scores = the conv_post blocks)
-// Per-block sums: fp32 per thread, fp64 per workgroup (atomics); k_mpd_loss_final combines them.
+// Per-block sums: fp32 per thread, fp64 per workgroup, written as per-(segment, block) partials;
+// k_mpd_loss_final adds the blocks of each segment in block order (deterministic run to run).
+constexpr int kMpdLossBlocks = 64;
+
 __global__ void __launch_bounds__(256) k_mpd_loss_sums(const float* __restrict__ out, MpdLossSegs sg,
-                                                       double* __restrict__ sums) {
+                                                       double* __restrict__ part) {
   const int seg = blockIdx.y;
   if (seg >= sg.n) return;
   const long long half = sg.half[seg];
@@ -754,18 +757,22 @@ __global__ void __launch_bounds__(256) k_mpd_loss_sums(const float* __restrict__
   __syncthreads();
   if (threadIdx.x < 4) {
     const int k = threadIdx.x;
-    atomicAdd(sums + seg * 4 + k, (double)red[k][0] + red[k][1] + red[k][2] + red[k][3]);
+    part[((size_t)seg * kMpdLossBlocks + blockIdx.x) * 4 + k] =
+        (((double)red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
   }
 }
 
-__global__ void k_mpd_loss_final(MpdLossSegs sg, const double* __restrict__ sums, double* __restrict__ loss) {
+__global__ void k_mpd_loss_final(MpdLossSegs sg, const double* __restrict__ part, double* __restrict__ loss) {
   double fm = 0, gen = 0, disc = 0;
   for (int s = 0; s < sg.n; ++s) {
+    double sums[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < kMpdLossBlocks; ++j)
+      for (int k = 0; k < 4; ++k) sums[k] += part[((size_t)s * kMpdLossBlocks + j) * 4 + k];
     const double n = (double)sg.half[s];
-    fm += sums[s * 4] / n;
+    fm += sums[0] / n;
     if (sg.score[s]) {
-      gen += sums[s * 4 + 2] / n;
-      disc += (sums[s * 4 + 1] + sums[s * 4 + 3]) / n;
+      gen += sums[2] / n;
+      disc += (sums[1] + sums[3]) / n;
     }
   }
   loss[0] = 2.0 * fm;
@@ -773,11 +780,11 @@ __global__ void k_mpd_loss_final(MpdLossSegs sg, const double* __restrict__ sums
   loss[2] = disc;
 }
 
-int st_mpd_losses(const float* out, const MpdLossSegs& sg, double* sums, double* loss, hipStream_t s) {
+int st_mpd_losses(const float* out, const MpdLossSegs& sg, double* part, double* loss, hipStream_t s) {
   if (sg.n <= 0 || sg.n > kMpdMaxSegs) return ST_EINVAL;
-  ST_CHECK_HIP(hipMemsetAsync(sums, 0, sizeof(double) * 4 * sg.n, s));
-  hipLaunchKernelGGL(k_mpd_loss_sums, dim3(64, sg.n), dim3(256), 0, s, out, sg, sums);
-  hipLaunchKernelGGL(k_mpd_loss_final, dim3(1), dim3(1), 0, s, sg, sums, loss);
+  hipLaunchKernelGGL(k_mpd_loss_sums, dim3(kMpdLossBlocks, sg.n), dim3(256), 0, s, out, sg, part);
+  ST_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_mpd_loss_final, dim3(1), dim3(1), 0, s, sg, part, loss);
   return (int)hipGetLastError();
 }
 

@@ -481,7 +481,7 @@ class MPDEngine(_Engine):
         out, B2, T = self.last
         if B2 % 2:
             raise ValueError("the last forward's batch is not real + generated halves")
-        scratch = torch.zeros(4 * 6 * len(self.periods), dtype=torch.float64, device=out.device)
+        scratch = torch.empty(64 * 4 * 6 * len(self.periods), dtype=torch.float64, device=out.device)
         loss = torch.empty(3, dtype=torch.float64, device=out.device)
         check(lib().stts_mpd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), _ptr(loss), _stream()),
               "stts_mpd_losses")
@@ -547,7 +547,7 @@ class MSDEngine(_Engine):
         out, B2, T = self.last
         if B2 % 2:
             raise ValueError("the last forward's batch is not real + generated halves")
-        scratch = torch.zeros(4 * 6 * len(self.res), dtype=torch.float64, device=out.device)
+        scratch = torch.empty(64 * 4 * 6 * len(self.res), dtype=torch.float64, device=out.device)
         loss = torch.empty(3, dtype=torch.float64, device=out.device)
         check(lib().stts_msd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), _ptr(loss), _stream()),
               "stts_msd_losses")

@@ -24,6 +24,14 @@ from .engine import _ptr, _require_device, _stream, check, lib
 
 _DT = {"fp32": 0, "bf16": 1}
 _TRAIN_READY = False
+# algorithmic conv work of the autograd path (measurement: tools/bench_train_step.py): 2 B Lq Cout Cin K flops per
+# conv forward, the same again per dx and per dw (the transposed conv: 2 B Lin Cin Cout K)
+CONV_FLOPS = {"on": False, "fwd": 0.0, "bwd": 0.0}
+
+
+def _count(kind, flops):
+    if CONV_FLOPS["on"]:
+        CONV_FLOPS[kind] += flops
 
 
 def _tl():
@@ -111,6 +119,7 @@ class _Conv1dFn(torch.autograd.Function):
                                         _ptr(y), _ptr(ws), int(nb), _stream()), "stts_conv1d_fwd")
         ctx.save_for_backward(xf, wc)
         ctx.geo = (B, Lin, Cin, Cout, K, stride, dil, pad, Lq, dt, bias is not None)
+        _count("fwd", 2.0 * B * Lq * Cout * Cin * K)
         return y
 
     @staticmethod
@@ -130,6 +139,7 @@ class _Conv1dFn(torch.autograd.Function):
         db = torch.empty(Cout, dtype=torch.float32, device=dev) if (need_b and has_bias) else None
         check(lib().stts_conv1d_bwd(dt, _ptr(xf), _ptr(wc), _ptr(dyf), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
                                     _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()), "stts_conv1d_bwd")
+        _count("bwd", 2.0 * B * Lq * Cout * Cin * K * ((dx is not None) + (dw is not None)))
         return dx, dw, db, None, None, None, None, (gy if ctx.needs_input_grad[7] else None), None
 
 
@@ -189,6 +199,7 @@ class _ConvT1dFn(torch.autograd.Function):
               "stts_conv_transpose1d_fwd")
         ctx.save_for_backward(xf, wc)
         ctx.geo = (B, Lin, Cin, Cout, K, stride, pad, Lout, dt, bias is not None)
+        _count("fwd", 2.0 * B * Lin * Cin * Cout * K)
         return y
 
     @staticmethod
@@ -205,6 +216,7 @@ class _ConvT1dFn(torch.autograd.Function):
         check(lib().stts_conv_transpose1d_bwd(dt, _ptr(xf), _ptr(wc), _ptr(dy), B, Lin, Cin, Cout, K, stride, pad,
                                               Lout, _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()),
               "stts_conv_transpose1d_bwd")
+        _count("bwd", 2.0 * B * Lin * Cin * Cout * K * ((dx is not None) + (dw is not None)))
         return dx, dw, db, None, None, None, None
 
 

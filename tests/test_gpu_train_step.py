@@ -55,7 +55,7 @@ def _sd(m):
     return {k: v.detach().clone().cpu() for k, v in m.state_dict().items()}
 
 
-def _check_grads(ours, ref, tol=1e-4, what=""):
+def _check_grads(ours, ref, tol=1e-4, what="", floor_frac=1e-3):
     gmax = max(float(g.abs().max()) for g in ref.values() if g is not None)
     worst = (0.0, None)
     for k, g in ref.items():
@@ -63,10 +63,33 @@ def _check_grads(ours, ref, tol=1e-4, what=""):
             assert ours.get(k) is None, k
             continue
         assert ours.get(k) is not None, f"{what}: no gradient for {k}"
-        e = _rel(ours[k], g, floor=1e-3 * gmax)
+        e = _rel(ours[k], g, floor=floor_frac * gmax)
         worst = max(worst, (e, k))
     print(f"{what}: worst gradient error {worst[0]:.2e} ({worst[1]}), {len(ref)} tensors, max |g| {gmax:.3e}")
     assert worst[0] < tol, worst
+
+
+def _sd64(sd):
+    return {k: v.double() for k, v in sd.items()}
+
+
+def _check3(ours, r32, r64, what, slack=2.0, abs_tol=1e-4):
+    """Gradients vs the oracle's fp64 autograd (the truth), next to the reference's own fp32 error: the
+    reference in fp32 is itself 1.6e-4 (decoder) to 3.3e-4 (MSD) of max |g| away from fp64 at T = 8
+    (tests/golden/make_golden_train.py's case), so 'as close as the reference' means
+    err(ours, fp64) <= max(slack * err(fp32 reference, fp64), abs_tol) per tensor (same floor as _check_grads)."""
+    gmax = max(float(g.abs().max()) for g in r64.values() if g is not None)
+    worst, worst_ref = (0.0, None), (0.0, None)
+    for k, g in r64.items():
+        if g is None:
+            continue
+        assert ours.get(k) is not None, f"{what}: no gradient for {k}"
+        eo = _rel(ours[k], g, floor=1e-3 * gmax)
+        er = _rel(r32[k], g, floor=1e-3 * gmax)
+        worst, worst_ref = max(worst, (eo, k)), max(worst_ref, (er, k))
+        assert eo <= max(slack * er, abs_tol), (k, eo, er)
+    print(f"{what}: vs fp64, ours worst {worst[0]:.2e} ({worst[1]}), fp32 reference worst {worst_ref[0]:.2e} "
+          f"({worst_ref[1]}), {len(r64)} tensors")
 
 
 # ------------------------------------------------------------------ the pieces
@@ -254,6 +277,8 @@ def test_adamw_matches_torch():
 
 # ------------------------------------------------------------------ whole modules vs the oracle's autograd
 def test_decoder_grads_vs_oracle():
+    """Every decoder parameter gradient and the input gradients (asr, F0_curve, N, s) of a fixed linear
+    probe of the output, vs autograd through the oracle in fp64 (next to its fp32 run = the reference)."""
     B, T = 2, 8
     dec, _ = make_decoder("hifigan")
     sd = _sd(dec)
@@ -263,15 +288,17 @@ def test_decoder_grads_vs_oracle():
     ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
     y = dec(*ins, noise=noise.cuda())
     (y * r.cuda()).sum().backward()
-    # the oracle, fp32 autograd
-    leaf = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
-    ir = [t.clone().requires_grad_(True) for t in (asr, f0, n, s)]
-    yr = orc.decoder_hifigan(*ir, leaf, HIFI_CFG, noise)
-    (yr * r).sum().backward()
-    assert _rel(y.detach(), yr.detach()) < 1e-4
-    _check_grads({k: p.grad for k, p in dec.named_parameters()}, {k: v.grad for k, v in leaf.items()},
-                 what="decoder params")
-    _check_grads({i: t.grad for i, t in enumerate(ins)}, {i: t.grad for i, t in enumerate(ir)}, what="decoder inputs")
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        leaf = {k: v.detach().to(dt).clone().requires_grad_(True) for k, v in sd.items()}
+        ir = [t.detach().to(dt).clone().requires_grad_(True) for t in (asr, f0, n, s)]
+        yr = orc.decoder_hifigan(*ir, leaf, HIFI_CFG, noise)
+        (yr * r.to(dt)).sum().backward()
+        refs[dt] = (yr.detach(), {k: v.grad for k, v in leaf.items()}, {i: t.grad for i, t in enumerate(ir)})
+    assert _rel(y.detach(), refs[torch.float64][0]) < 1e-4
+    _check3({k: p.grad for k, p in dec.named_parameters()}, refs[torch.float32][1], refs[torch.float64][1],
+            "decoder params")
+    _check3({i: t.grad for i, t in enumerate(ins)}, refs[torch.float32][2], refs[torch.float64][2], "decoder inputs")
 
 
 def test_decoder_train_mode_smoothing():
@@ -321,7 +348,8 @@ def test_discriminator_grads_vs_oracle():
 
 
 def test_generator_loss_input_grad_vs_oracle():
-    """GeneratorLoss w.r.t. y_hat through both discriminators (the G step's path into the decoder)."""
+    """GeneratorLoss w.r.t. y_hat through both discriminators (the G step's path into the decoder), vs the
+    oracle in fp64 next to its fp32 run (the |STFT| adjoint is ill-conditioned at near-zero bins: dX = g X / |X|)."""
     from stts2_mi355x.losses import GeneratorLoss
     mpd, msd = _discs()
     psd, ssd = _sd(mpd), _sd(msd)
@@ -331,27 +359,61 @@ def test_generator_loss_input_grad_vs_oracle():
     yhd = yh.cuda().requires_grad_(True)
     loss = GeneratorLoss(mpd, msd)(y.cuda(), yhd)
     loss.backward()
-    yhr = yh.clone().requires_grad_(True)
-    lr = orc.generator_loss_all(y, yhr, psd, ssd)
-    lr.backward()
-    assert abs(float(loss) - float(lr)) < 1e-4 * abs(float(lr))
-    print("generator loss d/dy_hat rel err", _rel(yhd.grad, yhr.grad))
-    assert _rel(yhd.grad, yhr.grad) < 1e-4
+    grads, vals = {}, {}
+    for dt in (torch.float32, torch.float64):
+        yhr = yh.detach().to(dt).clone().requires_grad_(True)
+        lr = orc.generator_loss_all(y.to(dt), yhr, _sd64(psd) if dt == torch.float64 else psd,
+                                    _sd64(ssd) if dt == torch.float64 else ssd)
+        lr.backward()
+        grads[dt], vals[dt] = yhr.grad, float(lr)
+    assert abs(float(loss) - vals[torch.float64]) < 1e-4 * abs(vals[torch.float64])
+    _check3({"y_hat": yhd.grad}, {"y_hat": grads[torch.float32]}, {"y_hat": grads[torch.float64]}, "d GeneratorLoss / d y_hat")
 
 
 # ------------------------------------------------------------------ the assembled step
-def _summary_check(ours, fx, tag, floor_frac=1e-3, tol=1e-4):
+def _summary_check(ours, fx, tag, floor_frac=1e-3, tol=1e-4, norm_tol=None):
+    """Per tensor: the values at the fixture's probe indices and the L2 norm, relative to the tensor's max
+    |g| (floored at floor_frac of the module's).  norm_tol: also the error relative to the module's max |g|."""
     names = [str(k) for k in fx[f"{tag}.names"]]
     gmax = float(fx[f"{tag}.maxabs"].max())
-    worst = (0.0, "")
+    worst, worst_n = (0.0, ""), (0.0, "")
     for i, k in enumerate(names):
         g = ours[k].detach().double().cpu().reshape(-1)
         scale = max(float(fx[f"{tag}.maxabs"][i]), floor_frac * gmax)
         e_val = float((g[torch.from_numpy(fx[f"{tag}.idx"][i])] - torch.from_numpy(fx[f"{tag}.val"][i])).abs().max())
         e_l2 = abs(float(g.norm()) - float(fx[f"{tag}.l2"][i])) / max(float(fx[f"{tag}.l2"][i]), scale)
         worst = max(worst, (e_val / scale, k), (e_l2, k + " (l2)"))
-    print(f"{tag}: worst {worst[0]:.2e} at {worst[1]} ({len(names)} tensors)")
+        worst_n = max(worst_n, (e_val / gmax, k))
+    print(f"{tag}: worst {worst[0]:.2e} at {worst[1]}, module-normwise {worst_n[0]:.2e} ({len(names)} tensors)")
     assert worst[0] < tol, worst
+    if norm_tol is not None:
+        assert worst_n[0] < norm_tol, worst_n
+
+
+def test_d_step_on_reference_output():
+    """The D step alone on the reference's own y_rec (the fixture's): DiscriminatorLoss (losses.py:170-190)
+    backward through the MPD and MSD, vs the oracle's fp64 autograd next to its fp32 run (the reference's
+    computation: bit for bit on the survey container's CPU, tests/test_train_oracle_cpu.py; another CPU's
+    BLAS rounds differently)."""
+    from stts2_mi355x.losses import DiscriminatorLoss
+    fx = golden("train_step_B2_T8")
+    B, T = int(fx["B"]), int(fx["T"])
+    mpd, msd = _discs()
+    psd, ssd = _sd(mpd), _sd(msd)
+    mpd, msd = mpd.cuda().train(), msd.cuda().train()
+    wav = _train_inputs(B, T)[4]
+    y_rec = torch.from_numpy(fx["y_rec"])
+    d_loss = DiscriminatorLoss(mpd, msd)(wav.cuda(), y_rec.cuda()).mean()
+    d_loss.backward()
+    assert abs(float(d_loss) - float(fx["d_loss"])) <= 1e-5 * float(fx["d_loss"])
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        lp = {k: v.detach().to(dt).clone().requires_grad_(True) for k, v in psd.items()}
+        ls = {k: v.detach().to(dt).clone().requires_grad_(True) for k, v in ssd.items()}
+        orc.discriminator_loss_all(wav.to(dt), y_rec.to(dt), lp, ls).backward()
+        refs[dt] = ({k: v.grad for k, v in lp.items()}, {k: v.grad for k, v in ls.items()})
+    _check3({k: p.grad for k, p in mpd.named_parameters()}, refs[torch.float32][0], refs[torch.float64][0], "D step mpd")
+    _check3({k: p.grad for k, p in msd.named_parameters()}, refs[torch.float32][1], refs[torch.float64][1], "D step msd")
 
 
 def test_train_step_vs_reference_fixture():
@@ -372,13 +434,16 @@ def test_train_step_vs_reference_fixture():
     assert _rel(out["y_rec"], fx["y_rec"]) < 1e-4
     for k in ("d_loss", "loss_mel", "loss_gen_all", "g_loss"):
         assert abs(float(out[k]) - float(fx[k])) <= 1e-4 * abs(float(fx[k])), (k, float(out[k]), float(fx[k]))
-    _summary_check(step.captured["mpd"], fx, "grad.mpd")
-    _summary_check(step.captured["msd"], fx, "grad.msd")
-    _summary_check(step.captured["dec"], fx, "grad.dec")
+    # end to end (our y_rec differs from the reference's by fp32 rounding, ~1e-6, which reaches every
+    # gradient through ~50 layers, the TPRLS medians and the AdamW-updated discriminators; the reference's
+    # own fp32 gradients are 1.6e-4 - 3.3e-4 of max |g| from fp64 here): 1e-3 per tensor, 1e-4 module-normwise
+    _summary_check(step.captured["mpd"], fx, "grad.mpd", tol=1e-3, norm_tol=1e-4)
+    _summary_check(step.captured["msd"], fx, "grad.msd", tol=1e-3, norm_tol=1e-4)
+    _summary_check(step.captured["dec"], fx, "grad.dec", tol=1e-3, norm_tol=1e-4)
     for i, k in enumerate(("asr", "F0_curve", "N", "s")):
         e = _rel(ins[i].grad, fx["grad_in." + k])
         print("input grad", k, e)
-        assert e < 1e-4
+        assert e < 1e-3
     # the AdamW updates (first step: ~ -lr sign(g) - lr wd p) where the gradient is well above rounding
     # (tolerance: 2 fp32 ulps of the parameter; the update itself is ~ lr = 1e-5 / 1e-4)
     names = [str(k) for k in fx["grad.dec.names"]]
@@ -387,7 +452,10 @@ def test_train_step_vs_reference_fixture():
         ix = torch.from_numpy(fx["grad.dec.idx"][i])
         old = p0[k].double().reshape(-1)[ix]
         d = sd1[k].cpu().double().reshape(-1)[ix] - old
-        sig = np.abs(fx["grad.dec.val"][i]) > 1e-3 * float(fx["grad.dec.maxabs"][i])
+        # entries whose gradient is well above its rounding level (a conv bias feeding an InstanceNorm has a
+        # true gradient of 0: its sign, and so its update, is noise in any fp32 implementation)
+        gm = float(fx["grad.dec.maxabs"].max())
+        sig = np.abs(fx["grad.dec.val"][i]) > 1e-2 * max(float(fx["grad.dec.maxabs"][i]), 1e-3 * gm)
         tol = 2.4e-7 * np.abs(old.numpy()) + 1e-12
         assert (np.abs(d.numpy() - fx["grad.dec.delta"][i]) <= tol)[sig].all(), k
     md = mpd.state_dict()
@@ -420,6 +488,42 @@ def test_train_step_config5_shape():
     for k in ("d_loss", "loss_mel", "loss_gen_all"):
         print(k, float(out[k]), l_o[k])
         assert abs(float(out[k]) - l_o[k]) <= 1e-3 * abs(l_o[k]), k
-    _check_grads(step.captured["mpd"], g_o["mpd"], tol=1e-3, what="config5 mpd")
-    _check_grads(step.captured["msd"], g_o["msd"], tol=1e-3, what="config5 msd")
-    _check_grads(step.captured["dec"], g_o["dec"], tol=1e-3, what="config5 decoder")
+    # module-normwise (each error relative to the module's largest |g|): at 93,000 samples the 186,000-term
+    # sums of e.g. l_linear's gradient cancel to ~1e-3 of their terms, so per-tensor relative errors of any
+    # fp32 implementation (the oracle's included) are large there
+    # (the decoder's gradients at this size are pinned against fp64 by test_decoder_grads_config5_shape;
+    # here the fp32 oracle is the yardstick, and its own error at 93,000 samples reaches ~1e-3 normwise)
+    for tag, tol in (("mpd", 1e-4), ("msd", 1e-4), ("dec", 1e-3)):
+        _check_grads(step.captured[tag], g_o[tag], tol=tol, what=f"config5 {tag} (normwise)", floor_frac=1.0)
+
+
+def test_decoder_grads_config5_shape():
+    """Decoder gradients of a fixed linear probe at the config-5 shape vs the fp64 truth and the fp32
+    reference's own values (tests/golden/train_c5_decoder_grads.npz, tests/golden/make_golden_train_c5.py)."""
+    fx = golden("train_c5_decoder_grads")
+    B, T = int(fx["B"]), int(fx["T"])
+    dec, _ = make_decoder("hifigan")
+    asr, f0, n, s, _, noise = _train_inputs(B, T)
+    r = torch.from_numpy(synth.normal("dec_probe_c5", (B, 1, 600 * T))).float()
+    dec = dec.cuda().eval()
+    ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
+    y = dec(*ins, noise=noise.cuda())
+    (y * r.cuda()).sum().backward()
+    grads = dict(dec.named_parameters())
+    names = [str(k) for k in fx["names"]]
+    gm = float(fx["f64.maxabs"].max())
+    worst, worst_ref = (0.0, ""), (0.0, "")
+    for i, k in enumerate(names):
+        g = grads[k].grad.detach().double().cpu().reshape(-1)[torch.from_numpy(fx["idx"][i])].numpy()
+        scale = max(float(fx["f64.maxabs"][i]), 1e-3 * gm)
+        eo = np.abs(g - fx["f64.val"][i]).max() / scale
+        er = np.abs(fx["f32.val"][i] - fx["f64.val"][i]).max() / scale
+        worst, worst_ref = max(worst, (eo, k)), max(worst_ref, (er, k))
+        assert eo <= max(2.0 * er, 1e-4), (k, eo, er)
+    print(f"config5 decoder probe: vs fp64 ours worst {worst[0]:.2e} ({worst[1]}), fp32 reference worst "
+          f"{worst_ref[0]:.2e} ({worst_ref[1]})")
+    for i, k in enumerate(("asr", "F0_curve", "N", "s")):
+        eo = _rel(ins[i].grad, fx[f"f64.grad_in.{k}"])
+        er = _rel(fx[f"f32.grad_in.{k}"], fx[f"f64.grad_in.{k}"])
+        print(f"  input {k}: ours {eo:.2e}, fp32 reference {er:.2e}")
+        assert eo <= max(2.0 * er, 1e-4), k

@@ -1,0 +1,107 @@
+"""Config-5 training step (BASELINE configs[4]: train.py fine-tune step, decoder + MPD/MSD fwd/bwd,
+batch_size 2, max_len 310 -> B = 2 segments of 155 asr frames = 93,000 samples) on one MI355X.
+
+One step = TrainStep (stts2_mi355x/trainstep.py): decoder forward, DiscriminatorLoss fwd/bwd + AdamW on MSD
+and MPD, MultiResolutionSTFTLoss + GeneratorLoss fwd/bwd + AdamW on the decoder, all HIP kernels.  Inputs
+(en, F0, N, s, wav) synthetic and resident in HBM, formula weights.  Prints one JSON line per dtype:
+ms per step (median of hipEvent-timed steps and wall), conv work per step (algorithmic flops of every conv
+forward, dx and dw the step launches) and its rate against the dense MFMA peak of the dtype; with
+--cpu-baseline also the oracle's step (oracle.train_step, torch CPU autograd) on the host cores.
+
+    python tools/bench_train_step.py [--steps 10] [--warmup 3] [--dtypes fp32,bf16] [--cpu-baseline]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd"), os.path.join(ROOT, "tests"),
+                os.path.join(ROOT, "tests", "golden")]
+import torch  # noqa: E402
+
+PEAK = {"fp32": 157.3e12, "bf16": 2.5e15}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+
+
+def build(B, T):
+    from helpers import fill_module, make_decoder
+    from make_golden_mpd import waves
+    from stts2_mi355x import synth
+    from stts2_mi355x.discriminators import MultiPeriodDiscriminator, MultiResSpecDiscriminator
+    dec, _ = make_decoder("hifigan")
+    mpd = fill_module(MultiPeriodDiscriminator(), "mpd.")
+    msd = fill_module(MultiResSpecDiscriminator(), "msd.")
+    asr, f0, n, s = (torch.from_numpy(a) for a in synth.decoder_inputs(B, T, tag="train"))
+    wav = torch.from_numpy(waves(B, 600 * T, 7))
+    return dec, mpd, msd, (asr, f0, n, s, wav)
+
+
+def run_gpu(dtype, B, T, steps, warmup):
+    from stts2_mi355x import training
+    from stts2_mi355x.trainstep import TrainStep
+    dec, mpd, msd, (asr, f0, n, s, wav) = build(B, T)
+    dec, mpd, msd = dec.cuda().eval(), mpd.cuda().train(), msd.cuda().train()
+    ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
+    wav = wav.cuda()
+    step = TrainStep(dec, mpd, msd, dtype=dtype)
+    for i in range(warmup):
+        step(*ins, wav, seed=100 + i)
+    torch.cuda.synchronize()
+    training.CONV_FLOPS.update(on=True, fwd=0.0, bwd=0.0)
+    step(*ins, wav, seed=99)
+    training.CONV_FLOPS["on"] = False
+    flops = training.CONV_FLOPS["fwd"] + training.CONV_FLOPS["bwd"]
+    ev = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = step(*ins, wav, seed=1000 + i)
+        b.record()
+        ev.append((a, b))
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps * 1e3
+    ms = statistics.median(x.elapsed_time(y) for x, y in ev)
+    return {"metric": "config5 train step", "dtype": dtype, "B": B, "T_frames": T, "samples_per_utt": 600 * T,
+            "ms_per_step_median": round(ms, 2), "ms_per_step_wall": round(wall, 2), "steps": steps,
+            "conv_gflop_per_step": round(flops / 1e9, 1), "conv_tflops": round(flops / ms / 1e9, 2),
+            "frac_of_dense_mfma_peak": round(flops / (ms * 1e-3) / PEAK[dtype], 4),
+            "losses": {k: float(out[k]) for k in ("d_loss", "loss_mel", "loss_gen_all")},
+            "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)}
+
+
+def run_cpu(B, T):
+    from helpers import HIFI_CFG
+    from oracle import stts_oracle as orc
+    from stts2_mi355x import synth
+    dec, mpd, msd, (asr, f0, n, s, wav) = build(B, T)
+    sd = lambda m: {k: v.detach().clone() for k, v in m.state_dict().items()}  # noqa: E731
+    noise = torch.from_numpy(synth.source_noise(B, 600 * T, tag="train_noise"))
+    t0 = time.perf_counter()
+    orc.train_step(sd(dec), sd(mpd), sd(msd), HIFI_CFG, asr, f0, n, s, wav, noise)
+    sec = time.perf_counter() - t0
+    return {"metric": "config5 train step", "kind": "port", "device": "cpu", "cores": torch.get_num_threads(),
+            "ms_per_step": round(sec * 1e3, 1), "sample": "one full config-5 step (B=2 x 93,000 samples)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtypes", default="fp32,bf16")
+    ap.add_argument("--B", type=int, default=2)
+    ap.add_argument("--T", type=int, default=155)
+    ap.add_argument("--cpu-baseline", action="store_true")
+    a = ap.parse_args()
+    for dt in a.dtypes.split(","):
+        print(json.dumps(run_gpu(dt, a.B, a.T, a.steps, a.warmup)), flush=True)
+    if a.cpu_baseline:
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())))
+        print(json.dumps(run_cpu(a.B, a.T)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -4,7 +4,11 @@ bf16 (the MFMA operands) and its output to bf16 (the stored activation), accumul
 the HIP bf16 path does.  Prints the waveform max-abs / rms error vs the fp32 oracle for each stage
 alone and for all stages.  (Test infrastructure only: the oracle is the checker, nothing here ships.)
 
-    python tools/bf16_error_study.py [T]
+    python tools/bf16_error_study.py [T] [bf16|fp16]
+
+With fp16 the operands and the stored activations round to IEEE half (10-bit mantissa, 8x finer than
+bf16's 7 bits, range +-65504): the candidate accuracy mode of gfx950's f16 MFMA, which runs at the bf16
+rate with the same bytes.  The largest |value| rounded is printed (fp16 overflows above 65504).
 """
 import os
 import sys
@@ -31,8 +35,12 @@ def stage(cin, cout):
     return {256: "s0", 128: "s1", 64: "s2", 32: "s3"}.get(c, "front")
 
 
+MODE = {"dt": torch.bfloat16, "amax": 0.0}
+
+
 def bf(x):
-    return x.to(torch.bfloat16).to(torch.float32)
+    MODE["amax"] = max(MODE["amax"], float(x.abs().max()))
+    return x.to(MODE["dt"]).to(torch.float32)
 
 
 def conv1d(x, w, b=None, *a, **k):
@@ -51,6 +59,8 @@ def convT(x, w, b=None, *a, **k):
 
 def main():
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+    name = sys.argv[2] if len(sys.argv) > 2 else "bf16"
+    MODE["dt"] = {"bf16": torch.bfloat16, "fp16": torch.float16}[name]
     torch.set_num_threads(os.cpu_count())
     dec, cfg = make_decoder("hifigan")
     sd = {k: v for k, v in dec.state_dict().items()}
@@ -64,8 +74,9 @@ def main():
             SEL.update(sel)
             out = orc.decoder_hifigan(asr, f0, n, s, sd, cfg, noise).numpy()
             d = out - ref
-            print(f"T={T} bf16 stages {'+'.join(sel):24s} max-abs {np.abs(d).max():.3e}  rms {np.sqrt((d ** 2).mean()):.3e}",
-                  flush=True)
+            print(f"T={T} {name} stages {'+'.join(sel):24s} max-abs {np.abs(d).max():.3e}  rms {np.sqrt((d ** 2).mean()):.3e}"
+                  f"  (largest rounded |value| {MODE['amax']:.3g})", flush=True)
+            MODE["amax"] = 0.0
 
 
 if __name__ == "__main__":
