@@ -99,8 +99,148 @@ __global__ __launch_bounds__(64) void k_wgrad(const float* __restrict__ x, const
     }
 }
 
-// part[s][t][co][ci] -> out[co][ci][t] = sum over s in order (fp64)
-__global__ void k_slice_reduce(const float* __restrict__ part, int S, int K, int Cout, int Cin,
+// bf16 weight gradient (the bf16 training mode): dw[co][ci][t] = sum_r dy[r][co] x[row(r, t)][ci] as
+// v_mfma_f32_32x32x16_bf16 over 32-row chunks staged through LDS.  A workgroup = 64 co x 64 ci x up to 4
+// taps (wave w computes tap 4 tg + w, 2 x 2 fragments) over one row slice; the dy chunk is staged once for
+// its 4 taps.  Both operands are fp32 frames in HBM (rows = (utterance, frame), channels contiguous):
+// staging converts them to bf16 in their natural [row][channel] layout (coalesced 32-B loads, 16-B LDS
+// writes), and ds_read_b64_tr_b16 delivers the k (= row) -contiguous MFMA fragments (cdna_hip_programming
+// T10): lane 4q + p of a 16-lane group addresses row q, channels 4p..4p+3 of a 4 x 16 block and receives
+// its channel's 4 rows.  Rows are 192 B apart (64 bf16 + 64 B of padding): the 4 rows x 64 B a 32-lane half
+// reads land in the 4 distinct 64-B bank quarters (conflict-free).  fp32 partials per slice, summed in
+// slice order by k_slice_reduce (deterministic).
+constexpr int WGB_ROWS = 32, WGB_STRIDE = 192;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void ld8_f32_bf16(const float* __restrict__ src, int c, int C, bool ok, char* dst) {
+  float v[8];
+  if (ok && c + 8 <= C && (C & 3) == 0) {
+    const float4 a = *reinterpret_cast<const float4*>(src + c);
+    const float4 b = *reinterpret_cast<const float4*>(src + c + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (ok && c + j < C) ? src[c + j] : 0.f;
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16_t)v[j];
+  *reinterpret_cast<bf16x8*>(dst) = o;
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int ks, int blk, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int row = ks * 16 + 8 * (g >> 1) + q, col = 32 * blk + 16 * (g & 1) + 4 * p;
+  const char* a0 = tile + row * WGB_STRIDE + col * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(a0 + 4 * WGB_STRIDE));
+  bf16x8 f;
+  __builtin_memcpy(&f, &lo, 8);
+  __builtin_memcpy(reinterpret_cast<char*>(&f) + 8, &hi, 8);
+  return f;
+}
+
+__global__ __launch_bounds__(256) void k_wgrad_bf16(const float* __restrict__ x, const float* __restrict__ dy, int Lin,
+                                                    int Cin, int Lq, int Cout, int K, int stride, int dil, int pad,
+                                                    int R, int S, int ntco, int ntci, int ntg,
+                                                    float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char lds[5 * WGB_ROWS * WGB_STRIDE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int tile = blockIdx.x;
+  const int tg = tile % ntg;
+  tile /= ntg;
+  const int tci = tile % ntci, tco = tile / ntci;
+  const int s = blockIdx.y;
+  const int r0 = (int)((long long)R * s / S), r1 = (int)((long long)R * (s + 1) / S);
+  const int t = tg * 4 + w;
+  const bool tap_ok = t < K;  // wave-uniform
+  const int co0 = tco * 64, ci0 = tci * 64;
+  char* At = lds;
+  char* Xt = lds + (1 + w) * WGB_ROWS * WGB_STRIDE;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const int toff = t * dil - pad;
+  for (int rb = r0; rb < r1; rb += WGB_ROWS) {
+    {  // dy chunk: thread -> row tid >> 3, channels 8 (tid & 7) .. + 8
+      const int rr = tid >> 3, c8 = (tid & 7) * 8;
+      const int r = rb + rr;
+      const bool ok = r < r1;
+      ld8_f32_bf16(dy + (size_t)(ok ? r : r0) * Cout, co0 + c8, Cout, ok, At + rr * WGB_STRIDE + c8 * 2);
+    }
+    {  // x chunk of this wave's tap: lane -> rows 4 (lane >> 3) .. + 4, channels 8 (lane & 7) .. + 8
+      const int c8 = (lane & 7) * 8;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = (lane >> 3) * 4 + q;
+        const int r = rb + rr;
+        int xr = -1, b = 0;
+        if (tap_ok && r < r1) {
+          b = r / Lq;
+          xr = (r - b * Lq) * stride + toff;
+        }
+        const bool ok = xr >= 0 && xr < Lin;
+        ld8_f32_bf16(x + ((size_t)b * Lin + (ok ? xr : 0)) * Cin, ci0 + c8, Cin, ok, Xt + rr * WGB_STRIDE + c8 * 2);
+      }
+    }
+    __syncthreads();
+    if (tap_ok) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 a0 = tr_frag(At, ks, 0, lane), a1 = tr_frag(At, ks, 1, lane);
+        const bf16x8 b0 = tr_frag(Xt, ks, 0, lane), b1 = tr_frag(Xt, ks, 1, lane);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  if (!tap_ok) return;
+  // C/D map of the 32x32 MFMAs: column = lane & 31 (ci), row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5) (co)
+  float* pt = part + ((size_t)s * K + t) * (size_t)Cout * Cin;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int co = co0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      if (co >= Cout) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ci = ci0 + 32 * j + (lane & 31);
+        if (ci < Cin) pt[(size_t)co * Cin + ci] = acc[i][j][e];
+      }
+    }
+}
+
+struct SlicesB {
+  int ntco, ntci, ntg, S;
+};
+
+SlicesB slices_bf16(int B, int Lq, int Cin, int Cout, int K) {
+  SlicesB sl;
+  sl.ntco = (Cout + 63) / 64;
+  sl.ntci = (Cin + 63) / 64;
+  sl.ntg = (K + 3) / 4;
+  const long long R = (long long)B * Lq;
+  const long long tiles = (long long)sl.ntco * sl.ntci * sl.ntg;
+  long long S = (1024 + tiles - 1) / tiles;
+  S = std::min<long long>(S, std::max<long long>(1, R / 256));  // >= 8 row chunks per slice
+  sl.S = (int)std::max<long long>(1, std::min<long long>(S, 4096));
+  return sl;
+}
+
+// part[s][t][co][ci] -> out[co][ci][t] = sum over s in order (fp64); P = float (wgrad partials) or double
+// (the bias column sums: a bias gradient often cancels to far below its slice partials, so those stay fp64)
+template <typename P>
+__global__ void k_slice_reduce(const P* __restrict__ part, int S, int K, int Cout, int Cin,
                                float* __restrict__ out) {
   const size_t per = (size_t)K * Cout * Cin;
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -113,7 +253,7 @@ __global__ void k_slice_reduce(const float* __restrict__ part, int S, int K, int
   double sum = 0.0;
   int s = 0;
   for (; s + 8 <= S; s += 8) {
-    float v[8];
+    P v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = part[(size_t)(s + k) * per + i];
 #pragma unroll
@@ -123,9 +263,9 @@ __global__ void k_slice_reduce(const float* __restrict__ part, int S, int K, int
   out[((size_t)co * Cin + ci) * K + t] = (float)sum;
 }
 
-// column sums of dy [R][C] over row slice s: part[s][c]
+// column sums of dy [R][C] over row slice s: part[s][c] (fp64)
 __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ dy, long long R, int C, int S,
-                                                float* __restrict__ part) {
+                                                double* __restrict__ part) {
   __shared__ double red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rl = threadIdx.x >> 6;
@@ -138,7 +278,7 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ dy, lo
   __syncthreads();
   if (rl == 0 && c < C) {
     const int l = threadIdx.x;
-    part[(size_t)s * C + c] = (float)(((red[0][l] + red[1][l]) + red[2][l]) + red[3][l]);
+    part[(size_t)s * C + c] = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
   }
 }
 
@@ -246,9 +386,11 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
   if (!fwd) {
     const Slices sl = slices_of(g);
     w.part = off;
-    off += al((size_t)sl.S * g.K * g.Cout * g.Cin * 4);
+    size_t ns = (size_t)sl.S;
+    if (dtype == ST_BF16) ns = std::max(ns, (size_t)slices_bf16(g.B, g.Lq, g.Cin, g.Cout, g.K).S);
+    off += al(ns * g.K * g.Cout * g.Cin * 4);
     w.part2 = off;
-    off += al((size_t)sl.S2 * g.Cout * 4);
+    off += al((size_t)sl.S2 * g.Cout * 8);
   }
   w.total = off;
   return w;
@@ -347,6 +489,20 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   return 0;
 }
 
+// dw as per-slice partials + the in-order reduction into dw [Cout][Cin][K]
+int wgrad_bf16(const Geo& g, const float* x, const float* dy, float* part, float* dw, hipStream_t s) {
+  const SlicesB sl = slices_bf16(g.B, g.Lq, g.Cin, g.Cout, g.K);
+  const long long R = (long long)g.B * g.Lq;
+  if (R > 0x7fffffffLL) return ST_EINVAL;
+  hipLaunchKernelGGL(k_wgrad_bf16, dim3(sl.ntco * sl.ntci * sl.ntg, sl.S), dim3(256), 0, s, x, dy, g.Lin, g.Cin, g.Lq,
+                     g.Cout, g.K, g.stride, g.dil, g.pad, (int)R, sl.S, sl.ntco, sl.ntci, sl.ntg, part);
+  ST_CHECK_HIP(hipGetLastError());
+  const size_t n = (size_t)g.K * g.Cout * g.Cin;
+  hipLaunchKernelGGL(k_slice_reduce<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, sl.S, g.K,
+                     g.Cout, g.Cin, dw);
+  return (int)hipGetLastError();
+}
+
 template <int NA, int NB>
 void launch_wgrad(const Geo& g, const Slices& sl, const float* x, const float* dy, float* part, hipStream_t s) {
   dim3 grid(g.K * sl.ntco * sl.ntci, sl.S);
@@ -412,7 +568,9 @@ extern "C" int stts_conv1d_bwd(int dtype, const float* x, const float* w, const 
   char* ws = (char*)workspace;
   if (dx) ST_CHECK(run_engine(dtype, g, false, dy, w, nullptr, dx, ws, s));
   const Slices sl = slices_of(g);
-  if (dw) {
+  if (dw && dtype == ST_BF16) {
+    ST_CHECK(wgrad_bf16(g, x, dy, (float*)(ws + L.part), dw, s));
+  } else if (dw) {
     float* part = (float*)(ws + L.part);
     if (sl.NA == 2 && sl.NB == 2)
       launch_wgrad<2, 2>(g, sl, x, dy, part, s);
@@ -424,17 +582,17 @@ extern "C" int stts_conv1d_bwd(int dtype, const float* x, const float* w, const 
       launch_wgrad<1, 1>(g, sl, x, dy, part, s);
     ST_CHECK_HIP(hipGetLastError());
     const size_t n = (size_t)K * Cout * Cin;
-    hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, sl.S, K, Cout, Cin,
-                       dw);
+    hipLaunchKernelGGL(k_slice_reduce<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, sl.S, K, Cout,
+                       Cin, dw);
     ST_CHECK_HIP(hipGetLastError());
   }
   if (db) {
-    float* part2 = (float*)(ws + L.part2);
+    double* part2 = (double*)(ws + L.part2);
     hipLaunchKernelGGL(k_colsum, dim3((unsigned)((Cout + 63) / 64), sl.S2), dim3(256), 0, s, dy,
                        (long long)B * Lq, Cout, sl.S2, part2);
     ST_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, part2, sl.S2, 1, Cout,
-                       1, db);
+    hipLaunchKernelGGL(k_slice_reduce<double>, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, part2, sl.S2, 1,
+                       Cout, 1, db);
     ST_CHECK_HIP(hipGetLastError());
   }
   return 0;
@@ -450,7 +608,7 @@ Geo convT_geo(int B, int Lin, int Cin, int Cout, int K, int stride, int pad, int
 size_t convT_ws(const Geo& gc, int dtype) {
   const size_t a = ws_layout(gc, dtype, false).total, b = ws_layout(gc, dtype, true).total;
   const int S2 = colsum_slices(gc.Cin, (long long)gc.B * gc.Lin);
-  return std::max(a, b) + al((size_t)S2 * gc.Cin * 4);
+  return std::max(a, b) + al((size_t)S2 * gc.Cin * 8);
 }
 }  // namespace
 
@@ -485,7 +643,10 @@ extern "C" int stts_conv_transpose1d_bwd(int dtype, const float* x, const float*
   const Geo gc = convT_geo(B, Lin, Cin, Cout, K, stride, pad, Lout);
   char* ws = (char*)workspace;
   if (dx) ST_CHECK(run_engine(dtype, gc, true, dy, w, nullptr, dx, ws, s));
-  if (dw) {
+  if (dw && dtype == ST_BF16) {
+    // wgrad of the conv with x := dy (Lout rows, Cout channels) and dy := x (Lin rows, Cin channels)
+    ST_CHECK(wgrad_bf16(gc, dy, x, (float*)(ws + ws_layout(gc, dtype, false).part), dw, s));
+  } else if (dw) {
     // wgrad of the conv with x := dy (Lout rows, Cout channels) and dy := x (Lin rows, Cin channels)
     const Slices sl = slices_of(gc);
     float* part = (float*)(ws + ws_layout(gc, dtype, false).part);
@@ -499,18 +660,18 @@ extern "C" int stts_conv_transpose1d_bwd(int dtype, const float* x, const float*
       launch_wgrad<1, 1>(gc, sl, dy, x, part, s);
     ST_CHECK_HIP(hipGetLastError());
     const size_t n = (size_t)K * gc.Cout * gc.Cin;
-    hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, sl.S, K, gc.Cout,
-                       gc.Cin, dw);
+    hipLaunchKernelGGL(k_slice_reduce<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, sl.S, K,
+                       gc.Cout, gc.Cin, dw);
     ST_CHECK_HIP(hipGetLastError());
   }
   if (db) {
     const long long R = (long long)B * Lout;
     const int S2 = colsum_slices(Cout, R);
-    float* part2 = (float*)(ws + convT_ws(gc, dtype) - al((size_t)S2 * Cout * 4));
+    double* part2 = (double*)(ws + convT_ws(gc, dtype) - al((size_t)S2 * Cout * 8));
     hipLaunchKernelGGL(k_colsum, dim3((unsigned)((Cout + 63) / 64), S2), dim3(256), 0, s, dy, R, Cout, S2, part2);
     ST_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, part2, S2, 1, Cout, 1,
-                       db);
+    hipLaunchKernelGGL(k_slice_reduce<double>, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, part2, S2, 1,
+                       Cout, 1, db);
     ST_CHECK_HIP(hipGetLastError());
   }
   return 0;

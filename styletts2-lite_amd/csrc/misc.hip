@@ -102,6 +102,49 @@ __global__ void __launch_bounds__(256) k_frames_convert(const float* __restrict_
   if (stats) atomic_stats(stats + ((size_t)b * stats_ld + c) * 2, a, q);
 }
 
+// fp32 frames [rows][ld_in] -> bf16 frames [rows][ld_out] (ld_out % 8 == 0), no statistics: one thread per
+// (row, 8-channel group), 32-B loads and one 16-B store; channels C .. ld_out - 1 written as 0 (the training
+// path's conv inputs; k_frames_convert serves the statistics-producing plan conversions)
+__global__ void __launch_bounds__(256) k_cvt_bf16_rows(const float* __restrict__ src, long long rows, int C, int ld_in,
+                                                       bf16_t* __restrict__ dst, int ld_out) {
+  const int ng = ld_out >> 3;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * ng) return;
+  const long long r = i / ng;
+  const int c = (int)(i - r * ng) * 8;
+  const float* sp = src + r * ld_in + c;
+  float v[8];
+  if (c + 8 <= C && ((ld_in | c) & 3) == 0) {
+    const float4 a = *reinterpret_cast<const float4*>(sp);
+    const float4 b = *reinterpret_cast<const float4*>(sp + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = c + j < C ? sp[j] : 0.f;
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16_t)v[j];
+  *reinterpret_cast<bf16x8*>(dst + r * ld_out + c) = o;
+}
+
+// bf16 frames [rows][ld] -> fp32 [rows][C] with C % 8 == 0: 16-B loads, 32-B stores
+__global__ void __launch_bounds__(256) k_cvt_f32_rows(const bf16_t* __restrict__ src, long long rows, int C, int ld,
+                                                      float* __restrict__ dst) {
+  const int ng = C >> 3;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * ng) return;
+  const long long r = i / ng;
+  const int c = (int)(i - r * ng) * 8;
+  const bf16x8 a = *reinterpret_cast<const bf16x8*>(src + r * ld + c);
+  float4 o0, o1;
+  o0.x = (float)a[0]; o0.y = (float)a[1]; o0.z = (float)a[2]; o0.w = (float)a[3];
+  o1.x = (float)a[4]; o1.y = (float)a[5]; o1.z = (float)a[6]; o1.w = (float)a[7];
+  float* dp = dst + r * C + c;
+  *reinterpret_cast<float4*>(dp) = o0;
+  *reinterpret_cast<float4*>(dp + 4) = o1;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) k_frames_to_f32(const T* __restrict__ src, int L, int C, int ld, float* dst) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -685,6 +728,12 @@ int st_ncl_to_frames(const float* src, int B, int C, int L, void* dst, int ld, i
 
 int st_frames_convert(const float* src, int B, int L, int C, int ld_in, void* dst, int ld_out, double* stats,
                       int stats_ld, int dtype, hipStream_t s) {
+  if (dtype == ST_BF16 && !stats && ld_out % 8 == 0) {
+    const long long n = (long long)B * L * (ld_out / 8);
+    hipLaunchKernelGGL(k_cvt_bf16_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, (long long)B * L, C,
+                       ld_in, reinterpret_cast<bf16_t*>(dst), ld_out);
+    return (int)hipGetLastError();
+  }
   dim3 grid((L + 63) / 64, B, (C + 255) / 256);
   DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_frames_convert<T>, grid, dim3(256), 0, s, src, L, C, ld_in,
                                               reinterpret_cast<T*>(dst), ld_out, stats, stats_ld));
@@ -789,6 +838,12 @@ int st_mpd_losses(const float* out, const MpdLossSegs& sg, double* part, double*
 }
 
 int st_frames_to_f32(const void* src, int B, int L, int C, int ld, float* dst, int dtype, hipStream_t s) {
+  if (dtype == ST_BF16 && C % 8 == 0 && ld % 8 == 0) {
+    const long long n = (long long)B * L * (C / 8);
+    hipLaunchKernelGGL(k_cvt_f32_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const bf16_t*>(src), (long long)B * L, C, ld, dst);
+    return (int)hipGetLastError();
+  }
   dim3 grid((unsigned)(((size_t)L * C + 255) / 256), B);
   DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_frames_to_f32<T>, grid, dim3(256), 0, s,
                                               reinterpret_cast<const T*>(src), L, C, ld, dst));

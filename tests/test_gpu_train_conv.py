@@ -2,7 +2,8 @@
 
 train.py:272-327 gets its conv gradients from torch autograd, so autograd (fp64 on the CPU) is the
 reference algorithm here; tolerances are relative to the gradient's max magnitude: fp32 1e-4,
-bf16 operands (forward and dx only; dw / db are fp32 in both modes) 2e-2.  The cases are the
+bf16 operands (forward, dx and dw: bf16 MFMA operands with fp32 accumulation; db stays an fp64-summed
+fp32 reduction in both modes) 2e-2.  The cases are the
 conv shapes of the decoder (Modules/hifigan.py) and the discriminators (discriminators.py)."""
 import numpy as np
 import pytest
@@ -21,6 +22,9 @@ CASES = [
     (1, 512, 256, 1, 1, 1, 0, 37),       # 1x1 shortcut
     (2, 16, 48, 4, 2, 1, 1, 99),         # even kernel, stride 2, ragged length
     (1, 64, 64, 7, 1, 5, 15, 48000),     # long rows: many wgrad slices
+    (20, 512, 1024, 5, 3, 1, 2, 36),     # MPD period 5 conv3 at T = 4800 (dx: output padding 2)
+    (20, 128, 512, 5, 3, 1, 2, 107),     # MPD period 5 conv2
+    (20, 1024, 1024, 5, 1, 1, 2, 12),    # MPD period 5 conv4 (12 rows per column)
 ]
 
 
@@ -58,7 +62,7 @@ def test_conv1d_fwd_bwd(case, dtype):
     errs = {"y": _rel(y, y_ref), "dx": _rel(xc.grad, dx_ref), "dw": _rel(wc.grad, dw_ref), "db": _rel(bc.grad, db_ref)}
     print(case, dtype, {k: f"{v:.2e}" for k, v in errs.items()})
     assert errs["y"] < tol and errs["dx"] < tol
-    assert errs["dw"] < 1e-4 and errs["db"] < 1e-5  # fp32 in both modes
+    assert errs["dw"] < (1e-4 if dtype == "fp32" else 2e-2) and errs["db"] < 1e-5  # db: fp32 in both modes
 
 
 def test_conv1d_bwd_deterministic_and_partial_outputs():
@@ -131,4 +135,4 @@ def test_conv_transpose1d_fwd_bwd(case, dtype):
             "db": _rel(bc.grad, bd_.grad)}
     print(case, dtype, {k: f"{v:.2e}" for k, v in errs.items()})
     assert errs["y"] < tol and errs["dx"] < tol
-    assert errs["dw"] < 1e-4 and errs["db"] < 1e-5
+    assert errs["dw"] < tol and errs["db"] < 1e-5
