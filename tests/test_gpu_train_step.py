@@ -73,7 +73,7 @@ def _sd64(sd):
     return {k: v.double() for k, v in sd.items()}
 
 
-def _check3(ours, r32, r64, what, slack=2.0, abs_tol=1e-4):
+def _check3(ours, r32, r64, what, slack=2.0, abs_tol=1e-4, norm_tol=None):
     """Gradients vs the oracle's fp64 autograd (the truth), next to the reference's own fp32 error: the
     reference in fp32 is itself 1.6e-4 (decoder) to 3.3e-4 (MSD) of max |g| away from fp64 at T = 8
     (tests/golden/make_golden_train.py's case), so 'as close as the reference' means
@@ -88,6 +88,8 @@ def _check3(ours, r32, r64, what, slack=2.0, abs_tol=1e-4):
         er = _rel(r32[k], g, floor=1e-3 * gmax)
         worst, worst_ref = max(worst, (eo, k)), max(worst_ref, (er, k))
         assert eo <= max(slack * er, abs_tol), (k, eo, er)
+        if norm_tol is not None:  # error relative to the module's largest |g|
+            assert _rel(ours[k], g, floor=gmax) <= norm_tol, (k, "normwise", _rel(ours[k], g, floor=gmax))
     print(f"{what}: vs fp64, ours worst {worst[0]:.2e} ({worst[1]}), fp32 reference worst {worst_ref[0]:.2e} "
           f"({worst_ref[1]}), {len(r64)} tensors")
 
@@ -412,8 +414,14 @@ def test_d_step_on_reference_output():
         ls = {k: v.detach().to(dt).clone().requires_grad_(True) for k, v in ssd.items()}
         orc.discriminator_loss_all(wav.to(dt), y_rec.to(dt), lp, ls).backward()
         refs[dt] = ({k: v.grad for k, v in lp.items()}, {k: v.grad for k, v in ls.items()})
-    _check3({k: p.grad for k, p in mpd.named_parameters()}, refs[torch.float32][0], refs[torch.float64][0], "D step mpd")
-    _check3({k: p.grad for k, p in msd.named_parameters()}, refs[torch.float32][1], refs[torch.float64][1], "D step msd")
+    # the discriminators' LeakyReLU(0.1): a pre-activation within fp32 rounding of 0 takes the other branch in
+    # one implementation (tools/diag_mpd_grad.py: ours 1 sign flip vs fp64 in period 5's fmap3 here, the
+    # reference 0), moving a few dozen entries of the layers below by ~1e-2 of their magnitude: per tensor
+    # 1e-3, and 1e-4 of the module's max |g|
+    _check3({k: p.grad for k, p in mpd.named_parameters()}, refs[torch.float32][0], refs[torch.float64][0], "D step mpd",
+            abs_tol=1e-3, norm_tol=1e-4)
+    _check3({k: p.grad for k, p in msd.named_parameters()}, refs[torch.float32][1], refs[torch.float64][1], "D step msd",
+            abs_tol=1e-3, norm_tol=1e-4)
 
 
 def test_train_step_vs_reference_fixture():

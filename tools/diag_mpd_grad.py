@@ -56,3 +56,12 @@ a, c = outs[("ours", 0)], outs[(str(torch.float64), 0)]
 diff = (a - c).abs()
 print("fmap0 grad diff: max at", np.unravel_index(int(diff.argmax()), tuple(diff.shape)), "value", diff.max().item(),
       "ref", c.reshape(-1)[int(diff.argmax())].item())
+# LeakyReLU kinks: conv outputs whose sign differs from the fp64 forward (their gradient factor is 1 vs 0.1)
+with torch.no_grad():
+    _, fm_o = T.discriminator_p_forward(d, x.cuda(), period)
+    _, fm_64 = orc.discriminator_p(x.double(), {k: v.double() for k, v in sd.items()}, f"discriminators.{idx}", period)
+    _, fm_32 = orc.discriminator_p(x.float(), {k: v.float() for k, v in sd.items()}, f"discriminators.{idx}", period)
+    for j in range(5):
+        a, b, c = fm_o[j].cpu().double(), fm_32[j].double(), fm_64[j]
+        print(f"fmap{j}: sign flips vs fp64: ours {int(((a > 0) != (c > 0)).sum())}, fp32 ref {int(((b > 0) != (c > 0)).sum())}"
+              f"; forward rel err ours {((a - c).abs().max() / c.abs().max()).item():.1e} ref {((b - c).abs().max() / c.abs().max()).item():.1e}")
