@@ -375,6 +375,11 @@ const char* stts_error_string(int code);
  *                     (fp32 slice partials in the plan workspace, summed in slice order; B = 1 decoder
  *                     5.70 -> 4.92 ms); 0 = off. */
 #define STTS_OPT_SPLITK 12
+/*   STTS_OPT_EXP      bit mask of engine experiments under A/B (tools/ab_engine.py); 0 = the measured
+ *                     defaults.  1: bigconv2 static MFMA priority for the second half of the waves;
+ *                     2: bigconv2 residual epilogue in one load batch; 4: resconv residual prefetched
+ *                     one tile ahead. */
+#define STTS_OPT_EXP 13
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

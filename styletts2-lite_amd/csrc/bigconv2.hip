@@ -164,7 +164,7 @@ __device__ __forceinline__ void bstore16(Rsrc r, unsigned off, const uint4& v) {
                                          r, (int)off, 0, 0);
 }
 
-template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C>
+template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false>
 __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   using G = B2<C, NW, K, DIL, PRO, CINP>;
   constexpr int TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
@@ -397,7 +397,9 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     // pending it would wait vmcnt(0) at every use); the empty asm fences pin the issue order.
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unconstrained
     lap(7);
-    constexpr int NB = RES ? 2 : 1, FB = 8 / NB;
+    // (EPI1: a residual-only epilogue loads all 8 fragments in one batch, into the registers the dead
+    // tap fragments held: one load latency per tile instead of two; STTS_OPT_EXP bit 2)
+    constexpr int NB = (RES && !(EPI1 && !ACC)) ? 2 : 1, FB = 8 / NB;
     uint4 rl[FB][2], al[FB][2];
     auto finish = [&](int f, const uint4 (&r2)[2], const uint4 (&a2)[2]) __attribute__((always_inline)) {
       f32x16& v = acc[f];  // in place: the accumulators of a finished tile are the output
@@ -563,6 +565,9 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 
   // ---------------- main loop: one iteration per 32-channel group; K taps unrolled
   init_acc(cur.ch);
+  // STTS_OPT_EXP bit 1: static MFMA-issue priority for the second-dispatched half of the waves
+  // (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if ((p.exp & 1) && wu >= NW / 2) __builtin_amdgcn_s_setprio(1);
   for (int gg = 0; gg < NGG; ++gg) {
     lap(6);
     if (!(dbg & 32)) barrier_lds();  // group gg's window transformed by every wave; group gg-1's reads all done
@@ -679,10 +684,10 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   }
 }
 
-template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C>
+template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
   using G = B2<C, NW, K, DIL, PRO, CINP>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -700,6 +705,7 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
   ConvParams q = p;
   q.skew = g_opt_skew;
+  q.exp = g_opt_exp;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
@@ -716,7 +722,9 @@ int launch_b2_k(const ConvParams& p, hipStream_t s) {
     }
   }
   if (p.dil != 1) return ST_EINVAL;  // conv2: dilation 1, residual, optionally the resblock sum
-  return p.accb ? launch_b2<C, NW, K, 1, true, true>(p, s) : launch_b2<C, NW, K, 1, true, false>(p, s);
+  if (p.accb) return launch_b2<C, NW, K, 1, true, true>(p, s);
+  return (g_opt_exp & 2) ? launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, true>(p, s)
+                         : launch_b2<C, NW, K, 1, true, false>(p, s);
 }
 
 template <int C, int NW>
@@ -735,6 +743,7 @@ int launch_b2_c(const ConvParams& p, hipStream_t s) {
 // 3 = this engine, 4-wave blocks (two per CU, C = 256 split into two 128-channel output parts)
 int g_opt_bigconv = 2;
 int g_opt_skew = 0;
+int g_opt_exp = 0;
 
 bool st_bigconv2_eligible(const ConvParams& p) {
   if (g_opt_bigconv < 2) return false;

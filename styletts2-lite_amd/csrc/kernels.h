@@ -53,6 +53,7 @@ struct ConvParams {
   int zc_period, zc_valid;
   int dbg;         // phase-skipping timing knob (STTS_OPT_DEBUG; results are wrong when set)
   int skew;        // bigconv2 start skew of half the workgroups (STTS_OPT_SKEW, set by the launcher)
+  int exp;         // experiment bits (STTS_OPT_EXP, set by the launchers that read them)
   unsigned long long* stamps;  // diagnostics: per-phase s_memtime cycle sums (stts_set_debug_buffer), or null
   int tg;          // taps per staged weight group (set by the launcher)
   int cps;         // 32-channel chunks per pipeline step, 1 or 2 (set by the launcher)
@@ -90,6 +91,7 @@ bool st_bigconv2_eligible(const ConvParams& p);
 int st_bigconv2(const ConvParams& p, hipStream_t stream);
 extern int g_opt_bigconv;
 extern int g_opt_skew;  // STTS_OPT_SKEW (bigconv2.hip)
+extern int g_opt_exp;   // STTS_OPT_EXP (bigconv2.hip, resconv.hip): A/B experiment bits
 // the decoder front-end's k3 AdainResBlk1d convs on the bigconv2 engine (STTS_OPT_FRONT)
 bool st_front_eligible(const ConvParams& p, int dtype);
 int st_bigconv2_front(const ConvParams& p, hipStream_t stream);

@@ -1803,6 +1803,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_FRONT: g_opt_front = (value >= 0 && value <= 2) ? value : 1; return 0;
     case STTS_OPT_PW: g_opt_pw = (value >= 0 && value <= 2) ? value : 1; return 0;
     case STTS_OPT_SPLITK: g_opt_splitk = value ? 1 : 0; return 0;
+    case STTS_OPT_EXP: g_opt_exp = value; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1826,6 +1827,7 @@ int stts_get_option(int key) {
     case STTS_OPT_FRONT: return g_opt_front;
     case STTS_OPT_PW: return g_opt_pw;
     case STTS_OPT_SPLITK: return g_opt_splitk;
+    case STTS_OPT_EXP: return g_opt_exp;
     default: return ST_EINVAL;
   }
 }

@@ -64,7 +64,9 @@ __device__ __forceinline__ uint4 f32_to_bf8(const float* v) {
 
 // ACC: the launch adds the output into the resblock running sum (p.accb, p.acc_div) and keeps
 // no statistics (hifigan.py:336-342); otherwise statistics are kept when p.stats is set.
-template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC>
+// RPF: the residual / running-sum rows of tile t+1 are loaded during tile t (two register sets,
+// STTS_OPT_EXP bit 4), instead of at the start of the tile that consumes them
+template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false>
 __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvParams p) {
   using G = RC<C, K, DIL, WAVES, WAVES_N>;
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, NTL = G::NTL, NCH = G::NCH, XP = G::XP, WP = G::WP;
@@ -111,8 +113,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   };
 
   // epilogue prefetch: residual rows of the tile (16 channels of one frame per lane)
-  uint4 rres[MT][NTL][2], racc[ACC ? MT : 1][ACC ? NTL : 1][2];
-  auto issue_epi = [&](int t) __attribute__((always_inline)) {
+  struct EpiRegs {
+    uint4 rres[MT][NTL][2], racc[ACC ? MT : 1][ACC ? NTL : 1][2];
+  };
+  auto issue_epi = [&](int t, EpiRegs& er_) __attribute__((always_inline)) {
+    auto& rres = er_.rres;
+    auto& racc = er_.racc;
     const int b = t / ntm, mt = t - b * ntm;
     const bool hr = p.res != nullptr;
     const Rsrc rr = make_rsrc(hr ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr,
@@ -203,8 +209,10 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   };
 
   int cur_b = -1;
-  auto step = [&](int t, uint4 (&pre)[MAXU]) __attribute__((always_inline)) {
+  auto step = [&](int t, uint4 (&pre)[MAXU], EpiRegs& er_, EpiRegs& er_next) __attribute__((always_inline)) {
     const int b = t / ntm, mt = t - b * ntm;
+    auto& rres = er_.rres;
+    auto& racc = er_.racc;
     if (b != cur_b) {
       if (cur_b >= 0 && p.stats) flush(cur_b);
       // every wave is past its previous transform (barrier B of the previous step): coef is free
@@ -221,7 +229,11 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
       }
       cur_b = b;
     }
-    issue_epi(t);
+    if constexpr (RPF) {
+      if (t + 1 < tend) issue_epi(t + 1, er_next);
+    } else {
+      issue_epi(t, er_);
+    }
     __syncthreads();  // (A) coef / weights visible; every wave done reading Xs of the previous tile
     transform(t, pre);
     if (t + 2 < tend) issue(t + 2, pre);
@@ -328,23 +340,25 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   };
 
   uint4 preA[MAXU], preB[MAXU];
+  EpiRegs eA, eB;
+  if constexpr (RPF) issue_epi(tbeg, eA);
   issue(tbeg, preA);
   if (tbeg + 1 < tend) issue(tbeg + 1, preB);
   for (int t = tbeg; t < tend; t += 2) {
-    step(t, preA);
-    if (t + 1 < tend) step(t + 1, preB);
+    step(t, preA, eA, eB);
+    if (t + 1 < tend) step(t + 1, preB, eB, eA);
   }
   if (p.stats) flush(cur_b);
 }
 
 int g_num_cu_rc = 0;
 
-template <int C, int K, int DIL, bool ACC>
+template <int C, int K, int DIL, bool ACC, bool RPF = false>
 int launch_rc(const ConvParams& p, hipStream_t stream) {
   constexpr int WAVES = C == 32 ? 4 : 8;
   constexpr int WAVES_N = C == 32 ? 1 : 2;
   using G = RC<C, K, DIL, WAVES, WAVES_N>;
-  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC>;
+  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -368,6 +382,10 @@ int launch_rc(const ConvParams& p, hipStream_t stream) {
 
 template <int C, int K, int DIL>
 int launch_rc_a(const ConvParams& p, hipStream_t s) {
+  if constexpr (DIL == 1) {  // (the residual launches: conv2 of an iteration, dilation 1)
+    if ((g_opt_exp & 4) && (p.res || p.accb))
+      return p.accb ? launch_rc<C, K, 1, true, true>(p, s) : launch_rc<C, K, 1, false, true>(p, s);
+  }
   return p.accb ? launch_rc<C, K, DIL, true>(p, s) : launch_rc<C, K, DIL, false>(p, s);
 }
 

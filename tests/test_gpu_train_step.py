@@ -416,10 +416,11 @@ def test_d_step_on_reference_output():
         refs[dt] = ({k: v.grad for k, v in lp.items()}, {k: v.grad for k, v in ls.items()})
     # the discriminators' LeakyReLU(0.1): a pre-activation within fp32 rounding of 0 takes the other branch in
     # one implementation (tools/diag_mpd_grad.py: ours 1 sign flip vs fp64 in period 5's fmap3 here, the
-    # reference 0), moving a few dozen entries of the layers below by ~1e-2 of their magnitude: per tensor
-    # 1e-3, and 1e-4 of the module's max |g|
+    # reference 0), moving the flipped layer's own bias / weight gradients by up to 1.5e-3 of their max |g|
+    # (profiles/r03_diag_mpd_kink.txt: convs.3.bias 1.17e-3, convs.3.weight_v 1.54e-3) and the layers below
+    # by ~3e-4: per tensor 2e-3, and 1e-4 of the module's max |g|
     _check3({k: p.grad for k, p in mpd.named_parameters()}, refs[torch.float32][0], refs[torch.float64][0], "D step mpd",
-            abs_tol=1e-3, norm_tol=1e-4)
+            abs_tol=2e-3, norm_tol=1e-4)
     _check3({k: p.grad for k, p in msd.named_parameters()}, refs[torch.float32][1], refs[torch.float64][1], "D step msd",
             abs_tol=1e-3, norm_tol=1e-4)
 
