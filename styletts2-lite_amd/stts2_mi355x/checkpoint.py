@@ -50,12 +50,21 @@ def _strip(sd: dict) -> "OrderedDict":
 
 
 def extend_token_table(ckpt: dict, extend_to: int, n_token: int | None = None,
-                       generator: torch.Generator | None = None) -> dict:
+                       generator: torch.Generator | None = None, fresh: dict | None = None) -> dict:
     """Extend/extend.ipynb on a training checkpoint: returns the notebook's saved layout with the
     token tables grown to `extend_to` rows.  `n_token` (len(symbols) + 1 from the config) defaults to
     the rows of the TextEncoder embedding; extend_to <= n_token raises ValueError as the notebook
-    exits.  The new rows are drawn from `generator` (torch's default when None)."""
+    exits.  The new rows are drawn from `generator` (torch's default when None).
+
+    The notebook builds all eight TRAINING_MODULES from the config and saves every one of them, so a
+    module the checkpoint lacks (e.g. mpd / msd in a fine-tune checkpoint) is saved freshly
+    initialised.  `fresh` (module name -> state dict of a module built from the config) supplies
+    those; without it such modules are left out of the result (the notebook's layout then differs
+    only by the missing entries)."""
     out = {k: _strip(v) for k, v in ckpt["net"].items() if k in TRAINING_MODULES}
+    for k in TRAINING_MODULES:
+        if k not in out and fresh is not None and k in fresh:
+            out[k] = _strip(fresh[k])
     if n_token is None:
         n_token = out["text_encoder"]["embedding.weight"].shape[0]
     if extend_to - n_token <= 0:

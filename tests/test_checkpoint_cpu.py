@@ -70,3 +70,19 @@ def test_roundtrip_through_weights_only_load(tmp_path):
     sd = te.state_dict()
     sd["embedding.weight"] = back["net"]["text_encoder"]["embedding.weight"]
     te.load_state_dict(sd)
+
+
+def test_extend_fills_missing_modules_from_fresh():
+    """extend.ipynb saves all eight modules built from the config: one the checkpoint lacks is saved
+    freshly initialised.  `fresh` supplies it; without `fresh` it is left out."""
+    src = fake_ckpt()
+    del src["net"]["mpd"], src["net"]["msd"]
+    assert "mpd" not in ck.extend_token_table(src, 180)["net"]
+    fresh = {"mpd": {"module.y.weight": torch.ones(2)}, "msd": {"z.weight": torch.zeros(2)},
+             "decoder": {"generator.conv_post.bias": torch.full((1,), 9.0)}}
+    out = ck.extend_token_table(src, 180, fresh=fresh)
+    assert sorted(out["net"]) == sorted(ck.TRAINING_MODULES)
+    assert torch.equal(out["net"]["mpd"]["y.weight"], torch.ones(2))
+    # modules the checkpoint has keep the checkpoint's values
+    assert torch.equal(out["net"]["decoder"]["generator.conv_post.bias"],
+                       src["net"]["decoder"]["generator.conv_post.bias"])

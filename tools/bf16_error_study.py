@@ -4,7 +4,9 @@ bf16 (the MFMA operands) and its output to bf16 (the stored activation), accumul
 the HIP bf16 path does.  Prints the waveform max-abs / rms error vs the fp32 oracle for each stage
 alone and for all stages.  (Test infrastructure only: the oracle is the checker, nothing here ships.)
 
-    python tools/bf16_error_study.py [T] [bf16|fp16]
+    python tools/bf16_error_study.py [T] [bf16|fp16] [all]
+
+(`all`: only the whole-decoder case, for long T.)
 
 With fp16 the operands and the stored activations round to IEEE half (10-bit mantissa, 8x finer than
 bf16's 7 bits, range +-65504): the candidate accuracy mode of gfx950's f16 MFMA, which runs at the bf16
@@ -68,8 +70,11 @@ def main():
     F.conv1d, F.conv_transpose1d = conv1d, convT
     with torch.no_grad():
         ref = orc.decoder_hifigan(asr, f0, n, s, sd, cfg, noise).numpy()
-        for sel in (["front"], ["s0"], ["s1"], ["s2"], ["s3"], ["post"], ["s2", "s3", "post"],
-                    ["front", "s0", "s1"], ["front", "s0", "s1", "s2", "s3", "post"]):
+        cases = (["front"], ["s0"], ["s1"], ["s2"], ["s3"], ["post"], ["s2", "s3", "post"],
+                 ["front", "s0", "s1"], ["front", "s0", "s1", "s2", "s3", "post"])
+        if len(sys.argv) > 3 and sys.argv[3] == "all":
+            cases = cases[-1:]
+        for sel in cases:
             SEL.clear()
             SEL.update(sel)
             out = orc.decoder_hifigan(asr, f0, n, s, sd, cfg, noise).numpy()
