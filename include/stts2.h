@@ -380,6 +380,9 @@ const char* stts_error_string(int code);
  *                     2: bigconv2 residual epilogue in one load batch; 4: resconv residual prefetched
  *                     one tile ahead. */
 #define STTS_OPT_EXP 13
+/*   STTS_OPT_UPS      1 = the HiFi-GAN ups[0] / ups[1] polyphase upsamplers (N = 2,560 / 640) on the bigconv2
+ *                     engine (default); 0 = on conv1d_igemm. */
+#define STTS_OPT_UPS 14
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);
@@ -395,6 +398,15 @@ int stts_profile_read(double* total_ms, long long* launches, double* alg_flops, 
  * res | acc<<1 | engine<<4} with engine 0 = conv1d_igemm, 1 = resconv, 2 = bigconv, 3 = resfused,
  * ms_flops_bytes = {hipEvent ms, algorithmic flops, algorithmic bytes}. */
 int stts_profile_launch(long long i, int* shape, double* ms_flops_bytes);
+
+/* Diagnostics (not a product path): traffic-counter calibration kernels (csrc/calib.hip) that read or
+ * write every byte of a bf16 frames buffer [rows][ld] exactly once (mode 3: plus `halo` rows per tile
+ * side) with the conv engines' access patterns: 0 coalesced 16-B loads, 1 LDS-DMA 1 KiB per instruction,
+ * 2 / 3 bigconv2's 64-B window row segments per 32-channel group (tile rows, halo), 4 coalesced 16-B
+ * stores, 5 bigconv2's epilogue stores, 6 bigconv2's residual loads (the epilogue's per-lane pieces).  `grid` workgroups of 256 threads; sink[grid] floats.
+ * Used by tools/calib_traffic.py under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE. */
+int stts_calib_traffic(int mode, void* buf, long long rows, int ld, int tile, int halo, int grid, float* sink,
+                       void* stream);
 
 /* ---- testing hook (not a product path): one conv1d_igemm launch on fp32 frames.
  * x [B][Lin][Cin] frames; w in nn.Conv1d [Cout][Cin][K] / nn.ConvTranspose1d [Cin][Cout][K] layout;

@@ -34,7 +34,11 @@ namespace {
 // channel; no prologue = a = 1, m = 0, slope 1)
 enum { PK_SNAKE = 0, PK_LRELU = 1 };
 
-template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C>
+// UPS: the polyphase ConvTranspose1d upsampler (hifigan.py:292-294, 333-335) as the 2-tap GEMM of
+// C = N = u Cout columns, tap t reads input row q + t - 1 (left pad 1); the epilogue maps GEMM
+// row q / column n to output frame q u + n / Cout - opad, channel n % Cout.
+// CO: channels of the bias / statistics arrays (C; Cout for UPS)
+template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C, bool UPS = false, int CO = C>
 struct B2 {
   static constexpr int NCOEF = PRO == PK_SNAKE ? 5 : 2;  // coefficient rows per input channel
   static constexpr int NCBW = (C / 32 < NW) ? C / 32 : NW;  // 32-channel output blocks per block tile
@@ -43,7 +47,7 @@ struct B2 {
   static constexpr int NCH = C / NCO;    // output-channel parts per frame tile (tiles per frame range)
   static constexpr int TM = 256 * FH;    // tile rows (frames)
   static constexpr int NG = CINP / 32;   // 32-channel input groups per tile (at most)
-  static constexpr int PAD = DIL * (K - 1) / 2;
+  static constexpr int PAD = UPS ? DIL * (K - 1) : DIL * (K - 1) / 2;
   static constexpr int R = TM + DIL * (K - 1);                    // window rows a group needs
   static constexpr int NWIN = (R * 4 + 64 * NW - 1) / (64 * NW);  // window DMA instructions per wave per group
   static constexpr int WROWS = NWIN * NW * 16;                    // rows the waves' DMAs cover
@@ -54,8 +58,8 @@ struct B2 {
   // ldsdma-fill, later from HBM under load; a tap is ~0.5 us of MFMA issue per SIMD)
   static constexpr int OFF_COEF = 0;                  // [2][NCOEF][CINP] f32 (utterance parity)
   static constexpr int OFF_BIAS = OFF_COEF + 2 * NCOEF * CINP * 4;
-  static constexpr int OFF_ST = OFF_BIAS + C * 4;     // [C][2] f32
-  static constexpr int OFF_W = (OFF_ST + 2 * C * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
+  static constexpr int OFF_ST = OFF_BIAS + CO * 4;    // [CO][2] f32
+  static constexpr int OFF_W = (OFF_ST + 2 * CO * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
   static constexpr int BPC = NW == 4 ? 2 : 1;                     // blocks per CU
   static constexpr int PDMAX_LDS = ((160 * 1024 / BPC - OFF_W - 2 * WROWS * 64) / (NW * 2048)) - 1;
   static constexpr int PD0 = PDMAX_LDS < K ? PDMAX_LDS : K;
@@ -164,9 +168,10 @@ __device__ __forceinline__ void bstore16(Rsrc r, unsigned off, const uint4& v) {
                                          r, (int)off, 0, 0);
 }
 
-template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false>
+template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
+          bool UPS = false, int CO = C>
 __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
-  using G = B2<C, NW, K, DIL, PRO, CINP>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO>;
   constexpr int TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
   constexpr int NCF = G::NCOEF;
   // input-channel groups: C / 32 for the square resblock convs, ceil(Cin / 32) for the front-end
@@ -216,7 +221,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     const unsigned long long d = (unsigned long long)(p.skew > 0 ? p.skew : -p.skew) * 1024ull;
     while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
   }
-  for (int i = tid; i < C; i += NT) {
+  for (int i = tid; i < CO; i += NT) {
     bias_s[i] = p.bias ? p.bias[i] : 0.f;
     st_lds[2 * i] = st_lds[2 * i + 1] = 0.f;
   }
@@ -256,9 +261,9 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   auto set_coef = [&](int b) __attribute__((always_inline)) {
     float* cf = coef + (b & 1) * NCF * CINP;
     if constexpr (PRO == PK_SNAKE) {
-      for (int ci = tid; ci < C; ci += NT) {
-        float mm, aa, be;
-        adain_coeffs(p.pro, b, ci, mm, aa, be);
+      for (int ci = tid; ci < CINP; ci += NT) {
+        float mm = 0.f, aa = 1.f, be = 0.f;  // Snake alone (the upsamplers' prologue): a = 1, m = 0
+        if (!UPS || (p.pro.mode & PRO_AFFINE)) adain_coeffs(p.pro, b, ci, mm, aa, be);
         const float al = p.pro.alpha[ci];
         const float m1 = be - mm * aa, ia2 = 0.5f / al, alr = al * 0.31830988618379067f;
         cf[ci] = m1 + ia2;
@@ -366,7 +371,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 
   // ---------------- statistics: LDS per-block sums -> fp64 global when the block leaves an utterance
   auto flush = [&](int b) __attribute__((always_inline)) {
-    for (int ci = tid; ci < C; ci += NT) {
+    for (int ci = tid; ci < CO; ci += NT) {
       double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ci) * 2;
       atomicAdd(d, (double)st_lds[2 * ci]);
       atomicAdd(d + 1, (double)st_lds[2 * ci + 1]);
@@ -380,9 +385,13 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     const int q0 = mt * TM + fh * 256 + l32;
     // the lane's 16 consecutive output channels (packing permutation)
     const int co0 = ch * NCO + 32 * cb + 16 * hi;
-    const Rsrc ry = make_rsrc(reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs, (unsigned)((size_t)p.Lq * p.y_ld * 2));
+    // UPS: the lane's 16 columns are channels c0.. of output phase ph; row q -> frame q u + ph - opad
+    const int ph = UPS ? co0 / p.Cout : 0, c0 = UPS ? co0 - ph * p.Cout : co0;
+    const int Lrows = UPS ? p.Lout : p.Lq;
+    auto orow = [&](int q) __attribute__((always_inline)) { return UPS ? q * p.up + ph - p.opad : q; };
+    const Rsrc ry = make_rsrc(reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs, (unsigned)((size_t)Lrows * p.y_ld * 2));
     const Rsrc rr = make_rsrc(RES ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr,
-                              RES ? (unsigned)((size_t)p.Lq * p.res_ld * 2) : 0u);
+                              RES ? (unsigned)((size_t)Lrows * p.res_ld * 2) : 0u);
     const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const bf16_t*>(p.accb) + (size_t)b * p.acc_bs : nullptr,
                               ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * 2) : 0u);
     const float osc = p.out_scale;
@@ -424,12 +433,13 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       if (!(dbg & 128)) {
         // (an LDS-transposed variant writing 16 rows x 64 contiguous bytes per store measured the
         // same in the decoder: the stores are bound by the chip-wide write burst, not by requests)
-        const unsigned ey = (unsigned)(q * p.y_ld + co0) * 2u;
-        bstore16(ry, ey, f32_to_bf8v(o));  // rows past Lq fall outside the descriptor: dropped
+        // rows past the output (and UPS rows before frame 0: negative offsets) fall outside the descriptor
+        const unsigned ey = (unsigned)(orow(q) * p.y_ld + c0) * 2u;
+        bstore16(ry, ey, f32_to_bf8v(o));
         bstore16(ry, ey + 16u, f32_to_bf8v(o + 8));
       }
       if (!ACC) {
-        const float m = q < p.Lq ? 1.f : 0.f;
+        const float m = (unsigned)orow(q) < (unsigned)Lrows ? 1.f : 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float x = v[r] * m;
@@ -444,7 +454,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       for (int k = 0; k < FB; ++k) {
         const int q = q0 + 32 * (nb * FB + k);
         if constexpr (RES) {
-          const unsigned er = (unsigned)((q >> p.res_shift) * p.res_ld + co0) * 2u;
+          const unsigned er = (unsigned)((UPS ? orow(q) : (q >> p.res_shift)) * p.res_ld + c0) * 2u;
           rl[k][0] = bload16(rr, er);
           rl[k][1] = bload16(rr, er + 16u);
         }
@@ -481,7 +491,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       };
       const float s1 = rs16(ts);
       const float s2 = rs16(tq);
-      atomicAdd(st_lds + 2 * (co0 + (l32 >> 1)) + (l32 & 1), (l32 & 1) ? s2 : s1);
+      atomicAdd(st_lds + 2 * (c0 + (l32 >> 1)) + (l32 & 1), (l32 & 1) ? s2 : s1);
     }
     lap(9);
   };
@@ -553,7 +563,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   // the accumulators of tile tt start at the bias.  Set right after the previous tile's epilogue
   // (not at the next group 0), so the compiler sees them dead while that epilogue reduces statistics
   auto init_acc = [&](int ch) __attribute__((always_inline)) {
-    const int co0 = ch * NCO + 32 * cb + 16 * hi;
+    const int co0 = (ch * NCO + 32 * cb + 16 * hi) % CO;  // (UPS: the bias of channel n % Cout)
     float bb[16];
     ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
     ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
@@ -684,10 +694,11 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   }
 }
 
-template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false>
+template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
+          bool UPS = false, int CO = C>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
-  using G = B2<C, NW, K, DIL, PRO, CINP>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -809,5 +820,26 @@ int st_bigconv2(const ConvParams& p, hipStream_t stream) {
                    (g_opt_bigconv == 2 && (tiles8 < b2_num_cu() || (p.Cout == 128 && p.KS >= 7)));
   if (p.Cout == 128) return two ? launch_b2_c<128, 4>(p, stream) : launch_b2_c<128, 8>(p, stream);
   if (p.Cout == 256) return two ? launch_b2_c<256, 4>(p, stream) : launch_b2_c<256, 8>(p, stream);
+  return ST_EINVAL;
+}
+
+// ---- the wide polyphase upsamplers (HiFi-GAN ups[0] 512 -> 256 x10, N = 2,560; ups[1] 256 -> 128 x5,
+// N = 640; hifigan.py:292-294 with the Snake(alphas[i]) prologue of :333 and the noise-branch residual
+// x + x_source of :335): 2 taps, on this engine instead of conv1d_igemm (STTS_OPT_UPS, default on)
+int g_opt_ups = 1;
+
+bool st_ups_eligible(const ConvParams& p, int dtype) {
+  if (!g_opt_ups || dtype != ST_BF16 || p.up <= 1 || !p.res || p.accb) return false;
+  const bool shape = (p.N == 2560 && p.Cin == 512 && p.Cout == 256) || (p.N == 640 && p.Cin == 256 && p.Cout == 128);
+  return shape && p.N == p.up * p.Cout && p.Cout % 16 == 0 && p.KS == 2 && (p.kw == 0 || p.kw == 2) &&
+         p.dil == 1 && p.stride == 1 && p.pad == 1 && p.row_off == 0 && p.pro.mode == PRO_SNAKE && p.pro.alpha &&
+         p.res_shift == 0 && p.y_row_off == 0 && !p.reflect_front && !p.epi_tanh && !p.epi_lrelu && !p.epi_gelu &&
+         !p.y_f32 && p.zc_period == 0 && p.x_ld % 8 == 0 && p.y_ld % 8 == 0 && p.res_ld % 8 == 0 &&
+         p.nchunks * 32 == p.Cin;
+}
+
+int st_bigconv2_ups(const ConvParams& p, hipStream_t s) {
+  if (p.N == 2560 && p.Cout == 256) return launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256>(p, s);
+  if (p.N == 640 && p.Cout == 128) return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128>(p, s);
   return ST_EINVAL;
 }

@@ -95,6 +95,10 @@ extern int g_opt_exp;   // STTS_OPT_EXP (bigconv2.hip, resconv.hip): A/B experim
 // the decoder front-end's k3 AdainResBlk1d convs on the bigconv2 engine (STTS_OPT_FRONT)
 bool st_front_eligible(const ConvParams& p, int dtype);
 int st_bigconv2_front(const ConvParams& p, hipStream_t stream);
+// the HiFi-GAN ups[0] / ups[1] polyphase upsamplers on the bigconv2 engine (STTS_OPT_UPS)
+extern int g_opt_ups;
+bool st_ups_eligible(const ConvParams& p, int dtype);
+int st_bigconv2_ups(const ConvParams& p, hipStream_t stream);
 extern int g_opt_front;
 // HiFi-GAN output head (head.hip): Snake -> conv_post (C -> 1, 7 taps) -> tanh as one streaming pass;
 // st_conv1d routes eligible launches to it while g_opt_head != 0

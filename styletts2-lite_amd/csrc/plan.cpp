@@ -1804,6 +1804,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_PW: g_opt_pw = (value >= 0 && value <= 2) ? value : 1; return 0;
     case STTS_OPT_SPLITK: g_opt_splitk = value ? 1 : 0; return 0;
     case STTS_OPT_EXP: g_opt_exp = value; return 0;
+    case STTS_OPT_UPS: g_opt_ups = value ? 1 : 0; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1828,6 +1829,7 @@ int stts_get_option(int key) {
     case STTS_OPT_PW: return g_opt_pw;
     case STTS_OPT_SPLITK: return g_opt_splitk;
     case STTS_OPT_EXP: return g_opt_exp;
+    case STTS_OPT_UPS: return g_opt_ups;
     default: return ST_EINVAL;
   }
 }

@@ -66,7 +66,9 @@ __device__ __forceinline__ uint4 f32_to_bf8(const float* v) {
 // no statistics (hifigan.py:336-342); otherwise statistics are kept when p.stats is set.
 // RPF: the residual / running-sum rows of tile t+1 are loaded during tile t (two register sets,
 // STTS_OPT_EXP bit 4), instead of at the start of the tile that consumes them
-template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false>
+// PF: window prefetch depth in tiles (2; 3 keeps a third raw window in flight: one block per CU at
+// C = 64 holds ~40 KB of loads in flight with two, below the ~70 KB an HBM-rate stream needs)
+template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false, int PF = 2>
 __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvParams p) {
   using G = RC<C, K, DIL, WAVES, WAVES_N>;
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, NTL = G::NTL, NCH = G::NCH, XP = G::XP, WP = G::WP;
@@ -236,7 +238,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     }
     __syncthreads();  // (A) coef / weights visible; every wave done reading Xs of the previous tile
     transform(t, pre);
-    if (t + 2 < tend) issue(t + 2, pre);
+    if (t + PF < tend) issue(t + PF, pre);
     __syncthreads();  // (B) window complete
 
     f32x16 acc[MT][NTL];
@@ -344,21 +346,31 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   if constexpr (RPF) issue_epi(tbeg, eA);
   issue(tbeg, preA);
   if (tbeg + 1 < tend) issue(tbeg + 1, preB);
-  for (int t = tbeg; t < tend; t += 2) {
-    step(t, preA, eA, eB);
-    if (t + 1 < tend) step(t + 1, preB, eB, eA);
+  if constexpr (PF == 3) {
+    uint4 preC[MAXU];
+    if (tbeg + 2 < tend) issue(tbeg + 2, preC);
+    for (int t = tbeg; t < tend; t += 3) {
+      step(t, preA, eA, eB);
+      if (t + 1 < tend) step(t + 1, preB, eB, eA);
+      if (t + 2 < tend) step(t + 2, preC, eA, eB);
+    }
+  } else {
+    for (int t = tbeg; t < tend; t += 2) {
+      step(t, preA, eA, eB);
+      if (t + 1 < tend) step(t + 1, preB, eB, eA);
+    }
   }
   if (p.stats) flush(cur_b);
 }
 
 int g_num_cu_rc = 0;
 
-template <int C, int K, int DIL, bool ACC, bool RPF = false>
+template <int C, int K, int DIL, bool ACC, bool RPF = false, int PF = 2>
 int launch_rc(const ConvParams& p, hipStream_t stream) {
   constexpr int WAVES = C == 32 ? 4 : 8;
   constexpr int WAVES_N = C == 32 ? 1 : 2;
   using G = RC<C, K, DIL, WAVES, WAVES_N>;
-  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF>;
+  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -386,6 +398,10 @@ int launch_rc_a(const ConvParams& p, hipStream_t s) {
     if ((g_opt_exp & 4) && (p.res || p.accb))
       return p.accb ? launch_rc<C, K, 1, true, true>(p, s) : launch_rc<C, K, 1, false, true>(p, s);
   }
+  // STTS_OPT_EXP bit 8 / 16: window prefetch three tiles deep at C = 64 / C = 32 (register budget allows it:
+  // 231-249 VGPRs, occupancy unchanged)
+  if ((C == 64 && (g_opt_exp & 8)) || (C == 32 && (g_opt_exp & 16)))
+    return p.accb ? launch_rc<C, K, DIL, true, false, 3>(p, s) : launch_rc<C, K, DIL, false, false, 3>(p, s);
   return p.accb ? launch_rc<C, K, DIL, true>(p, s) : launch_rc<C, K, DIL, false>(p, s);
 }
 

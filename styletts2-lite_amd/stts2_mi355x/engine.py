@@ -160,9 +160,12 @@ OPT_SKEW = 9
 OPT_FRONT = 10
 OPT_PW = 11
 OPT_SPLITK = 12
+OPT_EXP = 13
+OPT_UPS = 14
 # the production defaults of every STTS_OPT_* (include/stts2.h)
 OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
-                OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1, OPT_SKEW: 0, OPT_FRONT: 1, OPT_PW: 1, OPT_SPLITK: 1}
+                OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1, OPT_SKEW: 0, OPT_FRONT: 1, OPT_PW: 1, OPT_SPLITK: 1,
+                OPT_EXP: 0, OPT_UPS: 1}
 
 
 def set_option(key: int, value: int) -> None:

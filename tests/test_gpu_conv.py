@@ -70,7 +70,9 @@ def reference(x, w, b, gb, alpha, slope, res, scale, c):
     return y * scale
 
 
-def run_case(case, dtype, stats=True):
+def run_case(case, dtype, stats=True, res_tr=False):
+    """res_tr: a residual (scale 1) also for the transposed cases, as the HiFi-GAN upsamplers add the noise
+    branch (hifigan.py:335)."""
     name, Cin, Cout, K, tr, st, dil, pad, op, L, pro = case
     g = torch.Generator().manual_seed(hash(name) % 1000)
     B = 2
@@ -81,8 +83,8 @@ def run_case(case, dtype, stats=True):
     alpha = torch.rand(Cin, generator=g) + 0.5
     slope = 0.2
     Lout = (L - 1) * st - 2 * pad + K + op if tr else (L + 2 * pad - dil * (K - 1) - 1) // st + 1
-    res = torch.randn(B, Lout, Cout, generator=g) if not tr and not name.endswith("_nores") else None
-    scale = 0.70710677 if res is not None else 1.0
+    res = torch.randn(B, Lout, Cout, generator=g) if (res_tr or not tr) and not name.endswith("_nores") else None
+    scale = 0.70710677 if res is not None and not tr else 1.0
     ref = reference(x, w, b, gb, alpha, slope, res, scale, case)
     dev = "cuda"
     xd, wd, bd, gbd, ad = (t.to(dev).contiguous() for t in (x, w, b, gb, alpha))
@@ -250,3 +252,31 @@ def test_pw_engine(case):
     assert (y1 - y0).abs().max().item() <= 2 ** -7 * scale, case[0]
     assert torch.equal(y1, y2), case[0]
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-3, atol=1e-1)
+
+
+UPS_CASES = [c for c in CASES if c[0] in ("ups0_u10", "ups1_u5")] + [
+    ("ups0_u10_long", 512, 256, 20, 1, 10, 1, 5, 0, 700, 2),
+    ("ups1_u5_long", 256, 128, 10, 1, 5, 1, 3, 1, 2500, 2),
+]
+
+
+@pytest.mark.parametrize("cap", [0, 3])
+@pytest.mark.parametrize("case", UPS_CASES, ids=[c[0] for c in UPS_CASES])
+def test_ups_engine(case, cap):
+    """bf16: the HiFi-GAN ups[0] / ups[1] polyphase upsamplers (Snake prologue, noise-branch residual) on the
+    bigconv2 engine (STTS_OPT_UPS) against torch fp32 and against the igemm engine on the same launch (same
+    bf16 operands); cap = 3 makes every workgroup walk many tiles across output parts and utterances."""
+    try:
+        E.set_option(E.OPT_UPS, 0)
+        ref, y0, s0 = run_case(case, "bf16", res_tr=True)
+        E.set_option(E.OPT_UPS, 1)
+        E.set_option(E.OPT_GRID_CAP, cap)
+        _, y1, s1 = run_case(case, "bf16", res_tr=True)
+    finally:
+        E.reset_options()
+    tol = 0.03 * max(1.0, ref.abs().max().item() / 4)
+    assert (y1 - ref).abs().max().item() < tol, f"{case[0]}: vs torch fp32"
+    scale = max(1.0, y0.abs().max().item())
+    err = (y1 - y0).abs().max().item()
+    assert err <= 2 ** -7 * scale, f"{case[0]}: ups engine vs igemm differ by {err}"
+    np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)

@@ -1,0 +1,95 @@
+"""HBM traffic of the bigconv family per kernel instance, with the counter calibration of
+tools/calib_traffic.py applied.
+
+    python tools/traffic_calibrated.py <pmc_root> <calib_c256.json> <calib_c128.json> <out.json>
+
+<pmc_root> holds the FETCH_SIZE and WRITE_SIZE passes of tools/gpu_traffic.sh (one headline bench step,
+HiFi-GAN bf16, B = 32 x 400 frames).  Per dispatch:
+  * writes = WRITE_SIZE (calibrated exact for the epilogue's store pattern, calib mode 5);
+  * reads  = FETCH_SIZE x f_win, with f_win the measured bytes-per-counted-byte of bigconv2's own
+    64-B window row segments for the launch's row pitch (mode 2: 1.84 for 256-channel rows, 1.50 for
+    128-channel rows), except that a residual launch's residual rows are read in the epilogue's
+    32-B-per-lane pieces (mode 6): reads = (FETCH - res / f_res) x f_win + res.
+The algorithmic bytes of a launch are one read of its input rows and one write of its output rows (plus
+the residual / running-sum rows it reads), the §8(d) model.  Instances are named by their template
+arguments <C, waves, taps, dilation, residual, running sum>.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+ROWS = {256: 32 * 8000, 128: 32 * 40000}  # headline workload: B = 32, stage 0 / 1 frames per utterance
+
+
+def load(root, counter):
+    out = {}
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter or "k_bigconv2" not in r["Kernel_Name"]:
+                continue
+            d = (f, int(r["Dispatch_Id"]))
+            if d not in out:
+                out[d] = [r["Kernel_Name"], 0.0]
+            out[d][1] += float(r["Counter_Value"]) * 1024.0
+    return list(out.values())
+
+
+def factor(cal, mode):
+    return cal["modes"][str(mode)]["bytes_per_counted_byte"]
+
+
+def main():
+    root, c256, c128, dst = sys.argv[1:5]
+    cal = {256: json.load(open(c256)), 128: json.load(open(c128))}
+    fetch = load(os.path.join(root, "fetch"), "FETCH_SIZE")
+    write = load(os.path.join(root, "write"), "WRITE_SIZE")
+    per = defaultdict(lambda: {"n": 0, "fetch": 0.0, "write": 0.0})
+    for name, v in fetch:
+        per[name]["n"] += 1
+        per[name]["fetch"] += v
+    for name, v in write:
+        per[name]["write"] += v
+    res = {"workload": "hifigan bf16, B = 32 x 400 frames, one step", "instances": {}}
+    tot_cal = tot_alg = tot_raw = 0.0
+    for name, d in sorted(per.items()):
+        m = re.search(r"k_bigconv2<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false), (\d+), (\d+)", name)
+        if not m:
+            continue
+        C, NW, K, DIL = (int(m.group(i)) for i in range(1, 5))
+        RES, ACC, PRO, CINP = m.group(5) == "true", m.group(6) == "true", int(m.group(7)), int(m.group(8))
+        if PRO != 0 or C not in ROWS:
+            continue  # the front-end variant (1,090-channel rows): not calibrated, left out
+        n = d["n"]
+        fe, wr = d["fetch"] / n, d["write"] / n
+        act = ROWS[C] * C * 2
+        fw = factor(cal[C], 2)
+        resb = act * (RES + ACC)
+        reads = (fe - resb / factor(cal[C], 6)) * fw + resb if resb else fe * fw
+        alg = act * (2 + RES + ACC)
+        raw = 2 * fe + wr  # the uncalibrated x2 correction of round 2
+        key = f"<{C}, {NW}, {K}, {DIL}, {'res' if RES else '-'}, {'acc' if ACC else '-'}>"
+        res["instances"][key] = {"dispatches": n, "fetch_counter_bytes": fe, "write_bytes": wr,
+                                 "reads_calibrated": reads, "hbm_calibrated": reads + wr, "algorithmic": alg,
+                                 "ratio_calibrated": (reads + wr) / alg, "ratio_x2_correction": raw / alg}
+        tot_cal += (reads + wr) * n
+        tot_alg += alg * n
+        tot_raw += raw * n
+        print(f"{key:28s} x{n:3d}  calibrated {(reads + wr) / 1e6:7.1f} MB  x2-corrected {raw / 1e6:7.1f} MB  "
+              f"algorithmic {alg / 1e6:7.1f} MB  ratio {(reads + wr) / alg:.3f} (x2: {raw / alg:.3f})")
+    res["total"] = {"calibrated": tot_cal, "algorithmic": tot_alg, "x2_corrected": tot_raw,
+                    "ratio_calibrated": tot_cal / tot_alg if tot_alg else None}
+    res["calibration"] = {"window_f_c256": factor(cal[256], 2), "window_f_c128": factor(cal[128], 2),
+                          "residual_f_c256": factor(cal[256], 6), "residual_f_c128": factor(cal[128], 6),
+                          "store_f_c256": factor(cal[256], 5)}
+    print(f"total: calibrated {tot_cal / 1e9:.2f} GB vs algorithmic {tot_alg / 1e9:.2f} GB "
+          f"({tot_cal / tot_alg:.3f}); x2-corrected {tot_raw / 1e9:.2f} GB")
+    with open(dst, "w") as fh:
+        json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
