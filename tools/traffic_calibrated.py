@@ -29,7 +29,7 @@ def load(root, counter):
     out = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter or "k_bigconv2" not in r["Kernel_Name"]:
+            if r["Counter_Name"] != counter or "k_bigconv" not in r["Kernel_Name"]:
                 continue
             d = (f, int(r["Dispatch_Id"]))
             if d not in out:
@@ -55,6 +55,22 @@ def main():
         per[name]["write"] += v
     res = {"workload": "hifigan bf16, B = 32 x 400 frames, one step", "instances": {}}
     tot_cal = tot_alg = tot_raw = 0.0
+    # family level (every k_bigconv* dispatch): calibrated where the instance's read pattern was calibrated
+    # (bigconv2 resblock convs, 256- / 128-channel rows), else the guide's x2 for wide reads
+    fam_bytes, fam_n, fam_uncal = 0.0, 0, 0
+    for name, d in per.items():
+        m = re.search(r"k_bigconv2<(\d+), \d+, \d+, \d+, (true|false), (true|false), 0, (\d+)", name)
+        C = int(m.group(1)) if m else 0
+        if m and C in ROWS and int(m.group(4)) == C:
+            act = ROWS[C] * C * 2
+            resb = act * ((m.group(2) == "true") + (m.group(3) == "true"))
+            fe = d["fetch"] / d["n"]
+            rd = (fe - resb / factor(cal[C], 6)) * factor(cal[C], 2) + resb if resb else fe * factor(cal[C], 2)
+            fam_bytes += (rd + d["write"] / d["n"]) * d["n"]
+        else:
+            fam_bytes += 2 * d["fetch"] + d["write"]
+            fam_uncal += d["n"]
+        fam_n += d["n"]
     for name, d in sorted(per.items()):
         m = re.search(r"k_bigconv2<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false), (\d+), (\d+)", name)
         if not m:
@@ -87,6 +103,13 @@ def main():
                           "store_f_c256": factor(cal[256], 5)}
     print(f"total: calibrated {tot_cal / 1e9:.2f} GB vs algorithmic {tot_alg / 1e9:.2f} GB "
           f"({tot_cal / tot_alg:.3f}); x2-corrected {tot_raw / 1e9:.2f} GB")
+    res.update({"kernel": "k_bigconv", "decoder": "hifigan", "dtype": "bf16", "batch": 32, "frames": 400,
+                "hbm_bytes_per_launch": fam_bytes / fam_n, "dispatches": fam_n, "dispatches_uncalibrated": fam_uncal,
+                "correction": "per-pattern calibration (tools/calib_traffic.py): bigconv2 resblock launches "
+                              "reads = FETCH x f_window (+ residual rows at f_residual), writes = WRITE_SIZE; "
+                              "other k_bigconv* launches (front-end, v1, upsamplers) 2 x FETCH + WRITE"})
+    print(f"family k_bigconv: {fam_bytes / fam_n / 1e6:.1f} MB per launch over {fam_n} dispatches "
+          f"({fam_uncal} with the uncalibrated x2)")
     with open(dst, "w") as fh:
         json.dump(res, fh, indent=1)
 
