@@ -383,6 +383,12 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_UPS      1 = the HiFi-GAN ups[0] / ups[1] polyphase upsamplers (N = 2,560 / 640) on the bigconv2
  *                     engine (default); 0 = on conv1d_igemm. */
 #define STTS_OPT_UPS 14
+/*   STTS_OPT_WGRAD    1 = the bf16 weight gradient of stride-1 convs (stts_conv1d_bwd, training step) on the
+ *                     all-taps window kernel k_wgrad_bf16w (default); 0 = the per-tap kernel. */
+#define STTS_OPT_WGRAD 15
+/*   STTS_OPT_PLAINRC  1 = prologue-free C = 32 / 64 'same' convs (the training step's conv forwards and dx) on the
+ *                     resconv engine (default); 0 = on conv1d_igemm. */
+#define STTS_OPT_PLAINRC 16
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

@@ -23,6 +23,8 @@
 #include "common.h"
 #include "kernels.h"
 
+int g_opt_wgw = 1;  // k_wgrad_bf16w for the stride-1 convs (STTS_OPT_WGRAD); 0 = the per-tap kernel everywhere
+
 namespace {
 
 constexpr int kTargetWaves = 2048;  // 8 waves per CU on 256 CUs
@@ -220,6 +222,159 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16(const float* __restrict__ x,
     }
 }
 
+// Stride-1 convolutions (every decoder resblock / front-end conv, conv_post, the 1x1s): one workgroup owns a
+// 64 co x 64 ci tile for ALL K taps over a slice of 64-row chunks (chunks never cross an utterance; a slice
+// may span several short utterances, so the slice count and the partials stay small at any batch), and
+// stages per chunk the dy rows
+// and ONE x window of 64 + (K-1) dil rows, read at K row offsets (the per-tap kernel above stages K separate
+// x chunks).  Wave w = (co half w >> 1, ci half w & 1) accumulates K 32 x 32 fragments.  The next chunk's fp32
+// rows are loaded into registers while the current chunk's MFMAs run; LDS is double-buffered (one barrier per
+// chunk).  Partials part[s][t][co][ci] with s = utterance x slice, summed in order by k_slice_reduce.
+constexpr int WGW_CH = 64, WGW_DILMAX = 5;
+
+// 4 fp32 channels c .. c + 3 of a row (zeros past C or when !ok)
+__device__ __forceinline__ float4 ld4(const float* __restrict__ row, int c, int C, bool ok) {
+  if (ok && c + 4 <= C && (C & 3) == 0) return *reinterpret_cast<const float4*>(row + c);
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (ok && c + j < C) ? row[c + j] : 0.f;
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// ST > 1 (the discriminators' strided convs, dilation 1): the window is stored phase-split, ST blocks of PR
+// rows, block ph holding window rows ph, ph + ST, ...; tap t then reads block (t mod ST) from row t / ST on,
+// again consecutive rows for the transposed fragment reads.
+template <int K, int ST = 1>
+__global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x, const float* __restrict__ dy, int Lin,
+                                                     int Cin, int Lq, int Cout, int dil, int pad, int B, int S,
+                                                     int ntci, float* __restrict__ part) {
+  constexpr int DMAX = ST == 1 ? WGW_DILMAX : 1;
+  constexpr int PR = WGW_CH + ((K - 1) * DMAX + ST - 1) / ST;  // rows per phase block
+  constexpr int WMAX = ST * PR;                                // x window rows (LDS)
+  constexpr int XPT = (WMAX + 63) / 64;                        // x window rows per thread (4 threads per row)
+  constexpr int BUF = (WGW_CH + WMAX) * WGB_STRIDE;    // one stage: dy rows then the x window
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fi = w >> 1, fj = w & 1;
+  const int tci = blockIdx.x % ntci, tco = blockIdx.x / ntci;
+  const int co0 = tco * 64, ci0 = tci * 64;
+  const int sl = blockIdx.y;
+  const int ncb = (Lq + WGW_CH - 1) / WGW_CH;  // chunks per utterance
+  const long long U = (long long)B * ncb;      // chunk units (utterance, chunk), in order
+  const int u0 = (int)(U * sl / S), u1 = (int)(U * (sl + 1) / S);
+  const int WR = (WGW_CH - 1) * ST + (K - 1) * dil + 1;  // window rows the chunk reads
+  // staging: thread -> row (tid >> 2) (+ 64 j for the window), channels 16 (tid & 3) .. + 16
+  const int rr = tid >> 2, c16 = (tid & 3) * 16;
+  float4 pd[4], px[XPT][4];
+  auto load = [&](int u) __attribute__((always_inline)) {
+    const int b = u / ncb, qc = (u - b * ncb) * WGW_CH;
+    const float* dyb = dy + (size_t)b * Lq * Cout;
+    const float* xb = x + (size_t)b * Lin * Cin;
+    const int q = qc + rr;
+    const bool okd = q < Lq;
+    const int cc = co0 + c16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = cc + 4 * j;
+      pd[j] = ld4(dyb + (size_t)(okd ? q : 0) * Cout, c, Cout, okd);
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int wr = rr + 64 * i;                  // LDS row: phase block wr / PR, row wr % PR
+      const int j = ST == 1 ? wr : (wr % PR) * ST + wr / PR;  // window row
+      const int xr = qc * ST - pad + j;
+      const bool ok = wr < WMAX && j < WR && xr >= 0 && xr < Lin;
+      const int c0 = ci0 + c16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + 4 * j;
+        px[i][j] = ld4(xb + (size_t)(ok ? xr : 0) * Cin, c, Cin, ok);
+      }
+    }
+  };
+  auto st8 = [&](char* dst, const float4& a, const float4& c) __attribute__((always_inline)) {
+    bf16x8 o;
+    o[0] = (bf16_t)a.x; o[1] = (bf16_t)a.y; o[2] = (bf16_t)a.z; o[3] = (bf16_t)a.w;
+    o[4] = (bf16_t)c.x; o[5] = (bf16_t)c.y; o[6] = (bf16_t)c.z; o[7] = (bf16_t)c.w;
+    *reinterpret_cast<bf16x8*>(dst) = o;
+  };
+  auto store = [&](char* buf) __attribute__((always_inline)) {
+    char* d = buf + rr * WGB_STRIDE + c16 * 2;
+    st8(d, pd[0], pd[1]);
+    st8(d + 16, pd[2], pd[3]);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int wr = rr + 64 * i;
+      if (wr < WMAX) {
+        char* e = buf + (WGW_CH + wr) * WGB_STRIDE + c16 * 2;
+        st8(e, px[i][0], px[i][1]);
+        st8(e + 16, px[i][2], px[i][3]);
+      }
+    }
+  };
+  f32x16 acc[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  // a wave whose 32-channel block lies past Cout / Cin computes nothing (wave-uniform)
+  const bool live = co0 + 32 * fi < Cout && ci0 + 32 * fj < Cin;
+  const int nch = u1 - u0;
+  if (nch > 0) {
+    load(u0);
+    store(lds);
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    char* cur = lds + (c & 1) * BUF;
+    if (c + 1 < nch) load(u0 + c + 1);  // in flight under this chunk's MFMAs
+    if (live) {
+#pragma unroll
+      for (int ks = 0; ks < WGW_CH / 16; ++ks) {
+        const bf16x8 a = tr_frag(cur, ks, fi, lane);
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+          const int tj = t * dil;
+          const int row = ST == 1 ? tj : (tj % ST) * PR + tj / ST;
+          const bf16x8 bx = tr_frag(cur + (WGW_CH + row) * WGB_STRIDE, ks, fj, lane);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    if (c + 1 < nch) store(lds + ((c + 1) & 1) * BUF);
+    __syncthreads();
+  }
+  if (!live) return;
+  float* pt = part + (size_t)sl * K * Cout * Cin;
+#pragma unroll
+  for (int t = 0; t < K; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int co = co0 + 32 * fi + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      const int ci = ci0 + 32 * fj + (lane & 31);
+      if (co < Cout && ci < Cin) pt[((size_t)t * Cout + co) * Cin + ci] = acc[t][e];
+    }
+}
+
+// slices for k_wgrad_bf16w: about 1,024 workgroups, >= 2 chunks per slice
+int wgw_slices(int B, int Lq, int Cin, int Cout) {
+  const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64);
+  const long long units = (long long)B * ((Lq + WGW_CH - 1) / WGW_CH);
+  long long S = (1024 + tiles - 1) / tiles;
+  S = std::min<long long>(S, std::max<long long>(1, units / 2));
+  return (int)std::max<long long>(1, std::min<long long>(S, 4096));
+}
+
+bool wgw_eligible(int K, int stride, int dil) {
+  if (stride == 1)
+    return dil >= 1 && dil <= WGW_DILMAX && (K == 1 || K == 2 || K == 3 || K == 5 || K == 7 || K == 9 || K == 11);
+  if (dil != 1) return false;
+  if (stride == 2) return K == 3 || K == 4 || K == 9;  // F0 / N convs, ups[3] dw, MSD
+  if (stride == 3) return K == 5 || K == 6;            // MPD, ups[2] dw
+  return false;
+}
+
 struct SlicesB {
   int ntco, ntci, ntg, S;
 };
@@ -387,7 +542,11 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
     const Slices sl = slices_of(g);
     w.part = off;
     size_t ns = (size_t)sl.S;
-    if (dtype == ST_BF16) ns = std::max(ns, (size_t)slices_bf16(g.B, g.Lq, g.Cin, g.Cout, g.K).S);
+    if (dtype == ST_BF16) {
+      ns = std::max(ns, (size_t)slices_bf16(g.B, g.Lq, g.Cin, g.Cout, g.K).S);
+      if (wgw_eligible(g.K, g.stride, g.dil))
+        ns = std::max(ns, (size_t)wgw_slices(g.B, g.Lq, g.Cin, g.Cout));
+    }
     off += al(ns * g.K * g.Cout * g.Cin * 4);
     w.part2 = off;
     off += al((size_t)sl.S2 * g.Cout * 8);
@@ -489,8 +648,41 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   return 0;
 }
 
+template <int K, int ST = 1>
+void launch_wgw(const Geo& g, const float* x, const float* dy, float* part, int S, hipStream_t s) {
+  const int ntci = (g.Cin + 63) / 64, ntco = (g.Cout + 63) / 64;
+  hipLaunchKernelGGL((k_wgrad_bf16w<K, ST>), dim3(ntco * ntci, S), dim3(256), 0, s, x, dy, g.Lin, g.Cin, g.Lq, g.Cout,
+                     g.dil, g.pad, g.B, S, ntci, part);
+}
+
 // dw as per-slice partials + the in-order reduction into dw [Cout][Cin][K]
 int wgrad_bf16(const Geo& g, const float* x, const float* dy, float* part, float* dw, hipStream_t s) {
+  if (g_opt_wgw && wgw_eligible(g.K, g.stride, g.dil)) {
+    const int Sb = wgw_slices(g.B, g.Lq, g.Cin, g.Cout);
+    if (g.stride == 2) {
+      if (g.K == 3) launch_wgw<3, 2>(g, x, dy, part, Sb, s);
+      else if (g.K == 4) launch_wgw<4, 2>(g, x, dy, part, Sb, s);
+      else launch_wgw<9, 2>(g, x, dy, part, Sb, s);
+    } else if (g.stride == 3) {
+      if (g.K == 5) launch_wgw<5, 3>(g, x, dy, part, Sb, s);
+      else launch_wgw<6, 3>(g, x, dy, part, Sb, s);
+    } else {
+      switch (g.K) {
+        case 1: launch_wgw<1>(g, x, dy, part, Sb, s); break;
+        case 2: launch_wgw<2>(g, x, dy, part, Sb, s); break;
+        case 3: launch_wgw<3>(g, x, dy, part, Sb, s); break;
+        case 5: launch_wgw<5>(g, x, dy, part, Sb, s); break;
+        case 7: launch_wgw<7>(g, x, dy, part, Sb, s); break;
+        case 9: launch_wgw<9>(g, x, dy, part, Sb, s); break;
+        default: launch_wgw<11>(g, x, dy, part, Sb, s); break;
+      }
+    }
+    ST_CHECK_HIP(hipGetLastError());
+    const size_t n = (size_t)g.K * g.Cout * g.Cin;
+    hipLaunchKernelGGL(k_slice_reduce<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, Sb, g.K,
+                       g.Cout, g.Cin, dw);
+    return (int)hipGetLastError();
+  }
   const SlicesB sl = slices_bf16(g.B, g.Lq, g.Cin, g.Cout, g.K);
   const long long R = (long long)g.B * g.Lq;
   if (R > 0x7fffffffLL) return ST_EINVAL;

@@ -221,20 +221,39 @@ __global__ void k_adain_bwd_dx(const float* __restrict__ x, const float* __restr
 }
 
 // Linear backward (h = s W^T + bias; s [B][K], W [N][K], dh [B][N]), fp64 sums in fixed order.
-// ds[b][k] = sum_n dh[b][n] W[n][k]: one workgroup per (b, 64 k columns); its 4 waves stride n (a wave
-// reads 64 consecutive k of one W row: coalesced), then a fixed 4-way LDS sum.  (One thread per (b, k)
-// over all N = 2 C rows had B K = 256 threads for the whole GPU: 150 us a call.)
-__global__ __launch_bounds__(256) void k_linear_bwd_ds(const float* __restrict__ W, const float* __restrict__ dh,
-                                                       int B, int K, int N, float* __restrict__ ds) {
-  __shared__ double red[4][64];
+// ds[b][k] = sum_n dh[b][n] W[n][k]: one workgroup per (b, 64 k columns); its 16 waves stride n (a wave
+// reads 64 consecutive k of one W row: coalesced), each with 8 independent fp64 partials (loads in flight
+// instead of one dependent chain), then fixed-order sums (8-way in registers, 16-way in LDS): deterministic.
+// (4 waves with one chain each took ~40 us a call; one thread per (b, k) over all N = 2 C rows, 150 us.)
+__global__ __launch_bounds__(1024) void k_linear_bwd_ds(const float* __restrict__ W, const float* __restrict__ dh,
+                                                        int B, int K, int N, float* __restrict__ ds) {
+  constexpr int NW = 16, U = 8;
+  __shared__ double red[NW][64];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + l, b = blockIdx.y;
-  double acc = 0.0;
-  if (k < K)
-    for (int n = w; n < N; n += 4) acc += (double)dh[(size_t)b * N + n] * W[(size_t)n * K + k];
-  red[w][l] = acc;
+  double acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = 0.0;
+  if (k < K) {
+    const float* dhb = dh + (size_t)b * N;
+    int n = w;
+    for (; n + (U - 1) * NW < N; n += U * NW) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] += (double)dhb[n + u * NW] * W[(size_t)(n + u * NW) * K + k];
+    }
+    for (; n < N; n += NW) acc[0] += (double)dhb[n] * W[(size_t)n * K + k];
+  }
+  double t = 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) t += acc[u];
+  red[w][l] = t;
   __syncthreads();
-  if (w == 0 && k < K) ds[(size_t)b * K + k] = (float)(((red[0][l] + red[1][l]) + red[2][l]) + red[3][l]);
+  if (w == 0 && k < K) {
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) r += red[i][l];
+    ds[(size_t)b * K + k] = (float)r;
+  }
 }
 
 __global__ void k_linear_bwd_dw(const float* __restrict__ s, const float* __restrict__ dh, int B, int K, int N,
@@ -499,7 +518,7 @@ extern "C" int stts_linear_bwd(const float* s_in, const float* W, const float* d
   if (!dh || B <= 0 || K <= 0 || N <= 0 || (ds && !W) || (dW && !s_in)) return ST_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (ds) {
-    hipLaunchKernelGGL(k_linear_bwd_ds, dim3((K + 63) / 64, B), dim3(256), 0, s, W, dh, B, K, N, ds);
+    hipLaunchKernelGGL(k_linear_bwd_ds, dim3((K + 63) / 64, B), dim3(1024), 0, s, W, dh, B, K, N, ds);
     ST_CHECK_HIP(hipGetLastError());
   }
   if (dW || db) {

@@ -1805,6 +1805,8 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_SPLITK: g_opt_splitk = value ? 1 : 0; return 0;
     case STTS_OPT_EXP: g_opt_exp = value; return 0;
     case STTS_OPT_UPS: g_opt_ups = value ? 1 : 0; return 0;
+    case STTS_OPT_WGRAD: g_opt_wgw = value ? 1 : 0; return 0;
+    case STTS_OPT_PLAINRC: g_opt_plainrc = value ? 1 : 0; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1830,6 +1832,8 @@ int stts_get_option(int key) {
     case STTS_OPT_SPLITK: return g_opt_splitk;
     case STTS_OPT_EXP: return g_opt_exp;
     case STTS_OPT_UPS: return g_opt_ups;
+    case STTS_OPT_WGRAD: return g_opt_wgw;
+    case STTS_OPT_PLAINRC: return g_opt_plainrc;
     default: return ST_EINVAL;
   }
 }

@@ -219,6 +219,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
       if (cur_b >= 0 && p.stats) flush(cur_b);
       // every wave is past its previous transform (barrier B of the previous step): coef is free
       for (int ci = tid; ci < C; ci += NT) {
+        if (p.pro.mode == 0) {  // plain conv (the training step's convs, normalised by their own kernel):
+          coef[ci] = 0.f;       // x2 = v, cosine term times 0 -> the transform is exactly the identity
+          coef[C + ci] = 1.f;
+          coef[2 * C + ci] = coef[3 * C + ci] = coef[4 * C + ci] = 0.f;
+          continue;
+        }
         float mm, aa, be;
         adain_coeffs(p.pro, b, ci, mm, aa, be);
         const float al = p.pro.alpha[ci];
@@ -427,6 +433,8 @@ int launch_rc_k(const ConvParams& p, hipStream_t s) {
 
 }  // namespace
 
+int g_opt_plainrc = 1;
+
 bool st_resconv_eligible(const ConvParams& p, int dtype) {
   if (dtype != ST_BF16) return false;
   const int C = p.Cout;
@@ -435,7 +443,9 @@ bool st_resconv_eligible(const ConvParams& p, int dtype) {
   if ((p.kw != 0 && p.kw != p.KS) || p.row_off != 0 || p.stride != 1 || p.up != 1 || p.opad != 0) return false;
   if (p.pad != p.dil * (p.KS - 1) / 2 || p.Lq != p.Lout || p.Lq != p.Lin) return false;
   if (p.y_row_off || p.y_f32 || p.epi_tanh || p.epi_lrelu || p.epi_gelu || p.reflect_front || p.zc_period || p.res_shift) return false;
-  if (p.pro.mode != (PRO_AFFINE | PRO_SNAKE) || !p.pro.alpha || !p.pro.stats || !p.pro.gamma) return false;
+  // AdaIN -> Snake (the decoder), or no prologue (the training step's convs, STTS_OPT_PLAINRC)
+  const bool snake = p.pro.mode == (PRO_AFFINE | PRO_SNAKE) && p.pro.alpha && p.pro.stats && p.pro.gamma;
+  if (!snake && !(p.pro.mode == 0 && g_opt_plainrc)) return false;
   if (p.accb && p.stats) return false;  // the running-sum launch keeps no statistics
   if (p.x_ld % 8 || p.y_ld % 8 || (p.res && p.res_ld % 8) || (p.accb && p.acc_ld % 8)) return false;
   return true;

@@ -45,8 +45,6 @@ def _rel(a, ref):
 def test_conv1d_fwd_bwd(case, dtype):
     from stts2_mi355x.training import conv1d, out_length
     B, Cin, Cout, K, stride, dil, pad, Lin = case
-    if dtype == "bf16" and Lin > 10000:
-        pytest.skip("fp32 covers the long case")
     g = torch.Generator().manual_seed(hash(case) % 2**31)
     x = torch.randn(B, Cin, Lin, generator=g)
     w = torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)
@@ -136,3 +134,62 @@ def test_conv_transpose1d_fwd_bwd(case, dtype):
     print(case, dtype, {k: f"{v:.2e}" for k, v in errs.items()})
     assert errs["y"] < tol and errs["dx"] < tol
     assert errs["dw"] < tol and errs["db"] < 1e-5
+
+
+WGW_CASES = CASES  # stride 1, and the strided (2 / 3) discriminator / F0 convs on the phase-split window
+
+
+@pytest.mark.parametrize("case", WGW_CASES, ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_d{}_p{}_L{}".format(*c))
+def test_wgrad_window_kernel_matches_per_tap(case):
+    """bf16 dw: the all-taps window kernel (k_wgrad_bf16w, STTS_OPT_WGRAD = 1; strides 2 / 3 on a phase-split
+    window) against the per-tap kernel (0) on the same inputs: the same bf16 operands, fp32 accumulation in a
+    different order."""
+    from stts2_mi355x import engine as E
+    from stts2_mi355x.training import conv1d, out_length
+    B, Cin, Cout, K, stride, dil, pad, Lin = case
+    g = torch.Generator().manual_seed(7 + hash(case) % 1000)
+    x = torch.randn(B, Cin, Lin, generator=g).cuda()
+    w = (torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)).cuda()
+    gy = torch.randn(B, Cout, out_length(Lin, K, stride, pad, dil), generator=g).cuda()
+    dws = []
+    try:
+        for opt in (1, 0):
+            E.set_option(E.OPT_WGRAD, opt)
+            wc = w.clone().requires_grad_(True)
+            conv1d(x, wc, None, stride, pad, dil, dtype="bf16").backward(gy)
+            dws.append(wc.grad.detach().cpu().double())
+    finally:
+        E.reset_options()
+    err = float((dws[0] - dws[1]).abs().max() / dws[1].abs().max())
+    assert err < 2e-5, f"window vs per-tap dw differ by {err:.2e} of max"
+
+
+PLAIN_CASES = [c for c in CASES if c[4] == 1 and c[1] == c[2] and c[1] in (32, 64)]
+
+
+@pytest.mark.parametrize("case", PLAIN_CASES, ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_d{}_p{}_L{}".format(*c))
+def test_plain_resconv_matches_igemm(case):
+    """bf16 forward and dx of the training step's C = 32 / 64 'same' convs: on the resconv engine with its
+    transform set to the identity (STTS_OPT_PLAINRC = 1) against conv1d_igemm (0), same bf16 operands."""
+    from stts2_mi355x import engine as E
+    from stts2_mi355x.training import conv1d, out_length
+    B, Cin, Cout, K, stride, dil, pad, Lin = case
+    g = torch.Generator().manual_seed(11 + hash(case) % 1000)
+    x = torch.randn(B, Cin, Lin, generator=g).cuda()
+    w = (torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    gy = torch.randn(B, Cout, out_length(Lin, K, stride, pad, dil), generator=g).cuda()
+    outs = []
+    try:
+        for opt in (1, 0):
+            E.set_option(E.OPT_PLAINRC, opt)
+            xc = x.clone().requires_grad_(True)
+            y = conv1d(xc, w, b, stride, pad, dil, dtype="bf16")
+            y.backward(gy)
+            outs.append((y.detach().cpu().double(), xc.grad.detach().cpu().double()))
+    finally:
+        E.reset_options()
+    for k, name in enumerate(("y", "dx")):
+        a, r = outs[0][k], outs[1][k]
+        err = float((a - r).abs().max() / r.abs().max())
+        assert err < 2 ** -7, f"{name}: resconv vs igemm differ by {err:.2e} of max"
