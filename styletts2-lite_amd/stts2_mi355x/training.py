@@ -152,6 +152,44 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
     return conv1d_frames(x.transpose(1, 2), weight, bias, stride, padding, dilation, dtype).transpose(1, 2)
 
 
+# stride-2 convs (the MSD's N = 32 layers, F0 / N convs) run as stride-1 convs over phase-folded frames (see
+# _fold_strided); False = the engines' own strided paths (tests compare the two).  Stride 3 (MPD) keeps the
+# strided path: its folded form (3 C input channels, 2 taps) measured no faster.
+FOLD_STRIDED = True
+_FOLD_MAPS = {}
+
+
+def _fold_map(K, stride, pad):
+    """(K', pad', [(phase, k', t)]) of the stride-1 conv equivalent to a stride-`stride` one: input row
+    stride q + t - pad = stride (q + s') + ph, k' = s' - s'_min."""
+    key = (K, stride, pad)
+    if key not in _FOLD_MAPS:
+        js = [t - pad for t in range(K)]
+        smin, smax = min(j // stride for j in js), max(j // stride for j in js)
+        _FOLD_MAPS[key] = (smax - smin + 1, -smin, [(j % stride, j // stride - smin, t) for t, j in enumerate(js)])
+    return _FOLD_MAPS[key]
+
+
+def _fold_strided(x, weight, stride, padding):
+    """A Conv1d(stride s, dilation 1) y[q] = sum_t w[t] x[s q + t - pad] is the stride-1 conv
+    y[q] = sum_k' w'[k'] x'[q + k' - pad'] over the frames x'[m] = (x[s m], x[s m + 1], ..., x[s m + s - 1])
+    (a free view of the contiguous frames [B, L, C] as [B, L / s, s C], rows padded to a multiple of s),
+    with w'[k'][(ph, ci)] = w[t] where s (k' - pad') + ph = t - pad (zero elsewhere).  So the MSD / MPD
+    strided convs run on the stride-1 engines (full MFMA columns at N = 32, stride-1 dx and dw) instead of the
+    strided igemm tile (64 rows x 128 columns).  Autograd goes through the view and the weight gather."""
+    B, Lin, Cin = x.shape
+    Cout, _, K = weight.shape
+    K2, pad2, taps = _fold_map(K, stride, padding)
+    L2 = -(-Lin // stride)
+    if L2 * stride != Lin:
+        x = torch.nn.functional.pad(x, (0, 0, 0, L2 * stride - Lin))
+    x2 = x.reshape(B, L2, stride * Cin)
+    w2 = weight.new_zeros(Cout, stride, Cin, K2)
+    for ph, k2, t in taps:
+        w2[:, ph, :, k2] = weight[:, :, t]
+    return x2, w2.reshape(Cout, stride * Cin, K2), pad2
+
+
 def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32", residual=None, scale=1.0):
     """conv1d on frames tensors: x [B, Lin, Cin] -> [B, Lq, Cout] (the kernels' native layout);
     `residual` (frames [B, Lq, Cout], fp32 runs) is added and the sum multiplied by `scale` in the
@@ -160,7 +198,13 @@ def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="
         raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
     if residual is None and scale != 1.0:
         raise ValueError("conv1d_frames: `scale` applies to the residual sum; pass a residual or scale 1")
-    return _Conv1dFn.apply(x, weight, bias, int(stride), int(padding), int(dilation), dtype, residual, float(scale))
+    stride, padding, dilation = int(stride), int(padding), int(dilation)
+    if FOLD_STRIDED and stride == 2 and dilation == 1 and residual is None:
+        Lq = out_length(x.shape[1], weight.shape[-1], stride, padding, 1)
+        x2, w2, pad2 = _fold_strided(x, weight, stride, padding)
+        y = _Conv1dFn.apply(x2, w2, bias, 1, pad2, 1, dtype, None, 1.0)
+        return y[:, :Lq] if y.shape[1] != Lq else y
+    return _Conv1dFn.apply(x, weight, bias, stride, padding, dilation, dtype, residual, float(scale))
 
 
 class Conv1d(nn.Conv1d):

@@ -193,3 +193,34 @@ def test_plain_resconv_matches_igemm(case):
         a, r = outs[0][k], outs[1][k]
         err = float((a - r).abs().max() / r.abs().max())
         assert err < 2 ** -7, f"{name}: resconv vs igemm differ by {err:.2e} of max"
+
+
+STRIDED_CASES = [c for c in CASES if c[4] > 1]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", STRIDED_CASES, ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_d{}_p{}_L{}".format(*c))
+def test_folded_strided_conv_matches_engine_stride(case, dtype):
+    """Strided convs as stride-1 convs over phase-folded frames (training.FOLD_STRIDED, the default) against
+    the engines' own strided path, forward and every gradient (fp32: the same sums in another order)."""
+    from stts2_mi355x import training as T
+    B, Cin, Cout, K, stride, dil, pad, Lin = case
+    g = torch.Generator().manual_seed(3 + hash(case) % 1000)
+    x = torch.randn(B, Cin, Lin, generator=g).cuda()
+    w = (torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    gy = torch.randn(B, Cout, T.out_length(Lin, K, stride, pad, dil), generator=g).cuda()
+    res = []
+    try:
+        for fold in (True, False):
+            T.FOLD_STRIDED = fold
+            xc, wc, bc = (t.clone().requires_grad_(True) for t in (x, w, b))
+            y = T.conv1d(xc, wc, bc, stride, pad, dil, dtype=dtype)
+            y.backward(gy)
+            res.append([t.detach().double().cpu() for t in (y, xc.grad, wc.grad, bc.grad)])
+    finally:
+        T.FOLD_STRIDED = True
+    tol = 1e-5 if dtype == "fp32" else 2e-2
+    for name, a, r in zip(("y", "dx", "dw", "db"), res[0], res[1]):
+        err = float((a - r).abs().max() / max(r.abs().max().item(), 1e-30))
+        assert err < tol, f"{name}: folded vs strided differ by {err:.2e} of max"

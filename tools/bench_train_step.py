@@ -95,7 +95,11 @@ def main():
     ap.add_argument("--B", type=int, default=2)
     ap.add_argument("--T", type=int, default=155)
     ap.add_argument("--cpu-baseline", action="store_true")
+    ap.add_argument("--no-fold", action="store_true", help="strided convs on the engines' strided path")
     a = ap.parse_args()
+    if a.no_fold:
+        from stts2_mi355x import training
+        training.FOLD_STRIDED = False
     for dt in a.dtypes.split(","):
         print(json.dumps(run_gpu(dt, a.B, a.T, a.steps, a.warmup)), flush=True)
     if a.cpu_baseline:

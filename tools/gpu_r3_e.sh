@@ -1,0 +1,11 @@
+# Round-3: fold A/B on the config-5 step, MPD/step tests.
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_train_layers.py tests/test_gpu_train_step.py tests/test_gpu_train_conv.py -q -x -rfE --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_train.log 2>&1
+rc=$?
+tail -3 gpurun_out/pytest_train.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/bench_train_step.py --dtypes bf16 --steps 5 --warmup 2 > gpurun_out/bench_train_fold.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/bench_train_step.py --dtypes bf16 --steps 5 --warmup 2 --no-fold > gpurun_out/bench_train_nofold.log 2>&1 || exit $?
+cut -c1-200 gpurun_out/bench_train_fold.log gpurun_out/bench_train_nofold.log | grep config5
