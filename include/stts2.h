@@ -389,6 +389,10 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_PLAINRC  1 = prologue-free C = 32 / 64 'same' convs (the training step's conv forwards and dx) on the
  *                     resconv engine (default); 0 = on conv1d_igemm. */
 #define STTS_OPT_PLAINRC 16
+/*   STTS_OPT_MSDFOLD  1 = MultiResSpecDiscriminator models created from now on run their stride-2 layers as
+ *                     stride-1 convs over phase-folded frames (weights folded at pack time; default); 0 = the
+ *                     strided conv path.  Read at stts_model_create. */
+#define STTS_OPT_MSDFOLD 17
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

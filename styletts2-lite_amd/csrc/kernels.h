@@ -177,6 +177,7 @@ int st_noise_conv(const float* har, int B, int L, const float* w, const float* b
 int st_har_frames(const float* har, int B, int L, int S, int P, int rows, int ld, void* x, int dtype, hipStream_t s);
 // noise_convs weight [C][1][2S] -> [C][S][2] (the 2-tap conv over S-sample frames)
 int st_reframe_w(const float* w, int C, int S, float* out, hipStream_t s);
+int st_fold_w(const float* w, int Cout, int Cin, int K, int st, int pad, int K2, int pad2, float* out, hipStream_t s);
 // SineGen phase: ph[b][h][j] = ((cumsum_f64(rad)[j] * 2) * pi) * scale  (fp32)
 int st_sine_phase(const float* f0, int B, int n, int scale, float* ph, hipStream_t s);
 // SineGen + SourceModuleHnNSF: har[b][t] (fp32), t < n*scale
@@ -267,7 +268,7 @@ int st_logmel(const float* x, int S, long long L, long long ld, int n_fft, int w
 int st_stft_mag_x3(const float* x, int S, long long L, long long ld, int n_fft, int win, int hop, void* x3, int dtype,
                    hipStream_t s);
 // x3[s][h][w][c * 3 + dh] = y[s][h + dh - 1][w][c], 0 outside [0, H)
-int st_time_expand(const void* y, int S, int H, int W, int C, void* x3, int dtype, hipStream_t s);
+int st_time_expand(const void* y, int S, int H, int W, int C, void* x3, int dtype, hipStream_t s, int We = 0);
 // SpectralConvergengeLoss numerator / denominator partials of one resolution: part[blk][0] = sum |y - x|,
 // part[blk][1] = sum |y| over a fixed split of the n elements (st_sc_part_bytes(1) bytes per resolution)
 int st_sc_sums(const float* xm, const float* ym, long long n, double* part, hipStream_t s);

@@ -1047,3 +1047,27 @@ int st_reframe_w(const float* w, int C, int S, float* out, hipStream_t s) {
   hipLaunchKernelGGL(k_reframe_w, dim3((C * S * 2 + 255) / 256), dim3(256), 0, s, w, C, S, out);
   return (int)hipGetLastError();
 }
+
+// A stride-s Conv1d weight w [Cout][Cin][K] (padding pad) as the stride-1 conv over phase-folded frames
+// (s consecutive input rows side by side, s Cin channels): out [Cout][s Cin][K2] with
+// out[co][ph Cin + ci][k2] = w[co][ci][s (k2 - pad2) + ph + pad] (0 outside [0, K)).  MSD's stride-2 layers
+// (plan.cpp msd_forward) run folded, on the stride-1 N = 32 conv tiles.
+__global__ void k_fold_w(const float* __restrict__ w, int Cout, int Cin, int K, int st, int pad, int K2, int pad2,
+                         float* __restrict__ out) {
+  const long long n = (long long)Cout * st * Cin * K2;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int k2 = (int)(i % K2);
+  const long long r = i / K2;
+  const int cp = (int)(r % (st * Cin)), co = (int)(r / (st * Cin));
+  const int ph = cp / Cin, ci = cp - ph * Cin;
+  const int t = st * (k2 - pad2) + ph + pad;
+  out[i] = (t >= 0 && t < K) ? w[((size_t)co * Cin + ci) * K + t] : 0.f;
+}
+
+int st_fold_w(const float* w, int Cout, int Cin, int K, int st, int pad, int K2, int pad2, float* out, hipStream_t s) {
+  const long long n = (long long)Cout * st * Cin * K2;
+  hipLaunchKernelGGL(k_fold_w, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, Cout, Cin, K, st, pad, K2, pad2,
+                     out);
+  return (int)hipGetLastError();
+}

@@ -58,9 +58,28 @@ struct WConv {
   size_t bias_aux = 0;
   bool aux_bias = false;
   size_t off[2] = {0, 0};
-  int taps() const { return transposed ? (K + u - 1) / u : K; }
+  // fold > 1: a stride-`fold` conv (padding fpad0) packed as the stride-1 conv over phase-folded frames
+  // (fold consecutive input rows side by side): fold Cin channels, fK taps, padding fpad (k_fold_w)
+  int fold = 0, fpad0 = 0, fK = 0, fpad = 0;
+  int taps() const { return fold ? fK : (transposed ? (K + u - 1) / u : K); }
   int N() const { return transposed ? u * Cout : Cout; }
+  int pCin() const { return fold ? fold * Cin : Cin; }
 };
+
+// the stride-1 form of a stride-st conv (K taps, padding pad): input row st q + t - pad = st (q + s') + ph
+void set_fold(WConv& c, int st, int pad) {
+  int smin = 1 << 30, smax = -(1 << 30);
+  for (int t = 0; t < c.K; ++t) {
+    const int j = t - pad;
+    const int sq = j >= 0 ? j / st : -((-j + st - 1) / st);  // floor(j / st)
+    smin = std::min(smin, sq);
+    smax = std::max(smax, sq);
+  }
+  c.fold = st;
+  c.fpad0 = pad;
+  c.fK = smax - smin + 1;
+  c.fpad = -smin;
+}
 
 struct WAdaIN {
   int w = -1, b = -1, C = 0, hoff = 0;
@@ -430,6 +449,7 @@ int build_mpd(Model& m, const int* cfg, int n) {
 // each 4 weight-norm Conv2d (3, 9) [strides (1,1), (1,2) x 3] + Conv2d (3, 3) + out Conv2d(32, 1, 3)
 // (:38-45), cfg = {n, (n_fft, hop, win) x n}
 constexpr int kMsdCh = 32;
+int g_opt_msdfold = 1;  // STTS_OPT_MSDFOLD, read when an MSD model is created
 int build_msd(Model& m, const int* cfg, int n) {
   if (n < 4 || (n - 1) != 3 * cfg[0]) return ST_EINVAL;
   m.msd.resize(cfg[0]);
@@ -446,6 +466,10 @@ int build_msd(Model& m, const int* cfg, int n) {
     for (int j = 0; j < 5; ++j)
       add_wconv(m, d.convs[j], p + ".discriminators." + std::to_string(j), 3 * (j == 0 ? 1 : kMsdCh), kMsdCh,
                 j < 4 ? 9 : 3, true, true);
+    // the stride (1, 2) layers run folded: stride-1 convs over [W / 2][2 x 96] (N = 32 tiles fill the MFMA
+    // columns; the strided tile left 3/4 of them idle)
+    if (g_opt_msdfold)
+      for (int j = 1; j <= 3; ++j) set_fold(d.convs[j], 2, 4);
     add_wconv(m, d.out, p + ".out", 3 * kMsdCh, 1, 3, true, true);
   }
   return ST_OK;
@@ -505,7 +529,7 @@ void finalize_layout(Model& m) {
     size_t off = 0;
     for (auto* c : m.convs) {
       c->off[dt] = off;
-      off += rup(st_packed_conv_elems(c->Cin, c->Cout, c->K, c->transposed, c->u) * esz, ALIGN);
+      off += rup(st_packed_conv_elems(c->pCin(), c->Cout, c->fold ? c->fK : c->K, c->transposed, c->u) * esz, ALIGN);
     }
     m.conv_bytes[dt] = off;
   }
@@ -530,8 +554,10 @@ void finalize_layout(Model& m) {
     }
   m.aux_bytes = a;
   size_t sc = 0;
-  for (auto* c : m.convs)
+  for (auto* c : m.convs) {
     if (c->g >= 0 || c->reframe || c->rs >= 0 || c->src_rows) sc = std::max(sc, (size_t)c->Cin * c->Cout * c->K * 4);
+    if (c->fold) sc = std::max(sc, rup((size_t)c->Cin * c->Cout * c->K * 4, ALIGN) + (size_t)c->pCin() * c->Cout * c->fK * 4);
+  }
   m.scratch_bytes = rup(sc, ALIGN);
   for (int dt = 0; dt < 2; ++dt) {
     m.aux_off[dt] = m.conv_bytes[dt];
@@ -637,7 +663,7 @@ ConvParams conv_base(Ctx& c, const WConv& w, const Buf& x, int c0) {
   p.x_bs = x.bs;
   p.x_ld = x.ld;
   p.Lin = x.L;
-  p.Cin = w.Cin;
+  p.Cin = w.pCin();
   p.B = c.B;
   p.KS = w.taps();
   p.dil = 1;
@@ -645,7 +671,7 @@ ConvParams conv_base(Ctx& c, const WConv& w, const Buf& x, int c0) {
   p.pad = 0;
   p.N = w.N();
   p.w = c.wpk(w);
-  p.nchunks = (w.Cin + 31) / 32;
+  p.nchunks = (w.pCin() + 31) / 32;
   p.bias = w.aux_bias ? c.aux_f(w.bias_aux) : c.P(w.bias);
   p.Cout = w.Cout;
   p.pro = pro_none();
@@ -1283,9 +1309,15 @@ int msd_forward(Ctx& c, const float* wave, int Tn, float* out) {
     RUN(st_stft_mag_x3(wave, S, Tn, Tn, d.n_fft, d.win, d.hop, x3.p, c.dtype, c.s));
     for (int j = 0; j < 5; ++j) {
       Buf y = c.frames(g.W[j + 1], kMsdCh);
-      ConvParams q = conv_base(c, d.convs[j], x3, 0);
-      q.stride = (j >= 1 && j <= 3) ? 2 : 1;
-      q.pad = j < 4 ? 4 : 1;
+      const WConv& cw = d.convs[j];
+      Buf xin = x3;
+      if (cw.fold) {  // stride-2 layer, folded: [W_even / 2][2 x 96] rows of the same memory
+        xin.L = x3.L / cw.fold;
+        xin.ld = x3.ld * cw.fold;
+      }
+      ConvParams q = conv_base(c, cw, xin, 0);
+      q.stride = cw.fold ? 1 : ((j >= 1 && j <= 3) ? 2 : 1);
+      q.pad = cw.fold ? cw.fpad : (j < 4 ? 4 : 1);
       q.Lq = g.W[j + 1];
       conv_out(q, c, y, 0, g.W[j + 1]);
       q.epi_lrelu = 1;
@@ -1293,8 +1325,11 @@ int msd_forward(Ctx& c, const float* wave, int Tn, float* out) {
       RUN(conv_run(c, q));
       RUN(st_frames_to_f32(y.p, c.B, g.W[j + 1], kMsdCh, kMsdCh, out ? out + off : nullptr, c.dtype, c.s));
       off += (size_t)c.B * g.W[j + 1] * kMsdCh;
-      x3 = c.frames(g.W[j + 1], 3 * kMsdCh);
-      RUN(st_time_expand(y.p, S, g.H, g.W[j + 1], kMsdCh, x3.p, c.dtype, c.s));
+      // the next layer's input; a folded (stride-2) next layer reads an even number of rows per sequence
+      const int fnext = j + 1 < 5 ? d.convs[j + 1].fold : 0;
+      const int We = fnext ? (g.W[j + 1] + fnext - 1) / fnext * fnext : g.W[j + 1];
+      x3 = c.frames(We, 3 * kMsdCh);
+      RUN(st_time_expand(y.p, S, g.H, g.W[j + 1], kMsdCh, x3.p, c.dtype, c.s, We));
     }
     {  // out: Conv2d(32, 1, 3, 1, 1) straight into the fp32 output
       ConvParams q = conv_base(c, d.out, x3, 0);
@@ -1483,7 +1518,13 @@ int pack_model(Model& m, int dt, char* base, hipStream_t s) {
     if (c->aux_bias)
       ST_CHECK(st_scale_rows(m.P[c->bias], c->rs >= 0 ? m.P[c->rs] : nullptr, c->src_rows ? c->src_rows : c->Cout, 1,
                              c->Cout, reinterpret_cast<float*>(aux + c->bias_aux), s));
-    ST_CHECK(st_pack_conv(src, c->Cin, c->Cout, c->K, c->transposed, c->u, base + c->off[dt], dt, s));
+    if (c->fold) {
+      float* fo = scratch + rup((size_t)c->Cin * c->Cout * c->K * 4, ALIGN) / 4;
+      ST_CHECK(st_fold_w(src, c->Cout, c->Cin, c->K, c->fold, c->fpad0, c->fK, c->fpad, fo, s));
+      src = fo;
+    }
+    ST_CHECK(st_pack_conv(src, c->pCin(), c->Cout, c->fold ? c->fK : c->K, c->transposed, c->u, base + c->off[dt], dt,
+                          s));
   }
   // AdaIN projections: Wt[k][hoff + n] = fc.weight[n][k]; bias concat
   float* Wt = reinterpret_cast<float*>(aux + m.wt_off);
@@ -1807,6 +1848,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_UPS: g_opt_ups = value ? 1 : 0; return 0;
     case STTS_OPT_WGRAD: g_opt_wgw = value ? 1 : 0; return 0;
     case STTS_OPT_PLAINRC: g_opt_plainrc = value ? 1 : 0; return 0;
+    case STTS_OPT_MSDFOLD: g_opt_msdfold = value ? 1 : 0; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1834,6 +1876,7 @@ int stts_get_option(int key) {
     case STTS_OPT_UPS: return g_opt_ups;
     case STTS_OPT_WGRAD: return g_opt_wgw;
     case STTS_OPT_PLAINRC: return g_opt_plainrc;
+    case STTS_OPT_MSDFOLD: return g_opt_msdfold;
     default: return ST_EINVAL;
   }
 }

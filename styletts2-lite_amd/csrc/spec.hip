@@ -144,20 +144,24 @@ __global__ void __launch_bounds__(NT) k_stft_mag(const float* __restrict__ x, lo
 // bins) becomes a 1-D conv along the bins with 3 C input channels, whose weight is the reference's
 // [Cout][C][3][kw] tensor read as [Cout][3C][kw]
 template <typename T>
-__global__ void __launch_bounds__(NT) k_time_expand(const T* __restrict__ y, int H, int W, int C, T* __restrict__ x3) {
-  const long long i = (long long)blockIdx.x * NT + threadIdx.x;  // over H * W * C of utterance s
-  const long long n = (long long)H * W * C;
+__global__ void __launch_bounds__(NT) k_time_expand(const T* __restrict__ y, int H, int W, int C, T* __restrict__ x3,
+                                                    int We) {
+  // x3 rows per (signal, frame) sequence: We >= W (rows W .. We - 1 written as zeros: the even row count the
+  // phase-folded stride-2 convs of msd_forward read)
+  const long long i = (long long)blockIdx.x * NT + threadIdx.x;  // over H * We * C of utterance s
+  const long long n = (long long)H * We * C;
   if (i >= n) return;
   const int s = blockIdx.y;
   const int c = (int)(i % C);
   const long long hw = i / C;
-  const int w = (int)(hw % W), h = (int)(hw / W);
-  const T* ys = y + (size_t)s * n;
+  const int w = (int)(hw % We), h = (int)(hw / We);
+  const T* ys = y + (size_t)s * H * W * C;
   T* xs = x3 + (size_t)s * n * 3;
 #pragma unroll
   for (int dh = 0; dh < 3; ++dh) {
     const int hh = h + dh - 1;
-    xs[((size_t)h * W + w) * 3 * C + c * 3 + dh] = (hh >= 0 && hh < H) ? ys[((size_t)hh * W + w) * C + c] : from_f32<T>(0.f);
+    xs[((size_t)h * We + w) * 3 * C + c * 3 + dh] =
+        (hh >= 0 && hh < H && w < W) ? ys[((size_t)hh * W + w) * C + c] : from_f32<T>(0.f);
   }
 }
 
@@ -456,16 +460,17 @@ int st_stft_mag_x3(const float* x, int S, long long L, long long ld, int n_fft, 
   return (int)hipGetLastError();
 }
 
-int st_time_expand(const void* y, int S, int H, int W, int C, void* x3, int dtype, hipStream_t s) {
-  const long long n = (long long)H * W * C;
+int st_time_expand(const void* y, int S, int H, int W, int C, void* x3, int dtype, hipStream_t s, int We) {
+  if (We < W) We = W;
+  const long long n = (long long)H * We * C;
   if (S <= 0 || n <= 0) return ST_OK;
   dim3 grid((unsigned)((n + NT - 1) / NT), (unsigned)S);
   if (dtype == ST_FP32)
     hipLaunchKernelGGL(k_time_expand<float>, grid, dim3(NT), 0, s, reinterpret_cast<const float*>(y), H, W, C,
-                       reinterpret_cast<float*>(x3));
+                       reinterpret_cast<float*>(x3), We);
   else if (dtype == ST_BF16)
     hipLaunchKernelGGL(k_time_expand<bf16_t>, grid, dim3(NT), 0, s, reinterpret_cast<const bf16_t*>(y), H, W, C,
-                       reinterpret_cast<bf16_t*>(x3));
+                       reinterpret_cast<bf16_t*>(x3), We);
   else
     return ST_EDTYPE;
   return (int)hipGetLastError();

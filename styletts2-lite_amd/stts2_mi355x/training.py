@@ -152,10 +152,10 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
     return conv1d_frames(x.transpose(1, 2), weight, bias, stride, padding, dilation, dtype).transpose(1, 2)
 
 
-# stride-2 convs (the MSD's N = 32 layers, F0 / N convs) run as stride-1 convs over phase-folded frames (see
-# _fold_strided); False = the engines' own strided paths (tests compare the two).  Stride 3 (MPD) keeps the
-# strided path: its folded form (3 C input channels, 2 taps) measured no faster.
-FOLD_STRIDED = True
+# True: stride-2 convs run as stride-1 convs over phase-folded frames (see _fold_strided).  Off by default:
+# on the config-5 step it measured slower (103.9 vs 99.3 ms, profiles/r03_bench_train_fold_ab.txt): the
+# folded dx has 192 output channels and the per-call weight gather adds launches.  Tests compare both paths.
+FOLD_STRIDED = False
 _FOLD_MAPS = {}
 
 

@@ -201,7 +201,7 @@ STRIDED_CASES = [c for c in CASES if c[4] > 1]
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 @pytest.mark.parametrize("case", STRIDED_CASES, ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_d{}_p{}_L{}".format(*c))
 def test_folded_strided_conv_matches_engine_stride(case, dtype):
-    """Strided convs as stride-1 convs over phase-folded frames (training.FOLD_STRIDED, the default) against
+    """Strided convs as stride-1 convs over phase-folded frames (training.FOLD_STRIDED) against
     the engines' own strided path, forward and every gradient (fp32: the same sums in another order)."""
     from stts2_mi355x import training as T
     B, Cin, Cout, K, stride, dil, pad, Lin = case
@@ -219,7 +219,7 @@ def test_folded_strided_conv_matches_engine_stride(case, dtype):
             y.backward(gy)
             res.append([t.detach().double().cpu() for t in (y, xc.grad, wc.grad, bc.grad)])
     finally:
-        T.FOLD_STRIDED = True
+        T.FOLD_STRIDED = False
     tol = 1e-5 if dtype == "fp32" else 2e-2
     for name, a, r in zip(("y", "dx", "dw", "db"), res[0], res[1]):
         err = float((a - r).abs().max() / max(r.abs().max().item(), 1e-30))
