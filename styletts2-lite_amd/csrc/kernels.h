@@ -77,6 +77,8 @@ int st_conv1d_engine(const ConvParams& p, int dtype);
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.
 bool st_resconv_eligible(const ConvParams& p, int dtype);
 int st_resconv(const ConvParams& p, hipStream_t stream);
+bool st_resconv_ups_eligible(const ConvParams& p, int dtype);
+int st_resconv_ups(const ConvParams& p, hipStream_t stream);
 extern int g_opt_resconv;
 extern int g_opt_small_tiles;  // few-tile igemm launches use 64 x 128 tiles (STTS_OPT_SMALL_TILES)
 extern int g_opt_grid_cap;  // > 0: cap persistent conv grids (tests: many tiles per block)

@@ -20,7 +20,11 @@
 
 namespace {
 
-template <int C, int K, int DIL, int WAVES, int WAVES_N>
+// UPS: the HiFi-GAN ups[3] polyphase ConvTranspose1d (64 -> 32, x2; hifigan.py:292-294, 333-335) as the 2-tap
+// GEMM of DESIGN §2: C = Cin = N = u Cout = 64 columns, tap t reads input row q + t - 1 (left pad 1), Snake
+// prologue without AdaIN, and the epilogue maps row q / column n to output frame q u + n / Cout - opad,
+// channel n % Cout (residual = the noise branch at the same position; statistics per channel n % Cout).
+template <int C, int K, int DIL, int WAVES, int WAVES_N, bool UPS = false>
 struct RC {
   static constexpr int NT = 64 * WAVES;              // threads per block
   static constexpr int FW = 64;                      // frames per wave
@@ -28,7 +32,7 @@ struct RC {
   static constexpr int BM = (WAVES / WAVES_N) * FW;  // frames per tile
   static constexpr int NTL = C / 32 / WAVES_N;       // 32-channel output blocks per wave
   static constexpr int NCH = C / 32;                 // 32-channel K chunks
-  static constexpr int PAD = DIL * (K - 1) / 2;      // 'same' padding
+  static constexpr int PAD = UPS ? 1 : DIL * (K - 1) / 2;  // 'same' padding (UPS: rows q - 1, q)
   static constexpr int R = BM + DIL * (K - 1);       // window rows
   static constexpr int XP = C + 8;                   // window row pitch (bf16): conflict-free ds_read_b128
   static constexpr int WP = 40;                      // weight row pitch (bf16): 32 + 8
@@ -68,9 +72,9 @@ __device__ __forceinline__ uint4 f32_to_bf8(const float* v) {
 // STTS_OPT_EXP bit 4), instead of at the start of the tile that consumes them
 // PF: window prefetch depth in tiles (2; 3 keeps a third raw window in flight: one block per CU at
 // C = 64 holds ~40 KB of loads in flight with two, below the ~70 KB an HBM-rate stream needs)
-template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false, int PF = 2>
+template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false, int PF = 2, bool UPS = false>
 __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvParams p) {
-  using G = RC<C, K, DIL, WAVES, WAVES_N>;
+  using G = RC<C, K, DIL, WAVES, WAVES_N, UPS>;
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, NTL = G::NTL, NCH = G::NCH, XP = G::XP, WP = G::WP;
   constexpr int G8 = G::G8, UNITS = G::UNITS, MAXU = G::MAXU, FW = G::FW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -96,7 +100,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
       const unsigned off = (unsigned)((((size_t)ct * C + n) * 32 + 8 * (g ^ ((n >> 2) & 3))) * 2);
       *reinterpret_cast<uint4*>(Ws + ((size_t)ct * C + n) * WP + 8 * g) = bload16(rw, off);
     }
-    for (int i = tid; i < C; i += NT) bias_s[i] = p.bias ? p.bias[i] : 0.f;
+    for (int i = tid; i < C; i += NT) bias_s[i] = p.bias ? p.bias[UPS ? i % p.Cout : i] : 0.f;
   }
 
   const int g8 = tid % G8;  // this thread's 8-channel group in every window unit
@@ -123,8 +127,9 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     auto& racc = er_.racc;
     const int b = t / ntm, mt = t - b * ntm;
     const bool hr = p.res != nullptr;
+    const int Lrows = UPS ? p.Lout : p.Lq;
     const Rsrc rr = make_rsrc(hr ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr,
-                              hr ? (unsigned)((size_t)p.Lq * p.res_ld * 2) : 0u);
+                              hr ? (unsigned)((size_t)Lrows * p.res_ld * 2) : 0u);
     const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const bf16_t*>(p.accb) + (size_t)b * p.acc_bs : nullptr,
                               ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * 2) : 0u);
 #pragma unroll
@@ -133,7 +138,10 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
 #pragma unroll
       for (int ni = 0; ni < NTL; ++ni) {
         const int co0 = (wn * NTL + ni) * 32 + hi * 16;
-        const unsigned er = (unsigned)(q * p.res_ld + co0) * 2u;
+        // (UPS: output frame q u + phase - opad, channel co0 mod Cout; frames before 0 wrap past the range)
+        const int ph = UPS ? co0 / p.Cout : 0;
+        const int orow = UPS ? q * p.up + ph - p.opad : q, oc = UPS ? co0 - ph * p.Cout : co0;
+        const unsigned er = (unsigned)(orow * p.res_ld + oc) * 2u;
         rres[mi][ni][0] = bload16(rr, er);
         rres[mi][ni][1] = bload16(rr, er + 16u);
         if constexpr (ACC) {
@@ -167,7 +175,8 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
             q += __shfl_xor(q, o);
           }
           if (l32 == 0) {
-            double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + (wn * NTL + ni) * 32 + hi * 16 + r) * 2;
+            const int ch = (wn * NTL + ni) * 32 + hi * 16 + r;
+            double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + (UPS ? ch % p.Cout : ch)) * 2;
             atomicAdd(d, (double)a);
             atomicAdd(d + 1, (double)q);
           }
@@ -225,8 +234,8 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
           coef[2 * C + ci] = coef[3 * C + ci] = coef[4 * C + ci] = 0.f;
           continue;
         }
-        float mm, aa, be;
-        adain_coeffs(p.pro, b, ci, mm, aa, be);
+        float mm = 0.f, aa = 1.f, be = 0.f;  // UPS: Snake alone
+        if (!UPS) adain_coeffs(p.pro, b, ci, mm, aa, be);
         const float al = p.pro.alpha[ci];
         const float m1 = be - mm * aa, ia2 = 0.5f / al, alr = al * 0.31830988618379067f;  // alpha / pi
         coef[ci] = m1 + ia2;
@@ -296,10 +305,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int q = mt * BM + wm * FW + mi * 32 + l32;
-      const bool valid = q < p.Lq;
 #pragma unroll
       for (int ni = 0; ni < NTL; ++ni) {
         const int co0 = (wn * NTL + ni) * 32 + hi * 16;
+        const int ph = UPS ? co0 / p.Cout : 0;
+        const int orow = UPS ? q * p.up + ph - p.opad : q, oc = UPS ? co0 - ph * p.Cout : co0;
+        const bool valid = q < p.Lq && (!UPS || (unsigned)orow < (unsigned)p.Lout);
         float v[16], bb[16];
         ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
         ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
@@ -331,7 +342,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
             }
           }
           if (store) {
-            bf16_t* dst = yb + (size_t)q * p.y_ld + co0;
+            bf16_t* dst = yb + (size_t)orow * p.y_ld + oc;
             *reinterpret_cast<uint4*>(dst) = f32_to_bf8(&v[0]);
             *reinterpret_cast<uint4*>(dst + 8) = f32_to_bf8(&v[8]);
           }
@@ -371,12 +382,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
 
 int g_num_cu_rc = 0;
 
-template <int C, int K, int DIL, bool ACC, bool RPF = false, int PF = 2>
+template <int C, int K, int DIL, bool ACC, bool RPF = false, int PF = 2, bool UPS = false>
 int launch_rc(const ConvParams& p, hipStream_t stream) {
   constexpr int WAVES = C == 32 ? 4 : 8;
   constexpr int WAVES_N = C == 32 ? 1 : 2;
-  using G = RC<C, K, DIL, WAVES, WAVES_N>;
-  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF>;
+  using G = RC<C, K, DIL, WAVES, WAVES_N, UPS>;
+  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -455,4 +466,17 @@ int st_resconv(const ConvParams& p, hipStream_t stream) {
   if (p.Cout == 32) return launch_rc_k<32>(p, stream);
   if (p.Cout == 64) return launch_rc_k<64>(p, stream);
   return ST_EINVAL;
+}
+
+// HiFi-GAN ups[3] (64 -> 32 channels, x2) on this engine (STTS_OPT_UPS with ups[0] / ups[1] on bigconv2)
+bool st_resconv_ups_eligible(const ConvParams& p, int dtype) {
+  if (!g_opt_ups || dtype != ST_BF16 || p.up != 2 || !p.res || p.accb) return false;
+  return p.Cin == 64 && p.N == 64 && p.Cout == 32 && p.nchunks == 2 && p.KS == 2 && (p.kw == 0 || p.kw == 2) &&
+         p.dil == 1 && p.stride == 1 && p.pad == 1 && p.row_off == 0 && p.pro.mode == PRO_SNAKE && p.pro.alpha &&
+         p.res_shift == 0 && p.y_row_off == 0 && !p.reflect_front && !p.epi_tanh && !p.epi_lrelu && !p.epi_gelu &&
+         !p.y_f32 && p.zc_period == 0 && p.x_ld % 8 == 0 && p.y_ld % 8 == 0 && p.res_ld % 8 == 0;
+}
+
+int st_resconv_ups(const ConvParams& p, hipStream_t stream) {
+  return launch_rc<64, 2, 1, false, false, 2, true>(p, stream);
 }

@@ -254,9 +254,10 @@ def test_pw_engine(case):
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-3, atol=1e-1)
 
 
-UPS_CASES = [c for c in CASES if c[0] in ("ups0_u10", "ups1_u5")] + [
+UPS_CASES = [c for c in CASES if c[0] in ("ups0_u10", "ups1_u5", "ups3_u2")] + [
     ("ups0_u10_long", 512, 256, 20, 1, 10, 1, 5, 0, 700, 2),
     ("ups1_u5_long", 256, 128, 10, 1, 5, 1, 3, 1, 2500, 2),
+    ("ups3_u2_long", 64, 32, 4, 1, 2, 1, 1, 0, 9000, 2),
 ]
 
 
@@ -264,7 +265,7 @@ UPS_CASES = [c for c in CASES if c[0] in ("ups0_u10", "ups1_u5")] + [
 @pytest.mark.parametrize("case", UPS_CASES, ids=[c[0] for c in UPS_CASES])
 def test_ups_engine(case, cap):
     """bf16: the HiFi-GAN ups[0] / ups[1] polyphase upsamplers (Snake prologue, noise-branch residual) on the
-    bigconv2 engine (STTS_OPT_UPS) against torch fp32 and against the igemm engine on the same launch (same
+    bigconv2 engine and ups[3] on the resconv engine (STTS_OPT_UPS) against torch fp32 and against the igemm engine on the same launch (same
     bf16 operands); cap = 3 makes every workgroup walk many tiles across output parts and utterances."""
     try:
         E.set_option(E.OPT_UPS, 0)
