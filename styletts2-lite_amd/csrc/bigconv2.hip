@@ -163,10 +163,6 @@ __device__ __forceinline__ uint4 f32_to_bf8v(const float* v) {
   __builtin_memcpy(&r, &o, 16);
   return r;
 }
-__device__ __forceinline__ void bstore16(Rsrc r, unsigned off, const uint4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) unsigned*>(&v),
-                                         r, (int)off, 0, 0);
-}
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
           bool UPS = false, int CO = C>

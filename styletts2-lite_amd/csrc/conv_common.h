@@ -30,6 +30,16 @@ __device__ __forceinline__ uint4 bload16(Rsrc r, unsigned off) {
   return o;
 }
 
+// Branch-free store through a buffer descriptor: out-of-range offsets (OOB, or a descriptor of 0 bytes)
+// are dropped by the range check, so a tile's stores are issued unconditionally and later counted vmcnt
+// waits stay exact (a predicated `if (valid) store` makes the waitcnt pass assume the stores may be
+// missing and over-wait: every load issued before them then waits for them too)
+__device__ __forceinline__ void bstore16(Rsrc r, unsigned off, const uint4& v) {
+  __attribute__((ext_vector_type(4))) unsigned w;
+  __builtin_memcpy(&w, &v, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)off, 0, 0);
+}
+
 template <typename T> struct RawT;
 template <> struct RawT<bf16_t> { using type = uint4; };
 struct F8 { float4 a, b; };

@@ -280,4 +280,5 @@ def test_ups_engine(case, cap):
     scale = max(1.0, y0.abs().max().item())
     err = (y1 - y0).abs().max().item()
     assert err <= 2 ** -7 * scale, f"{case[0]}: ups engine vs igemm differ by {err}"
-    np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
+    # (per-channel fp32 sums over up to 1.4 M outputs, accumulated in a different order by the two engines)
+    np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-3, atol=1e-1)
