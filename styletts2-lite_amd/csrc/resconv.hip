@@ -219,6 +219,21 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     }
   };
 
+  // diagnostics (STTS_OPT_DEBUG bit 64 + a debug buffer): per-wave s_memtime sums of the step's phases
+  // 0 coefficients / residual issue, 1 barrier A, 2 transform (with its window wait), 3 window issue,
+  // 4 barrier B, 5 MFMA, 6 epilogue; 7 = total, [15] = blocks
+  const bool stamp = (p.dbg & 64) && p.stamps;
+  unsigned long long sacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long t_start = stamp ? __builtin_amdgcn_s_memtime() : 0;
+  unsigned long long t_mark = t_start;
+  auto mark = [&](int k) __attribute__((always_inline)) {
+    if (stamp) {
+      const unsigned long long tt = __builtin_amdgcn_s_memtime();
+      sacc[k] += tt - t_mark;
+      t_mark = tt;
+    }
+  };
+
   int cur_b = -1;
   auto step = [&](int t, uint4 (&pre)[MAXU], EpiRegs& er_, EpiRegs& er_next) __attribute__((always_inline)) {
     const int b = t / ntm, mt = t - b * ntm;
@@ -251,10 +266,15 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     } else {
       issue_epi(t, er_);
     }
+    mark(0);
     __syncthreads();  // (A) coef / weights visible; every wave done reading Xs of the previous tile
+    mark(1);
     transform(t, pre);
+    mark(2);
     if (t + PF < tend) issue(t + PF, pre);
+    mark(3);
     __syncthreads();  // (B) window complete
+    mark(4);
 
     f32x16 acc[MT][NTL];
 #pragma unroll
@@ -295,6 +315,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
       }
     }
 
+    mark(5);
     // ---- epilogue: lane = frame l32 of block mi, channels (wn*NTL + ni)*32 + 16*hi + r
     if (p.dbg & 4) return;
     bf16_t* yb = reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs;
@@ -356,6 +377,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
         }
       }
     }
+    mark(6);
   };
 
   uint4 preA[MAXU], preB[MAXU];
@@ -378,6 +400,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     }
   }
   if (p.stats) flush(cur_b);
+  if (stamp) {
+    sacc[7] = __builtin_amdgcn_s_memtime() - t_start;
+    if (lane == 0)
+      for (int k = 0; k < 8; ++k) atomicAdd(p.stamps + k, sacc[k]);
+    if (tid == 0) atomicAdd(p.stamps + 15, 1ull);
+  }
 }
 
 int g_num_cu_rc = 0;
