@@ -427,8 +427,18 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ dy, lo
   const int s = blockIdx.y;
   const long long r0 = R * s / S, r1 = R * (s + 1) / S;
   double acc = 0.0;
-  if (c < C)
-    for (long long r = r0 + rl; r < r1; r += 4) acc += dy[r * C + c];
+  if (c < C) {
+    // eight rows' loads in flight per thread (one load per add made the call latency-bound)
+    long long r = r0 + rl;
+    for (; r + 28 < r1; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = dy[(r + 4 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; r < r1; r += 4) acc += dy[r * C + c];
+  }
   red[rl][threadIdx.x & 63] = acc;
   __syncthreads();
   if (rl == 0 && c < C) {

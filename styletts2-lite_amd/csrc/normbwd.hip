@@ -227,25 +227,33 @@ __global__ void k_adain_bwd_dx(const float* __restrict__ x, const float* __restr
 // (4 waves with one chain each took ~40 us a call; one thread per (b, k) over all N = 2 C rows, 150 us.)
 __global__ __launch_bounds__(1024) void k_linear_bwd_ds(const float* __restrict__ W, const float* __restrict__ dh,
                                                         int B, int K, int N, float* __restrict__ ds) {
-  constexpr int NW = 16, U = 8;
+  // U = 32 loads in flight per thread (a 2,048-row W is 4 batches per wave): the call is latency-bound,
+  // two blocks per 64 k columns, so the batch count, not the bytes, sets its time
+  constexpr int NW = 16, U = 32, NA = 4;
   __shared__ double red[NW][64];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + l, b = blockIdx.y;
-  double acc[U];
+  double acc[NA];
 #pragma unroll
-  for (int u = 0; u < U; ++u) acc[u] = 0.0;
+  for (int u = 0; u < NA; ++u) acc[u] = 0.0;
   if (k < K) {
     const float* dhb = dh + (size_t)b * N;
     int n = w;
     for (; n + (U - 1) * NW < N; n += U * NW) {
+      float hv[U], wv[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc[u] += (double)dhb[n + u * NW] * W[(size_t)(n + u * NW) * K + k];
+      for (int u = 0; u < U; ++u) {
+        hv[u] = dhb[n + u * NW];
+        wv[u] = W[(size_t)(n + u * NW) * K + k];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u % NA] += (double)hv[u] * wv[u];
     }
     for (; n < N; n += NW) acc[0] += (double)dhb[n] * W[(size_t)n * K + k];
   }
   double t = 0.0;
 #pragma unroll
-  for (int u = 0; u < U; ++u) t += acc[u];
+  for (int u = 0; u < NA; ++u) t += acc[u];
   red[w][l] = t;
   __syncthreads();
   if (w == 0 && k < K) {
@@ -272,14 +280,22 @@ __global__ void k_linear_bwd_dw(const float* __restrict__ s, const float* __rest
 }
 
 // h[b][n] = bias[n] + sum_k s[b][k] W[n][k]  (nn.Linear layout; fp64 sum)
-__global__ void k_linear_fwd(const float* __restrict__ s, const float* __restrict__ W, const float* __restrict__ bias,
-                             int B, int K, int N, float* __restrict__ h) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * N) return;
-  const int b = i / N, n = i % N;
-  double acc = bias ? bias[n] : 0.0;
-  for (int k = 0; k < K; ++k) acc += (double)s[(size_t)b * K + k] * W[(size_t)n * K + k];
-  h[i] = (float)acc;
+// one wave per output row n: lanes stride over k (coalesced W row reads), fp64 lane partials reduced by
+// shuffles in a fixed order, every utterance b from the same W row
+__global__ __launch_bounds__(256) void k_linear_fwd(const float* __restrict__ s, const float* __restrict__ W,
+                                                    const float* __restrict__ bias, int B, int K, int N,
+                                                    float* __restrict__ h) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (n >= N) return;  // uniform per wave
+  const float* wr = W + (size_t)n * K;
+  for (int b = 0; b < B; ++b) {
+    const float* sb = s + (size_t)b * K;
+    double acc = 0.0;
+    for (int k = l; k < K; k += 64) acc += (double)sb[k] * wr[k];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if (l == 0) h[(size_t)b * N + n] = (float)(acc + (bias ? (double)bias[n] : 0.0));
+  }
 }
 
 // weight_norm backward per row i of v [d0][inner] (w = g v / ||v||):
@@ -501,8 +517,7 @@ extern "C" int stts_adain_act_bwd(const float* x, const float* gb, const float* 
 extern "C" int stts_linear_fwd(const float* s_in, const float* W, const float* bias, int B, int K, int N, float* h,
                                void* stream) {
   if (!s_in || !W || !h || B <= 0 || K <= 0 || N <= 0) return ST_EINVAL;
-  hipLaunchKernelGGL(k_linear_fwd, dim3((B * N + 255) / 256), dim3(256), 0, (hipStream_t)stream, s_in, W, bias, B, K,
-                     N, h);
+  hipLaunchKernelGGL(k_linear_fwd, dim3((N + 3) / 4), dim3(256), 0, (hipStream_t)stream, s_in, W, bias, B, K, N, h);
   return (int)hipGetLastError();
 }
 
