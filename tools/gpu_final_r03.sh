@@ -19,7 +19,3 @@ tail -1 gpurun_out/bench.log | cut -c1-300
 rm -rf gpurun_out/prof_bench
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o bench --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1 || exit $?
 echo "profiled bench ok"
-bash tools/gpu_configs_r02.sh > gpurun_out/configs.log 2>&1 || exit $?
-tail -2 gpurun_out/configs.log
-timeout -k 10 300 python -u tools/bench_train_step.py --dtypes bf16,fp32 --steps 5 --warmup 2 > gpurun_out/bench_train.log 2>&1 || exit $?
-cut -c1-200 gpurun_out/bench_train.log | grep config5
