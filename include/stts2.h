@@ -393,6 +393,11 @@ const char* stts_error_string(int code);
  *                     stride-1 convs over phase-folded frames (weights folded at pack time; default); 0 = the
  *                     strided conv path.  Read at stts_model_create. */
 #define STTS_OPT_MSDFOLD 17
+/*   STTS_OPT_RCPP     resconv's two-group ping-pong kernel at C = 64 (one 4-wave group computes a 128-frame tile
+ *                     while the other runs the previous tile's epilogue and the next window's transform):
+ *                     1 = for the residual / running-sum launches with K >= 7 (default, where it measured
+ *                     faster), 2 = for every C = 64 launch, 0 = never. */
+#define STTS_OPT_RCPP 18
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

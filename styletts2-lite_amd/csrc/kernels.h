@@ -77,6 +77,7 @@ int st_conv1d_engine(const ConvParams& p, int dtype);
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.
 bool st_resconv_eligible(const ConvParams& p, int dtype);
 int st_resconv(const ConvParams& p, hipStream_t stream);
+extern int g_opt_rcpp;  // STTS_OPT_RCPP
 bool st_resconv_ups_eligible(const ConvParams& p, int dtype);
 int st_resconv_ups(const ConvParams& p, hipStream_t stream);
 extern int g_opt_resconv;

@@ -1849,6 +1849,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_WGRAD: g_opt_wgw = value ? 1 : 0; return 0;
     case STTS_OPT_PLAINRC: g_opt_plainrc = value ? 1 : 0; return 0;
     case STTS_OPT_MSDFOLD: g_opt_msdfold = value ? 1 : 0; return 0;
+    case STTS_OPT_RCPP: g_opt_rcpp = (value >= 0 && value <= 2) ? value : 1; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1877,6 +1878,7 @@ int stts_get_option(int key) {
     case STTS_OPT_WGRAD: return g_opt_wgw;
     case STTS_OPT_PLAINRC: return g_opt_plainrc;
     case STTS_OPT_MSDFOLD: return g_opt_msdfold;
+    case STTS_OPT_RCPP: return g_opt_rcpp;
     default: return ST_EINVAL;
   }
 }

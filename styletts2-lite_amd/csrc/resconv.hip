@@ -437,11 +437,352 @@ int launch_rc(const ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// ---- Ping-pong variant for C = 64 (STTS_OPT_RCPP): the block's 8 waves form two groups of 4 (one
+// wave of each group per SIMD) that work on alternate 128-frame tiles half a step apart.  In every slot
+// one group runs its tile's MFMAs while the other runs the previous tile's epilogue and the next tile's
+// window transform, so the VALU / memory phases, which the lock-step kernel above runs after its MFMAs
+// (profiles/r03_resconv_stamps.txt), overlap the partner's MFMAs (MI355X_MICROARCH.md "Two waves per
+// SIMD").  Slot s of group g: compute tile j = (s - g) / 2 when s - g is even, else epilogue of tile
+// (s - 1 - g) / 2 and transform of the next; one block barrier closes each slot, so a group's window is
+// written in one slot and read in the next.  The weights are kept as packed (64-B rows, XOR-swizzled
+// 16-B units), which makes room for the two windows next to the K = 11 weights.
+template <int K, int DIL>
+struct PP {
+  static constexpr int C = 64, NT = 512, GT = 256, FW = 64, MT = 2, NCH = 2;
+  static constexpr int BM = 128;                       // frames per group tile (2 wave rows x 64)
+  static constexpr int PAD = DIL * (K - 1) / 2;
+  static constexpr int R = BM + DIL * (K - 1);         // window rows
+  static constexpr int XP = C + 8;                     // window row pitch (bf16)
+  static constexpr int G8 = C / 8;
+  static constexpr int UNITS = R * G8;
+  static constexpr int MAXU = (UNITS + GT - 1) / GT;
+  static constexpr int OFF_BIAS = 2 * 5 * C * 4;       // after coef [2 groups][5][C] f32
+  static constexpr int OFF_W = OFF_BIAS + C * 4;
+  static constexpr int W_B = NCH * K * C * 32 * 2;     // [chunk][tap][n][32] as packed
+  static constexpr int OFF_X = OFF_W + W_B;
+  static constexpr int X_B = R * XP * 2;               // one group's window
+  static constexpr int LDS = OFF_X + 2 * X_B;
+  static_assert(GT % G8 == 0 && OFF_W % 16 == 0 && OFF_X % 16 == 0 && X_B % 16 == 0, "carve");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <int K, int DIL, bool ACC>
+__global__ void __launch_bounds__(512, 1) k_resconv_pp(const ConvParams p) {
+  using G = PP<K, DIL>;
+  constexpr int C = G::C, GT = G::GT, BM = G::BM, MT = G::MT, NCH = G::NCH, XP = G::XP, FW = G::FW;
+  constexpr int G8 = G::G8, UNITS = G::UNITS, MAXU = G::MAXU;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, hi = lane >> 5;
+  const int grp = wid >> 2, gw = wid & 3, gtid = tid & (GT - 1);
+  const int wn = gw & 1, wm = gw >> 1;
+  float* coef = reinterpret_cast<float*>(smem) + grp * 5 * C;  // this group's [5][C]
+  float* bias_s = reinterpret_cast<float*>(smem + G::OFF_BIAS);
+  bf16_t* Ws = reinterpret_cast<bf16_t*>(smem + G::OFF_W);
+  bf16_t* Xs = reinterpret_cast<bf16_t*>(smem + G::OFF_X + grp * G::X_B);
+
+  const int ntm = (p.Lq + BM - 1) / BM;
+  const long long total = (long long)ntm * p.B;
+  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
+  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
+  if (tbeg >= tend) return;  // uniform over the block
+  const int n0 = (tend - tbeg + 1) / 2, n1 = (tend - tbeg) / 2;
+  const int ng = grp ? n1 : n0;  // this group's tiles: tbeg + grp + 2 j
+  auto utt = [&](int j) { return (tbeg + grp + 2 * j) / ntm; };
+
+  {  // weights (copied as packed) and bias, once per block
+    const Rsrc rw = make_rsrc(p.w, (unsigned)G::W_B);
+    for (int u = tid; u < G::W_B / 16; u += G::NT) *reinterpret_cast<uint4*>(Ws + 8 * u) = bload16(rw, 16u * u);
+    for (int i = tid; i < C; i += G::NT) bias_s[i] = p.bias ? p.bias[i] : 0.f;
+  }
+  auto set_coef = [&](int b) __attribute__((always_inline)) {
+    for (int ci = gtid; ci < C; ci += GT) {
+      if (p.pro.mode == 0) {
+        coef[ci] = 0.f;
+        coef[C + ci] = 1.f;
+        coef[2 * C + ci] = coef[3 * C + ci] = coef[4 * C + ci] = 0.f;
+        continue;
+      }
+      float mm, aa, be;
+      adain_coeffs(p.pro, b, ci, mm, aa, be);
+      const float al = p.pro.alpha[ci];
+      const float m1 = be - mm * aa, ia2 = 0.5f / al, alr = al * 0.31830988618379067f;
+      coef[ci] = m1 + ia2;
+      coef[C + ci] = aa;
+      coef[2 * C + ci] = aa * alr;
+      coef[3 * C + ci] = m1 * alr;
+      coef[4 * C + ci] = -ia2;
+    }
+  };
+
+  const int g8 = gtid % G8;
+  uint4 pre[MAXU];
+  auto issue = [&](int j) __attribute__((always_inline)) {
+    const int t = tbeg + grp + 2 * j;
+    const int b = t / ntm, mt = t - b * ntm;
+    const Rsrc rx = make_rsrc(reinterpret_cast<const bf16_t*>(p.x) + (size_t)b * p.x_bs,
+                              (unsigned)((size_t)p.Lin * p.x_ld * 2));
+    const int gr0 = mt * BM - G::PAD;
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      const int u = gtid + k * GT;
+      const int e = (gr0 + u / G8) * p.x_ld + 8 * g8;
+      const bool in = (k + 1) * GT <= UNITS || u < UNITS;
+      pre[k] = bload16(rx, in && e >= 0 ? (unsigned)e * 2u : OOB);
+    }
+  };
+  auto transform = [&](int j) __attribute__((always_inline)) {
+    const int t = tbeg + grp + 2 * j;
+    const int mt = t % ntm;
+    const int gr0 = mt * BM - G::PAD;
+    float m2[8], a[8], ar[8], mr[8], nia[8];
+    ld8_lds(coef + 8 * g8, m2);
+    ld8_lds(coef + C + 8 * g8, a);
+    ld8_lds(coef + 2 * C + 8 * g8, ar);
+    ld8_lds(coef + 3 * C + 8 * g8, mr);
+    ld8_lds(coef + 4 * C + 8 * g8, nia);
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      const int u = gtid + k * GT;
+      if ((k + 1) * GT <= UNITS || u < UNITS) {
+        const int r = u / G8;
+        float v[8];
+        bf8_to_f32(pre[k], v);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const float x2 = __builtin_fmaf(v[jj], a[jj], m2[jj]);
+          const float c = __builtin_amdgcn_cosf(__builtin_fmaf(v[jj], ar[jj], mr[jj]));
+          v[jj] = __builtin_fmaf(c, nia[jj], x2);
+        }
+        uint4 o = f32_to_bf8(v);
+        if ((unsigned)(gr0 + r) >= (unsigned)p.Lin) o = make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(Xs + r * XP + 8 * g8) = o;
+      }
+    }
+  };
+
+  // residual / running-sum rows of the tile being computed (read by its epilogue one slot later)
+  uint4 rres[MT][2], racc[ACC ? MT : 1][2];
+  auto issue_epi = [&](int j) __attribute__((always_inline)) {
+    const int t = tbeg + grp + 2 * j;
+    const int b = t / ntm, mt = t - b * ntm;
+    const bool hr = p.res != nullptr;
+    const Rsrc rr = make_rsrc(hr ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr,
+                              hr ? (unsigned)((size_t)p.Lq * p.res_ld * 2) : 0u);
+    const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const bf16_t*>(p.accb) + (size_t)b * p.acc_bs : nullptr,
+                              ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * 2) : 0u);
+    const int co0 = wn * 32 + hi * 16;
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int q = mt * BM + wm * FW + mi * 32 + l32;
+      const unsigned er = (unsigned)(q * p.res_ld + co0) * 2u;
+      rres[mi][0] = bload16(rr, er);
+      rres[mi][1] = bload16(rr, er + 16u);
+      if constexpr (ACC) {
+        const unsigned ea = (unsigned)(q * p.acc_ld + co0) * 2u;
+        racc[mi][0] = bload16(ra, ea);
+        racc[mi][1] = bload16(ra, ea + 16u);
+      }
+    }
+  };
+
+  float st_s[16], st_q[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) st_s[r] = st_q[r] = 0.f;
+  int stat_b = -1;
+  auto flush = [&](int b) __attribute__((always_inline)) {
+    if constexpr (!ACC) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float a = st_s[r], q = st_q[r];
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) {
+          a += __shfl_xor(a, o);
+          q += __shfl_xor(q, o);
+        }
+        if (l32 == 0) {
+          double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + wn * 32 + hi * 16 + r) * 2;
+          atomicAdd(d, (double)a);
+          atomicAdd(d + 1, (double)q);
+        }
+        st_s[r] = st_q[r] = 0.f;
+      }
+    }
+  };
+
+  f32x16 acc[MT];
+  // weight fragment: packed row n = wn * 32 + l32, 16-B unit g stored at g ^ ((n >> 2) & 3)
+  const int swz = (l32 >> 2) & 3;
+  const bf16_t* ww = Ws + (size_t)(wn * 32 + l32) * 32;
+  const int wo0 = 8 * (hi ^ swz), wo1 = 8 * ((2 | hi) ^ swz);
+  const bf16_t* xw = Xs + (size_t)(wm * FW + l32) * XP + hi * 8;
+  constexpr int S = K * NCH * 2;
+  auto ldfr = [&](int st, bf16x8& wa, bf16x8 (&xb)[MT]) __attribute__((always_inline)) {
+    const int tap = st / (NCH * 2), c = (st / 2) % NCH, kk = st & 1;
+    wa = *reinterpret_cast<const bf16x8*>(ww + (size_t)((c * K + tap) * C) * 32 + (kk ? wo1 : wo0));
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+      xb[mi] = *reinterpret_cast<const bf16x8*>(xw + (tap * DIL + mi * 32) * XP + c * 32 + kk * 16);
+  };
+  auto compute = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][r] = 0.f;
+    // fragments two steps ahead (one wave per SIMD computes: no partner wave covers the LDS latency)
+    // (sched_group_barrier pins the order: hipcc otherwise sinks each read to one MFMA before its use)
+    bf16x8 wa[3], xb[3][MT];
+    ldfr(0, wa[0], xb[0]);
+    ldfr(1, wa[1], xb[1]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * (1 + MT), 0);
+#pragma unroll
+    for (int st = 0; st < S; ++st) {
+      const int cb = st % 3;
+      if (st + 2 < S) {
+        ldfr(st + 2, wa[(st + 2) % 3], xb[(st + 2) % 3]);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1 + MT, 0);
+      }
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+        acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[cb], xb[cb][mi], acc[mi], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, MT, 0);
+    }
+  };
+  auto epilogue = [&](int j) __attribute__((always_inline)) {
+    const int t = tbeg + grp + 2 * j;
+    const int b = t / ntm, mt = t - b * ntm;
+    if (b != stat_b) {
+      if (stat_b >= 0 && p.stats) flush(stat_b);
+      stat_b = b;
+    }
+    bf16_t* yb = reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs;
+    const bool store = p.y != nullptr;
+    const bool hr = p.res != nullptr;
+    const float osc = p.out_scale;
+    const float adiv = (ACC && p.acc_div != 0.f) ? 1.0f / p.acc_div : 1.0f;
+    const int co0 = wn * 32 + hi * 16;
+    float bb[16];
+    ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
+    ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int q = mt * BM + wm * FW + mi * 32 + l32;
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[mi][r] + bb[r];
+      if (hr) {
+        float r0[8], r1[8];
+        bf8_to_f32(rres[mi][0], r0);
+        bf8_to_f32(rres[mi][1], r1);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          v[r] += r0[r];
+          v[8 + r] += r1[r];
+        }
+        if (osc != 1.0f) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] *= osc;
+        }
+      }
+      if (q < p.Lq) {
+        if constexpr (ACC) {
+          float r0[8], r1[8];
+          bf8_to_f32(racc[mi][0], r0);
+          bf8_to_f32(racc[mi][1], r1);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            v[r] = (r0[r] + v[r]) * adiv;
+            v[8 + r] = (r1[r] + v[8 + r]) * adiv;
+          }
+        }
+        if (store) {
+          bf16_t* dst = yb + (size_t)q * p.y_ld + co0;
+          *reinterpret_cast<uint4*>(dst) = f32_to_bf8(&v[0]);
+          *reinterpret_cast<uint4*>(dst + 8) = f32_to_bf8(&v[8]);
+        }
+        if constexpr (!ACC) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            st_s[r] += v[r];
+            st_q[r] = __builtin_fmaf(v[r], v[r], st_q[r]);
+          }
+        }
+      }
+    }
+  };
+
+  // prologue: coefficients of each group's first tile, its window loads; group 0 transforms tile 0
+  int coef_b = -1;
+  if (ng > 0) {
+    coef_b = utt(0);
+    set_coef(coef_b);
+    issue(0);
+  }
+  __syncthreads();  // weights, bias, coefficients visible
+  if (grp == 0 && ng > 0) {
+    transform(0);
+    if (1 < ng) issue(1);
+  }
+  __syncthreads();
+  const int nslots = (2 * n0 > 2 * n1 + 1) ? 2 * n0 : 2 * n1 + 1;
+  for (int s = 0; s < nslots; ++s) {
+    if (((s - grp) & 1) == 0) {  // compute slot: tile j
+      const int j = (s - grp) >> 1;
+      if (j < ng) {
+        issue_epi(j);
+        if (j + 1 < ng && utt(j + 1) != coef_b) {  // the next transform (next slot) needs its utterance
+          coef_b = utt(j + 1);
+          set_coef(coef_b);
+        }
+        compute();
+      }
+    } else {  // epilogue of tile j, transform of tile j + 1, loads of tile j + 2
+      const int j = (s - 1 - grp) >> 1;
+      if (j >= 0 && j < ng) epilogue(j);
+      if (j + 1 < ng) {
+        transform(j + 1);
+        if (j + 2 < ng) issue(j + 2);
+      }
+    }
+    __syncthreads();
+  }
+  if (p.stats && stat_b >= 0) flush(stat_b);
+}
+
+int g_num_cu_pp = 0;
+
+template <int K, int DIL, bool ACC>
+int launch_pp(const ConvParams& p, hipStream_t stream) {
+  using G = PP<K, DIL>;
+  auto kern = k_resconv_pp<K, DIL, ACC>;
+  static bool attr = false;
+  if (!attr) {
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    attr = true;
+  }
+  if (!g_num_cu_pp) {
+    int dev = 0;
+    ST_CHECK_HIP(hipGetDevice(&dev));
+    ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_pp, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
+  long long grid = g_num_cu_pp;
+  if (grid > tiles) grid = tiles;
+  if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, p);
+  return (int)hipGetLastError();
+}
+
 template <int C, int K, int DIL>
 int launch_rc_a(const ConvParams& p, hipStream_t s) {
   if constexpr (DIL == 1) {  // (the residual launches: conv2 of an iteration, dilation 1)
     if ((g_opt_exp & 4) && (p.res || p.accb))
       return p.accb ? launch_rc<C, K, 1, true, true>(p, s) : launch_rc<C, K, 1, false, true>(p, s);
+  }
+  // STTS_OPT_RCPP: the two-group ping-pong kernel at C = 64 (1: residual / running-sum launches with K >= 7,
+  // where the in-process A/B measured it faster, profiles/r03_ab_resconv_pp.txt; 2: every launch)
+  if constexpr (C == 64) {
+    if (g_opt_rcpp == 2 || (g_opt_rcpp == 1 && K >= 7 && (p.res || p.accb)))
+      return p.accb ? launch_pp<K, DIL, true>(p, s) : launch_pp<K, DIL, false>(p, s);
   }
   // STTS_OPT_EXP bit 8 / 16: window prefetch three tiles deep at C = 64 / C = 32 (register budget allows it:
   // 231-249 VGPRs, occupancy unchanged)
@@ -473,6 +814,7 @@ int launch_rc_k(const ConvParams& p, hipStream_t s) {
 }  // namespace
 
 int g_opt_plainrc = 1;
+int g_opt_rcpp = 1;
 
 bool st_resconv_eligible(const ConvParams& p, int dtype) {
   if (dtype != ST_BF16) return false;

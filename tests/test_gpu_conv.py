@@ -179,6 +179,33 @@ def test_resblock_engines_many_tiles_per_workgroup(case):
     np.testing.assert_allclose(s.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
 
 
+PP_CASES = [c for c in RB_CASES if c[1] == 64] + [
+    ("rb64_k11_d1_long", 64, 64, 11, 0, 1, 1, 5, 0, 9000, 3),
+    ("rb64_k7_d5_long_nores", 64, 64, 7, 0, 1, 5, 15, 0, 5000, 3),
+    ("rb64_k3_d3_nores", 64, 64, 3, 0, 1, 3, 3, 0, 1111, 3),
+]
+
+
+@pytest.mark.parametrize("cap", [0, 3])
+@pytest.mark.parametrize("case", PP_CASES, ids=[c[0] for c in PP_CASES])
+def test_resconv_pingpong_matches_lockstep(case, cap):
+    """bf16, C = 64: the two-group ping-pong resconv kernel (STTS_OPT_RCPP = 2) against the lock-step
+    kernel on the same launch (same MFMA order per tile, so equal outputs; statistics summed in another
+    order); cap = 3 makes each group walk many tiles across the two utterances."""
+    try:
+        E.set_option(E.OPT_GRID_CAP, cap)
+        E.set_option(E.OPT_RCPP, 0)
+        _, y0, s0 = run_case(case, "bf16")
+        E.set_option(E.OPT_RCPP, 2)
+        _, y1, s1 = run_case(case, "bf16")
+    finally:
+        E.reset_options()
+    scale = max(1.0, y0.abs().max().item())
+    err = (y1 - y0).abs().max().item()
+    assert err <= 2 ** -7 * scale, f"{case[0]}: ping-pong vs lock-step differ by {err}"
+    np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
+
+
 FRONT_CASES = [c for c in CASES if c[0].startswith("front")]
 
 
