@@ -155,6 +155,13 @@ int stts_conv1d_fwd(int dtype, const float* x, const float* w, const float* bias
 int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, const float* bias, const float* res, float scale, int B,
                         int Lin, int Cin, int Cout, int K, int stride, int dil, int pad, int Lq, float* y,
                         void* workspace, long long ws_bytes, void* stream);
+/* The same forward with leaky_relu(., slope) applied in the conv epilogue (after the bias): the
+ * discriminators' conv -> F.leaky_relu(x, 0.1) pairs (discriminators.py:59-61, 120-123) in one launch.
+ * Its gradient is dy * (y > 0 ? 1 : slope) on the output y (slope > 0 keeps the sign), then
+ * stts_conv1d_bwd.  Same workspace as stts_conv1d_fwd. */
+int stts_conv1d_fwd_act(int dtype, const float* x, const float* w, const float* bias, int B, int Lin, int Cin, int Cout,
+                        int K, int stride, int dil, int pad, int Lq, float slope, float* y, void* workspace,
+                        long long ws_bytes, void* stream);
 long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride, int dil,
                                           int pad, int Lq);
 int stts_conv1d_bwd(int dtype, const float* x, const float* w, const float* dy, int B, int Lin, int Cin, int Cout,

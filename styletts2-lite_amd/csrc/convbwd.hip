@@ -569,7 +569,8 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
 // weight [Cout][Cin][K]; wm says how the engine's weight derives from it (W_PLAIN: as is, W_FLIP:
 // channel-transposed and tap-reversed, W_TRANS: as a ConvTranspose1d weight [in][out][K]).
 int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* w, const float* bias, float* y,
-               char* ws, hipStream_t s, const float* res = nullptr, float scale = 1.f) {
+               char* ws, hipStream_t s, const float* res = nullptr, float scale = 1.f, bool lrelu = false,
+               float slope = 0.f) {
   const EngineGeo e = engine_geo(g, fwd);
   const WsLayout L = ws_layout(g, dtype, fwd);
   const int K = g.K, B = g.B;
@@ -647,6 +648,10 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   p.y_bs = (long long)e.Lout * e.co_p;
   p.y_ld = e.co_p;
   p.out_scale = scale;
+  if (lrelu) {  // leaky ReLU in the epilogue (the engines that lack it decline the launch: igemm takes it)
+    p.epi_lrelu = 1;
+    p.epi_slope = slope;
+  }
   if (res) {  // y = conv + res (fp32 frames [B][Lout][co], the same layout as y)
     if (dtype != ST_FP32 || e.co_p != e.co) return ST_EINVAL;
     p.res = res;
@@ -734,6 +739,17 @@ extern "C" int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, co
   if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
   const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
   return run_engine(dtype, g, true, x, w, bias, y, (char*)workspace, (hipStream_t)stream, res, scale);
+}
+
+extern "C" int stts_conv1d_fwd_act(int dtype, const float* x, const float* w, const float* bias, int B, int Lin,
+                                   int Cin, int Cout, int K, int stride, int dil, int pad, int Lq, float slope, float* y,
+                                   void* workspace, long long ws_bytes, void* stream) {
+  const long long need = stts_conv1d_fwd_workspace_bytes(dtype, B, Lin, Cin, Cout, K, stride, dil, pad, Lq);
+  if (need < 0) return (int)need;
+  if (!x || !w || !y) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
+  return run_engine(dtype, g, true, x, w, bias, y, (char*)workspace, (hipStream_t)stream, nullptr, 1.f, true, slope);
 }
 
 extern "C" int stts_conv1d_fwd(int dtype, const float* x, const float* w, const float* bias, int B, int Lin, int Cin,

@@ -75,6 +75,9 @@ def lib():
         getattr(L, fn).restype = c_ll
     L.stts_conv1d_fwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
     L.stts_conv1d_fwd.restype = c_int
+    L.stts_conv1d_fwd_act.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [ctypes.c_float, c_vp, c_vp, c_ll,
+                                                                                  c_vp]
+    L.stts_conv1d_fwd_act.restype = c_int
     L.stts_conv1d_fwd_res.argtypes = [c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_float] + [c_int] * 9 + [c_vp, c_vp,
                                                                                                    c_ll, c_vp]
     L.stts_pool_workspace_bytes.argtypes = [c_int, c_int, c_int]

@@ -83,8 +83,9 @@ def out_length(Lin: int, K: int, stride: int, pad: int, dil: int) -> int:
 
 class _Conv1dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, dil, dtype, res=None, scale=1.0):
-        """x: frames [B, Lin, Cin] -> y frames [B, Lq, Cout] (+ res, fp32 frames [B, Lq, Cout])"""
+    def forward(ctx, x, w, bias, stride, pad, dil, dtype, res=None, scale=1.0, act=None):
+        """x: frames [B, Lin, Cin] -> y frames [B, Lq, Cout] (+ res, fp32 frames [B, Lq, Cout]);
+        act = a leaky-ReLU slope applied in the conv epilogue (stts_conv1d_fwd_act), or None"""
         _require_device()
         B, Lin, Cin = x.shape
         Cout, Cin_w, K = w.shape
@@ -100,7 +101,14 @@ class _Conv1dFn(torch.autograd.Function):
         ws = _ws(nb, x.device)
         y = torch.empty(B, Lq, Cout, dtype=torch.float32, device=x.device)
         ctx.scale = float(scale)
-        if res is not None and dt != 0:
+        ctx.act = act
+        if act is not None:
+            if res is not None or scale != 1.0:
+                raise ValueError("conv1d_frames: the fused leaky ReLU takes no residual / scale")
+            check(lib().stts_conv1d_fwd_act(dt, _ptr(xf), _ptr(wc), _ptr(bc), B, Lin, Cin, Cout, K, stride, dil, pad,
+                                            Lq, ctypes.c_float(act), _ptr(y), _ptr(ws), int(nb), _stream()),
+                  "stts_conv1d_fwd_act")
+        elif res is not None and dt != 0:
             # the residual epilogue of stts_conv1d_fwd_res is fp32-only: bf16 runs add it in a second pass
             check(lib().stts_conv1d_fwd(dt, _ptr(xf), _ptr(wc), _ptr(bc), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
                                         _ptr(y), _ptr(ws), int(nb), _stream()), "stts_conv1d_fwd")
@@ -117,19 +125,24 @@ class _Conv1dFn(torch.autograd.Function):
         else:
             check(lib().stts_conv1d_fwd(dt, _ptr(xf), _ptr(wc), _ptr(bc), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
                                         _ptr(y), _ptr(ws), int(nb), _stream()), "stts_conv1d_fwd")
-        ctx.save_for_backward(xf, wc)
+        ctx.save_for_backward(xf, wc, y if act is not None else None)
         ctx.geo = (B, Lin, Cin, Cout, K, stride, dil, pad, Lq, dt, bias is not None)
         _count("fwd", 2.0 * B * Lq * Cout * Cin * K)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        xf, wc = ctx.saved_tensors
+        xf, wc, ya = ctx.saved_tensors
         B, Lin, Cin, Cout, K, stride, dil, pad, Lq, dt, has_bias = ctx.geo
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         if ctx.scale != 1.0:
             gy = gy * ctx.scale
         dyf = gy.detach().to(torch.float32).contiguous()
+        if ctx.act is not None:  # through the fused leaky ReLU, on its output (the slope keeps the sign)
+            dpre = torch.empty_like(dyf)
+            check(lib().stts_leaky_relu_bwd(_ptr(ya), _ptr(dyf), ya.numel(), ctypes.c_float(ctx.act), _ptr(dpre),
+                                            _stream()), "stts_leaky_relu_bwd")
+            dyf = dpre
         dev = dyf.device
         nb = lib().stts_conv1d_bwd_workspace_bytes(dt, B, Lin, Cin, Cout, K, stride, dil, pad, Lq)
         check(int(nb) if nb < 0 else 0, "stts_conv1d_bwd_workspace_bytes")
@@ -140,7 +153,7 @@ class _Conv1dFn(torch.autograd.Function):
         check(lib().stts_conv1d_bwd(dt, _ptr(xf), _ptr(wc), _ptr(dyf), B, Lin, Cin, Cout, K, stride, dil, pad, Lq,
                                     _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()), "stts_conv1d_bwd")
         _count("bwd", 2.0 * B * Lq * Cout * Cin * K * ((dx is not None) + (dw is not None)))
-        return dx, dw, db, None, None, None, None, (gy if ctx.needs_input_grad[7] else None), None
+        return dx, dw, db, None, None, None, None, (gy if ctx.needs_input_grad[7] else None), None, None
 
 
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
@@ -156,6 +169,8 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
 # on the config-5 step it measured slower (103.9 vs 99.3 ms, profiles/r03_bench_train_fold_ab.txt): the
 # folded dx has 192 output channels and the per-call weight gather adds launches.  Tests compare both paths.
 FOLD_STRIDED = False
+# the discriminators' conv -> leaky_relu(0.1) pairs as one launch (stts_conv1d_fwd_act); False = separate passes
+FUSE_LRELU = True
 _FOLD_MAPS = {}
 
 
@@ -190,10 +205,11 @@ def _fold_strided(x, weight, stride, padding):
     return x2, w2.reshape(Cout, stride * Cin, K2), pad2
 
 
-def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32", residual=None, scale=1.0):
+def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32", residual=None, scale=1.0,
+                  act_slope=None):
     """conv1d on frames tensors: x [B, Lin, Cin] -> [B, Lq, Cout] (the kernels' native layout);
     `residual` (frames [B, Lq, Cout], fp32 runs) is added and the sum multiplied by `scale` in the
-    conv epilogue."""
+    conv epilogue; `act_slope`: leaky_relu(., act_slope) applied in the epilogue instead (FUSE_LRELU)."""
     if dtype not in _DT:
         raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
     if residual is None and scale != 1.0:
@@ -202,9 +218,9 @@ def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="
     if FOLD_STRIDED and stride == 2 and dilation == 1 and residual is None:
         Lq = out_length(x.shape[1], weight.shape[-1], stride, padding, 1)
         x2, w2, pad2 = _fold_strided(x, weight, stride, padding)
-        y = _Conv1dFn.apply(x2, w2, bias, 1, pad2, 1, dtype, None, 1.0)
+        y = _Conv1dFn.apply(x2, w2, bias, 1, pad2, 1, dtype, None, 1.0, act_slope)
         return y[:, :Lq] if y.shape[1] != Lq else y
-    return _Conv1dFn.apply(x, weight, bias, stride, padding, dilation, dtype, residual, float(scale))
+    return _Conv1dFn.apply(x, weight, bias, stride, padding, dilation, dtype, residual, float(scale), act_slope)
 
 
 class Conv1d(nn.Conv1d):
@@ -967,8 +983,11 @@ def discriminator_p_forward(m, x, period, dtype="fp32"):
     for layer in m.convs:
         k, st, pad = _k1_geom(layer)
         w = _wn_w(layer)
-        h = conv1d_frames(h, w.reshape(w.shape[0], w.shape[1], k), layer.bias, st, pad, dtype=dtype)
-        h = leaky_relu(h, 0.1)
+        wk = w.reshape(w.shape[0], w.shape[1], k)
+        if FUSE_LRELU:
+            h = conv1d_frames(h, wk, layer.bias, st, pad, dtype=dtype, act_slope=0.1)
+        else:
+            h = leaky_relu(conv1d_frames(h, wk, layer.bias, st, pad, dtype=dtype), 0.1)
         fmap.append(nchw(h))
     cp = m.conv_post
     k, st, pad = _k1_geom(cp)
@@ -996,9 +1015,11 @@ def spec_discriminator_forward(m, y, dtype="fp32"):
         W3 = x3.shape[2]
         w = _wn_w(layer)
         co, ci, kh, kw = w.shape
+        act = j < len(layers) - 1
         out = conv1d_frames(x3.reshape(S * Fr, W3, 3 * ci), w.reshape(co, ci * kh, kw), layer.bias,
-                            layer.stride[1], layer.padding[1], dtype=dtype)
-        if j < len(layers) - 1:
+                            layer.stride[1], layer.padding[1], dtype=dtype,
+                            act_slope=0.1 if (act and FUSE_LRELU) else None)
+        if act and not FUSE_LRELU:
             out = leaky_relu(out, 0.1)
         h = out.reshape(S, Fr, out.shape[1], co)
         fmap.append(h.permute(0, 3, 1, 2))
