@@ -357,11 +357,15 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x
     }
 }
 
-// slices for k_wgrad_bf16w: about 1,024 workgroups, >= 2 chunks per slice
+// slices for k_wgrad_bf16w: about 256 workgroups, >= 2 chunks per slice
 int wgw_slices(int B, int Lq, int Cin, int Cout) {
   const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64);
   const long long units = (long long)B * ((Lq + WGW_CH - 1) / WGW_CH);
-  long long S = (1024 + tiles - 1) / tiles;
+  // ~256 workgroups: the fp32 partials (S x Cout x Cin x K) and their reduction scale with the slice count,
+  // and at config-5 shapes 256 measured 30-50 % faster than 1,024 on the dw call (wgrad + reduction,
+  // profiles/r03_ab_wgrad_slices.txt).  STTS_OPT_EXP bit 128 / 256 / 512: 512 / 1,024 / 128 (A/B).
+  const long long target = (g_opt_exp & 512) ? 128 : (g_opt_exp & 256) ? 1024 : (g_opt_exp & 128) ? 512 : 256;
+  long long S = (target + tiles - 1) / tiles;
   S = std::min<long long>(S, std::max<long long>(1, units / 2));
   return (int)std::max<long long>(1, std::min<long long>(S, 4096));
 }
