@@ -63,6 +63,48 @@ def test_conv1d_fwd_bwd(case, dtype):
     assert errs["dw"] < (1e-4 if dtype == "fp32" else 2e-2) and errs["db"] < 1e-5  # db: fp32 in both modes
 
 
+ACT_CASES = [c for c in CASES if c[2] >= 16] + [(4, 96, 32, 9, 2, 1, 4, 257)]  # + an MSD (3, 9) layer
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", ACT_CASES, ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_d{}_p{}_L{}".format(*c))
+def test_conv1d_fused_leaky_relu(case, dtype):
+    """conv1d_frames(..., act_slope=0.1) (stts_conv1d_fwd_act, the activation in the conv epilogue).  fp32:
+    against torch autograd (fp64) of leaky_relu(conv1d(x), 0.1).  bf16: against the unfused path on the
+    same engine (conv1d_frames, then leaky_relu): the gradient mask comes from the output's sign, which the
+    bf16 rounding keeps, so the gradients agree to fp32 rounding and the outputs to one bf16 rounding
+    (a comparison with fp64 would flip the mask wherever the bf16 conv lands on the other side of 0)."""
+    from stts2_mi355x.training import conv1d_frames, leaky_relu, out_length
+    B, Cin, Cout, K, stride, dil, pad, Lin = case
+    g = torch.Generator().manual_seed(hash(case) % 2**31 + 7)
+    x = torch.randn(B, Lin, Cin, generator=g)
+    w = torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)
+    b = torch.randn(Cout, generator=g) * 0.3
+    Lq = out_length(Lin, K, stride, pad, dil)
+    gy = torch.randn(B, Lq, Cout, generator=g)
+    if dtype == "fp32":
+        xd, wd, bd = (t.double().requires_grad_(True) for t in (x, w, b))
+        yr = torch.nn.functional.leaky_relu(
+            torch.nn.functional.conv1d(xd.transpose(1, 2), wd, bd, stride=stride, padding=pad, dilation=dil), 0.1)
+        yr = yr.transpose(1, 2)
+        yr.backward(gy.double())
+        ref = (yr, xd.grad, wd.grad, bd.grad)
+        tol = {"y": 1e-4, "dx": 1e-4, "dw": 1e-4, "db": 1e-4}
+    else:
+        xr, wr, br = (t.cuda().requires_grad_(True) for t in (x, w, b))
+        yr = leaky_relu(conv1d_frames(xr, wr, br, stride, pad, dil, dtype=dtype), 0.1)
+        yr.backward(gy.cuda())
+        ref = (yr, xr.grad, wr.grad, br.grad)
+        tol = {"y": 2 ** -7, "dx": 1e-5, "dw": 1e-5, "db": 1e-5}
+    xc, wc, bc = (t.cuda().requires_grad_(True) for t in (x, w, b))
+    y = conv1d_frames(xc, wc, bc, stride, pad, dil, dtype=dtype, act_slope=0.1)
+    y.backward(gy.cuda())
+    errs = {"y": _rel(y, ref[0]), "dx": _rel(xc.grad, ref[1]), "dw": _rel(wc.grad, ref[2]), "db": _rel(bc.grad, ref[3])}
+    print(case, dtype, {k: f"{v:.2e}" for k, v in errs.items()})
+    for k, v in errs.items():
+        assert v < tol[k], f"{k}: {v:.2e}"
+
+
 def test_conv1d_bwd_deterministic_and_partial_outputs():
     """Fixed slice order: two backward passes agree bitwise; dw-only / dx-only calls give the same
     values as the full call."""
