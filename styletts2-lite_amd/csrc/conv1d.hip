@@ -224,7 +224,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   // prefetched 8-channel units per thread (two sets in flight); the rest load synchronously.
   // Sized for a 'same' window of BM + a few rows; the strided config (iSTFTNet noise_convs)
   // has windows of ~6 BM rows.
-  constexpr int MAXU = (!C::BF || (WAVES_M == 2 && WAVES_N == 2)) ? 6 : (BM * 4 + NT - 1) / NT + 1;
+  // (4, 1, 1, 1) is the stride-2 narrow-N tile (BM 128 x BN 32, windows of ~2 BM rows): 6 units as well.
+  constexpr int MAXU = (!C::BF || (WAVES_M == 2 && WAVES_N == 2) || (WAVES_M == 4 && WAVES_N == 1 && WM == 1))
+                           ? 6
+                           : (BM * 4 + NT - 1) / NT + 1;
   const int units = R * 4;
   // every unit of a thread is the same 8-channel group: u = tid + k*NT, NT % 4 == 0
   const int g8 = tid & 3;
@@ -771,6 +774,12 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
     return launch_cfg<T, MT, 4, 1, 2, 1, true>(p, stream);
   }
   if (p.epi_tanh) return ST_EINVAL;  // tanh only on narrow heads
+  // stride 2 with N <= 32 (the MSD (3, 9) layers of the training step, N = 32): BM 128 x BN 32, every
+  // column live, instead of the 64 x 128 tile with three quarters of its columns idle (STTS_OPT_EXP 1024:
+  // the old tile, for A/B)
+  if constexpr (ConvCfg<T, MT, 1, 1, 1, 1>::BF) {
+    if (p.stride == 2 && p.N <= 32 && !(g_opt_exp & 1024)) return launch_cfg<T, MT, 4, 1, 1, 1>(p, stream);
+  }
   if (p.stride > 1) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);  // BM 64 x BN 128 (short window)
   if (p.N > 64 && g_opt_small_tiles) {
     // few tiles (small batches: the 400-frame front-end at B = 1 makes 16 tiles of 256 x 128 for 256

@@ -25,6 +25,8 @@ CASES = [
     (20, 512, 1024, 5, 3, 1, 2, 36),     # MPD period 5 conv3 at T = 4800 (dx: output padding 2)
     (20, 128, 512, 5, 3, 1, 2, 107),     # MPD period 5 conv2
     (20, 1024, 1024, 5, 1, 1, 2, 12),    # MPD period 5 conv4 (12 rows per column)
+    (6, 96, 32, 9, 2, 1, 4, 513),        # MSD (3, 9) stride-2 layer on the time-expanded image (BM 128 x BN 32)
+    (5, 96, 32, 9, 2, 1, 4, 65),         # the same, short ragged rows
 ]
 
 
