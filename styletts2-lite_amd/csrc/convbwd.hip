@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x
 }
 
 // slices for k_wgrad_bf16w: about 256 workgroups, >= 2 chunks per slice
-int wgw_slices(int B, int Lq, int Cin, int Cout) {
+int wgw_slices(int B, int Lq, int Cin, int Cout, int K) {
   const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64);
   const long long units = (long long)B * ((Lq + WGW_CH - 1) / WGW_CH);
   // ~256 workgroups: the fp32 partials (S x Cout x Cin x K) and their reduction scale with the slice count,
@@ -366,6 +366,12 @@ int wgw_slices(int B, int Lq, int Cin, int Cout) {
   // profiles/r03_ab_wgrad_slices.txt).  STTS_OPT_EXP bit 128 / 256 / 512: 512 / 1,024 / 128 (A/B).
   const long long target = (g_opt_exp & 512) ? 128 : (g_opt_exp & 256) ? 1024 : (g_opt_exp & 128) ? 512 : 256;
   long long S = (target + tiles - 1) / tiles;
+  // few-input-channel convs over many rows (the MSD first layer: Cin = 3, 1.9 M rows): one slice would walk
+  // hundreds of 64-row chunks, so aim at 16 chunks a slice while the partials stay under 32 MB
+  if (Cin <= 16 && !(g_opt_exp & 2048)) {
+    const long long per = std::max<long long>(1, (long long)Cout * Cin * K * 4);
+    S = std::max(S, std::min<long long>(units / 16, (32ll << 20) / per));
+  }
   S = std::min<long long>(S, std::max<long long>(1, units / 2));
   return (int)std::max<long long>(1, std::min<long long>(S, 4096));
 }
@@ -559,7 +565,7 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
     if (dtype == ST_BF16) {
       ns = std::max(ns, (size_t)slices_bf16(g.B, g.Lq, g.Cin, g.Cout, g.K).S);
       if (wgw_eligible(g.K, g.stride, g.dil))
-        ns = std::max(ns, (size_t)wgw_slices(g.B, g.Lq, g.Cin, g.Cout));
+        ns = std::max(ns, (size_t)wgw_slices(g.B, g.Lq, g.Cin, g.Cout, g.K));
     }
     off += al(ns * g.K * g.Cout * g.Cin * 4);
     w.part2 = off;
@@ -677,7 +683,7 @@ void launch_wgw(const Geo& g, const float* x, const float* dy, float* part, int 
 // dw as per-slice partials + the in-order reduction into dw [Cout][Cin][K]
 int wgrad_bf16(const Geo& g, const float* x, const float* dy, float* part, float* dw, hipStream_t s) {
   if (g_opt_wgw && wgw_eligible(g.K, g.stride, g.dil)) {
-    const int Sb = wgw_slices(g.B, g.Lq, g.Cin, g.Cout);
+    const int Sb = wgw_slices(g.B, g.Lq, g.Cin, g.Cout, g.K);
     if (g.stride == 2) {
       if (g.K == 3) launch_wgw<3, 2>(g, x, dy, part, Sb, s);
       else if (g.K == 4) launch_wgw<4, 2>(g, x, dy, part, Sb, s);

@@ -27,6 +27,7 @@ CASES = [
     (20, 1024, 1024, 5, 1, 1, 2, 12),    # MPD period 5 conv4 (12 rows per column)
     (6, 96, 32, 9, 2, 1, 4, 513),        # MSD (3, 9) stride-2 layer on the time-expanded image (BM 128 x BN 32)
     (5, 96, 32, 9, 2, 1, 4, 65),         # the same, short ragged rows
+    (300, 3, 32, 9, 1, 1, 4, 257),       # MSD first (3, 9) layer: Cin = 3 over many rows (many wgrad slices)
 ]
 
 

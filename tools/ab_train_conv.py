@@ -27,6 +27,8 @@ SHAPES = [  # (name, B, Cin, Cout, K, stride, dil, pad, Lin)
     ("s3_32_k3_d1", 2, 32, 32, 3, 1, 1, 1, 93000),
     ("s3_32_k11_d5", 2, 32, 32, 11, 1, 5, 25, 93000),
     ("mpd_32_128_k5_s3", 10, 32, 128, 5, 3, 1, 2, 9300),
+    ("msd1_3_32_k9", 7444, 3, 32, 9, 1, 1, 4, 257),
+    ("msd2_96_32_k9_s2", 7444, 96, 32, 9, 2, 1, 4, 257),
 ]
 
 
