@@ -366,9 +366,10 @@ int wgw_slices(int B, int Lq, int Cin, int Cout, int K) {
   // profiles/r03_ab_wgrad_slices.txt).  STTS_OPT_EXP bit 128 / 256 / 512: 512 / 1,024 / 128 (A/B).
   const long long target = (g_opt_exp & 512) ? 128 : (g_opt_exp & 256) ? 1024 : (g_opt_exp & 128) ? 512 : 256;
   long long S = (target + tiles - 1) / tiles;
-  // few-input-channel convs over many rows (the MSD first layer: Cin = 3, 1.9 M rows): one slice would walk
-  // hundreds of 64-row chunks, so aim at 16 chunks a slice while the partials stay under 32 MB
-  if (Cin <= 16 && !(g_opt_exp & 2048)) {
+  // (STTS_OPT_EXP bit 2048, off: few-input-channel convs over many rows get one slice per 16 chunks while the
+  // partials stay under 32 MB; on the MSD first layer, Cin = 3 over 1.9 M rows, it measured slower, dw 0.59 ->
+  // 0.75 ms, profiles/r03_ab_msd_conv.txt)
+  if (Cin <= 16 && (g_opt_exp & 2048)) {
     const long long per = std::max<long long>(1, (long long)Cout * Cin * K * 4);
     S = std::max(S, std::min<long long>(units / 16, (32ll << 20) / per));
   }
