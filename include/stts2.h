@@ -114,10 +114,15 @@ int stts_mpd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, floa
 /* GAN losses over stts_mpd_fwd's output for a batch of 2B = B real then B generated waveforms,
  * <- losses.py:97-128 feature_loss(fmap_r, fmap_g), generator_loss(y_d_gs)[0] and
  * discriminator_loss(y_d_rs, y_d_gs)[0] over the MultiPeriodDiscriminator outputs.  loss (device,
- * 3 doubles) = {feature, generator, discriminator}; scratch (device) >= 64 * 4 * 6 * n_periods doubles
+ * 3 doubles) = {feature, generator, discriminator}; scratch (device) >= stts_gan_losses_scratch_bytes(m)
+ * bytes = 64 * 4 * 6 * n_periods doubles
  * (per-block partial sums, added in block order: the result is bitwise reproducible). */
-int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
-                    void* stream);
+int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double* scratch,
+                    long long scratch_bytes, double* loss, void* stream);
+/* Bytes of `scratch` that stts_mpd_losses / stts_msd_losses need for model m (an MPD or MSD handle);
+ * a smaller scratch_bytes returns ST_EWORKSPACE before anything is launched (ABI 4: the size argument
+ * was added when the partials went from 4 to 64 blocks per segment). */
+long long stts_gan_losses_scratch_bytes(const stts_model* m);
 
 /* Multi-resolution mel loss, <- losses.py:55-94 MultiResolutionSTFTLoss(fft_sizes, hop_sizes, win_lengths)
  * .forward(x, y) as train.py:282 calls it (stft_loss(y_rec, wav)): per resolution r the torchaudio
@@ -232,9 +237,9 @@ long long stts_msd_out_elems(const stts_model* m, int B, int T);
 int stts_msd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, float* out, long long out_elems,
                  void* workspace, long long ws_bytes, void* stream);
 /* The GAN losses of stts_mpd_losses over stts_msd_fwd's output (losses.py:97-128 with the MSD outputs);
- * scratch >= 64 * 4 * 6 * n_resolutions doubles. */
-int stts_msd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
-                    void* stream);
+ * scratch >= stts_gan_losses_scratch_bytes(m) bytes. */
+int stts_msd_losses(const stts_model* m, int B, int T, const float* out, double* scratch,
+                    long long scratch_bytes, double* loss, void* stream);
 
 /* Style front-end, <- inference.py:43-49 Preprocess.wave_preprocess(wave) (the torchaudio
  * MelSpectrogram(n_mels=80, n_fft=2048, win_length=1200, hop_length=300) it builds, then

@@ -126,7 +126,9 @@ int stts_gan_loss_bwd(const stts_gan_term* terms, float* const* da, float* const
  *   p *= 1 - lr wd;  m = lerp(m, g, 1 - beta1);  v = v beta2 + (1 - beta2) g g;
  *   p += (-lr / (1 - beta1^step)) m / (sqrt(v) / sqrt(1 - beta2^step) + eps)
  * with `step` the tensor's step count after the increment (1 on the first call).  `tensors` is a HOST
- * array; any number of tensors (one launch per 32). */
+ * array; any number of tensors (one launch per 32).  The hyper-parameters are doubles (Python floats): the
+ * scalars 1 - lr wd, 1 - beta1, 1 - beta2, the bias corrections and lr / bc1 are formed in double and rounded
+ * to fp32 once, as torch forms them, so the update is bitwise torch's. */
 typedef struct {
   float* param;
   const float* grad;
@@ -134,8 +136,8 @@ typedef struct {
   float* exp_avg_sq;
   long long n;
 } stts_adamw_tensor;
-int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, float lr, float beta1, float beta2, float eps,
-                    float weight_decay, long long step, void* stream);
+int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, double lr, double beta1, double beta2,
+                    double eps, double weight_decay, long long step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -213,6 +213,7 @@ int st_frames_to_f32(const void* src, int B, int L, int C, int ld, float* dst, i
 // GAN losses over the MPD engine's outputs (misc.hip): per (period, layer) block, its offset, the
 // size of its real half, and whether it is a score block (conv_post)
 constexpr int kMpdMaxSegs = 64;
+constexpr int kMpdLossBlocks = 64;  // per-segment partial blocks of st_mpd_losses (scratch: 4 doubles each)
 struct MpdLossSegs {
   int n;
   long long off[kMpdMaxSegs], half[kMpdMaxSegs];

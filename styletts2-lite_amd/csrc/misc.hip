@@ -777,7 +777,6 @@ int st_period_frames(const float* wave, int B, int Tn, int p, int L0, void* dst,
 //   discriminator_loss = sum_periods mean((1 - r)^2) + mean(g^2)   (scores = the conv_post blocks)
 // Per-block sums: fp32 per thread, fp64 per workgroup, written as per-(segment, block) partials;
 // k_mpd_loss_final adds the blocks of each segment in block order (deterministic run to run).
-constexpr int kMpdLossBlocks = 64;
 
 __global__ void __launch_bounds__(256) k_mpd_loss_sums(const float* __restrict__ out, MpdLossSegs sg,
                                                        double* __restrict__ part) {

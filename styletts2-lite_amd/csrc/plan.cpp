@@ -1717,8 +1717,19 @@ int stts_mpd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, floa
   return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return mpd_forward(c, wave, T, out); }, nullptr);
 }
 
-int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
-                    void* stream) {
+// scratch of stts_mpd_losses / stts_msd_losses: kMpdLossBlocks partial blocks x 4 sums per (discriminator,
+// layer) segment (6 per period / resolution)
+long long stts_gan_losses_scratch_bytes(const stts_model* m) {
+  if (!m) return ST_EINVAL;
+  long long segs;
+  if (m->kind == STTS_KIND_MPD) segs = 6LL * (long long)m->mpd.size();
+  else if (m->kind == STTS_KIND_MSD) segs = 6LL * (long long)m->msd.size();
+  else return ST_EINVAL;
+  return segs * kMpdLossBlocks * 4 * (long long)sizeof(double);
+}
+
+int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double* scratch,
+                    long long scratch_bytes, double* loss, void* stream) {
   if (!m || m->kind != STTS_KIND_MPD || B <= 0 || T <= 0 || !out || !scratch || !loss) return ST_EINVAL;
   MpdLossSegs sg;
   memset(&sg, 0, sizeof(sg));
@@ -1736,6 +1747,7 @@ int stts_mpd_losses(const stts_model* m, int B, int T, const float* out, double*
       off += 2 * half;
     }
   }
+  if (scratch_bytes < (long long)sg.n * kMpdLossBlocks * 4 * (long long)sizeof(double)) return ST_EWORKSPACE;
   return st_mpd_losses(out, sg, scratch, loss, (hipStream_t)stream);
 }
 
@@ -1788,8 +1800,8 @@ int stts_msd_fwd(stts_model* m, int dtype, const float* wave, int B, int T, floa
   return with_ctx(m, dtype, B, ws, ws_bytes, stream, [&](Ctx& c) { return msd_forward(c, wave, T, out); }, nullptr);
 }
 
-int stts_msd_losses(const stts_model* m, int B, int T, const float* out, double* scratch, double* loss,
-                    void* stream) {
+int stts_msd_losses(const stts_model* m, int B, int T, const float* out, double* scratch,
+                    long long scratch_bytes, double* loss, void* stream) {
   if (!m || m->kind != STTS_KIND_MSD || B <= 0 || T <= 0 || !out || !scratch || !loss) return ST_EINVAL;
   MpdLossSegs sg;
   memset(&sg, 0, sizeof(sg));
@@ -1806,6 +1818,7 @@ int stts_msd_losses(const stts_model* m, int B, int T, const float* out, double*
       off += 2 * half;
     }
   }
+  if (scratch_bytes < (long long)sg.n * kMpdLossBlocks * 4 * (long long)sizeof(double)) return ST_EWORKSPACE;
   return st_mpd_losses(out, sg, scratch, loss, (hipStream_t)stream);
 }
 

@@ -742,19 +742,20 @@ extern "C" int stts_gan_loss_bwd(const stts_gan_term* terms, float* const* da, f
   return 0;
 }
 
-extern "C" int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, float lr, float beta1, float beta2,
-                               float eps, float weight_decay, long long step, void* stream) {
-  if (!tensors || n_tensors < 0 || step < 1 || !(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f))
+extern "C" int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, double lr, double beta1,
+                               double beta2, double eps, double weight_decay, long long step, void* stream) {
+  if (!tensors || n_tensors < 0 || step < 1 || !(beta1 >= 0.0 && beta1 < 1.0) || !(beta2 >= 0.0 && beta2 < 1.0))
     return ST_EINVAL;
-  // the scalars as torch's single-tensor AdamW forms them: Python floats (double), cast to fp32 by ATen
+  // the scalars as torch's single-tensor AdamW forms them: Python floats (double) combined in double, each
+  // cast to fp32 by ATen where it meets the fp32 tensor
   const double dlr = lr, dwd = weight_decay, db1 = beta1, db2 = beta2;
   AdamScalars sc;
   sc.decay = (float)(1.0 - dlr * dwd);
   sc.w1 = (float)(1.0 - db1);
-  sc.beta2 = beta2;
+  sc.beta2 = (float)beta2;
   sc.omb2 = (float)(1.0 - db2);
   sc.bc2_sqrt = (float)sqrt(1.0 - pow(db2, (double)step));
-  sc.eps = eps;
+  sc.eps = (float)eps;
   sc.neg_step = (float)(-(dlr / (1.0 - pow(db1, (double)step))));
   hipStream_t s = (hipStream_t)stream;
   for (int base = 0; base < n_tensors; base += kAdamChunk) {

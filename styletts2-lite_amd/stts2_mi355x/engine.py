@@ -62,13 +62,15 @@ def lib():
     L.stts_mpd_out_elems.restype = c_ll
     L.stts_mpd_fwd.argtypes = [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_ll, c_vp, c_ll, c_vp]
     L.stts_mpd_fwd.restype = c_int
-    L.stts_mpd_losses.argtypes = [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]
+    L.stts_mpd_losses.argtypes = [c_vp, c_int, c_int, c_vp, c_vp, c_ll, c_vp, c_vp]
     L.stts_mpd_losses.restype = c_int
     L.stts_msd_out_elems.argtypes = [c_vp, c_int, c_int]
     L.stts_msd_out_elems.restype = c_ll
     L.stts_msd_fwd.argtypes = [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_ll, c_vp, c_ll, c_vp]
     L.stts_msd_fwd.restype = c_int
-    L.stts_msd_losses.argtypes = [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]
+    L.stts_msd_losses.argtypes = [c_vp, c_int, c_int, c_vp, c_vp, c_ll, c_vp, c_vp]
+    L.stts_gan_losses_scratch_bytes.argtypes = [c_vp]
+    L.stts_gan_losses_scratch_bytes.restype = c_ll
     L.stts_msd_losses.restype = c_int
     for fn in ("stts_conv1d_fwd_workspace_bytes", "stts_conv1d_bwd_workspace_bytes"):
         getattr(L, fn).argtypes = [c_int] * 10
@@ -492,9 +494,11 @@ class MPDEngine(_Engine):
         out, B2, T = self.last
         if B2 % 2:
             raise ValueError("the last forward's batch is not real + generated halves")
-        scratch = torch.empty(64 * 4 * 6 * len(self.periods), dtype=torch.float64, device=out.device)
+        nb = int(lib().stts_gan_losses_scratch_bytes(self.model.h))
+        check(nb if nb < 0 else 0, "stts_gan_losses_scratch_bytes")
+        scratch = torch.empty(nb // 8, dtype=torch.float64, device=out.device)
         loss = torch.empty(3, dtype=torch.float64, device=out.device)
-        check(lib().stts_mpd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), _ptr(loss), _stream()),
+        check(lib().stts_mpd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), nb, _ptr(loss), _stream()),
               "stts_mpd_losses")
         return loss
 
@@ -558,9 +562,11 @@ class MSDEngine(_Engine):
         out, B2, T = self.last
         if B2 % 2:
             raise ValueError("the last forward's batch is not real + generated halves")
-        scratch = torch.empty(64 * 4 * 6 * len(self.res), dtype=torch.float64, device=out.device)
+        nb = int(lib().stts_gan_losses_scratch_bytes(self.model.h))
+        check(nb if nb < 0 else 0, "stts_gan_losses_scratch_bytes")
+        scratch = torch.empty(nb // 8, dtype=torch.float64, device=out.device)
         loss = torch.empty(3, dtype=torch.float64, device=out.device)
-        check(lib().stts_msd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), _ptr(loss), _stream()),
+        check(lib().stts_msd_losses(self.model.h, B2 // 2, T, _ptr(out), _ptr(scratch), nb, _ptr(loss), _stream()),
               "stts_msd_losses")
         return loss
 

@@ -13,6 +13,7 @@ import ctypes
 from functools import reduce
 
 import torch
+from torch.autograd.graph import increment_version
 
 from .engine import _require_device, _stream, check
 from .training import _tl
@@ -62,10 +63,14 @@ class AdamW(torch.optim.Optimizer):
                 arr = (_AdamWTensor * len(items))()
                 for i, (p, g, m, v) in enumerate(items):
                     arr[i] = _AdamWTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel())
-                check(_tl().stts_adamw_step(arr, len(items), ctypes.c_float(group["lr"]), ctypes.c_float(beta1),
-                                            ctypes.c_float(beta2), ctypes.c_float(group["eps"]),
-                                            ctypes.c_float(group["weight_decay"]), step, _stream()),
+                check(_tl().stts_adamw_step(arr, len(items), ctypes.c_double(group["lr"]), ctypes.c_double(beta1),
+                                            ctypes.c_double(beta2), ctypes.c_double(group["eps"]),
+                                            ctypes.c_double(group["weight_decay"]), step, _stream()),
                       "stts_adamw_step")
+                # the kernel writes through raw pointers: bump each parameter's version counter as torch's
+                # in-place update would, so cached packed weights (engine._Engine.stale) see the new values
+                for p, _, _, _ in items:
+                    increment_version(p)
         return loss
 
 

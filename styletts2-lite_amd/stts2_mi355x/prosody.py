@@ -346,9 +346,9 @@ class AdaLayerNorm(nn.Module):
         self.fc = nn.Linear(style_dim, channels * 2)
 
     def forward(self, x, s, lengths=None, extra=None):
+        """x [B,T,C] (any strides), s [B,style_dim] -> [B,T,C(+E)]; rows t >= lengths are zero."""
         from .engine import forward_only
         forward_only(self, "AdaLayerNorm")
-        """x [B,T,C] (any strides), s [B,style_dim] -> [B,T,C(+E)]; rows t >= lengths are zero."""
         gb = linear_frames(s.unsqueeze(0), self.fc.weight.detach(), self.fc.bias.detach())[0]
         return row_norm(x, self.channels, 1, gamma=gb, gb_sb=gb.stride(0), eps=self.eps, lengths=lengths,
                         extra=extra)

@@ -154,3 +154,17 @@ def decoder_inputs(B: int, T: int, utt0: int = 0, tag: str = "in"):
 def source_noise(B: int, L: int, utt0: int = 0, tag: str = "noise") -> np.ndarray:
     """The reference's randn_like(sine_waves) draw (hifigan.py:213) as a formula: [B, L, 9]."""
     return np.stack([normal(f"{tag}:{utt0 + b}:{L}", (L, 9)) for b in range(B)])
+
+
+def waves(B, T, seed):
+    """Speech-like test waveforms [B, 1, T] fp32: two harmonic tones with an envelope plus formula noise (the
+    discriminator / training-step fixtures' signals, tests/golden/make_golden_mpd.py)."""
+    t = np.arange(T, dtype=np.float64) / 24000.0
+    out = np.zeros((B, 1, T), np.float32)
+    for b in range(B):
+        f = 110.0 + 37.0 * (b + seed)
+        env = 0.5 + 0.4 * np.sin(2 * np.pi * 3.0 * t + b)
+        x = env * (0.6 * np.sin(2 * np.pi * f * t) + 0.25 * np.sin(2 * np.pi * 2.3 * f * t + 0.4))
+        x = x + 0.05 * normal(f"mpd.wave.{seed}.{b}", (T,)).astype(np.float64)
+        out[b, 0] = x.astype(np.float32)
+    return out

@@ -40,7 +40,8 @@ def _tl():
     L = lib()
     if _TRAIN_READY:
         return L
-    vp, i, ll, f, ull = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_ulonglong
+    vp, i, ll, f, d, ull = (ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_double,
+                           ctypes.c_ulonglong)
     sig = {
         "stts_snake_workspace_bytes": ([i, i, i], ll),
         "stts_snake_fwd": ([vp, vp, i, i, i, vp, vp], i),
@@ -64,7 +65,7 @@ def _tl():
         "stts_gan_workspace_bytes": ([i], ll),
         "stts_gan_loss": ([vp, i, vp, vp, ll, vp], i),
         "stts_gan_loss_bwd": ([vp, vp, vp, i, vp, vp, ll, vp], i),
-        "stts_adamw_step": ([vp, i, f, f, f, f, f, ll, vp], i),
+        "stts_adamw_step": ([vp, i, d, d, d, d, d, ll, vp], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -31,8 +31,7 @@ class TrainStep:
         self.decoder, self.mpd, self.msd = decoder, mpd, msd
         self.capture = capture  # keep copies of the gradients each optimizer step consumed (tests)
         self.captured = {}
-        self.dtype = dtype
-        mpd.dtype_compute = msd.dtype_compute = dtype
+        self.dtype = dtype  # the discriminators take it for the duration of each step only (__call__)
         self.gl, self.dl = GeneratorLoss(mpd, msd), DiscriminatorLoss(mpd, msd)
         self.stft_loss = MultiResolutionSTFTLoss()
         mk = lambda m, lr: AdamW(m.parameters(), lr=lr, weight_decay=1e-4, betas=(0.0, 0.99), eps=1e-9)  # noqa: E731
@@ -45,6 +44,14 @@ class TrainStep:
             o.zero_grad()
 
     def __call__(self, en, F0, N, s, wav, noise=None, seed=None):
+        saved = (self.mpd.dtype_compute, self.msd.dtype_compute)
+        self.mpd.dtype_compute = self.msd.dtype_compute = self.dtype
+        try:
+            return self._step(en, F0, N, s, wav, noise, seed)
+        finally:  # other users of the same discriminators keep their own compute dtype
+            self.mpd.dtype_compute, self.msd.dtype_compute = saved
+
+    def _step(self, en, F0, N, s, wav, noise, seed):
         y_rec = self.decoder(en, F0, N, s, noise=noise, seed=seed, dtype=self.dtype)
         self.zero_grad()
         d_loss = self.dl(wav.detach(), y_rec.detach()).mean()

@@ -43,17 +43,7 @@ def import_losses():
     return losses
 
 
-def waves(B, T, seed):
-    """Speech-like test waveforms: two harmonic tones with an envelope plus formula noise."""
-    t = np.arange(T, dtype=np.float64) / 24000.0
-    out = np.zeros((B, 1, T), np.float32)
-    for b in range(B):
-        f = 110.0 + 37.0 * (b + seed)
-        env = 0.5 + 0.4 * np.sin(2 * np.pi * 3.0 * t + b)
-        x = env * (0.6 * np.sin(2 * np.pi * f * t) + 0.25 * np.sin(2 * np.pi * 2.3 * f * t + 0.4))
-        x = x + 0.05 * synth.normal(f"mpd.wave.{seed}.{b}", (T,)).astype(np.float64)
-        out[b, 0] = x.astype(np.float32)
-    return out
+waves = synth.waves  # moved to stts2_mi355x/synth.py (GPU-side tests and tools import it from there)
 
 
 def main():

@@ -2,9 +2,6 @@
 the MPD / MSD, mel + generator loss backward + AdamW on the decoder; train.py:267-327) reproduces the
 reference modules' own autograd and torch's AdamW (tests/golden/train_step_B2_T8.npz, made by
 tests/golden/make_golden_train.py) - which makes it the checker of the HIP step (test_gpu_train_step.py)."""
-import os
-import sys
-
 import numpy as np
 import torch
 
@@ -12,11 +9,9 @@ from helpers import HIFI_CFG, fill_module, golden, make_decoder
 from oracle import stts_oracle as orc
 from stts2_mi355x import synth
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
-
 
 def test_oracle_train_step_matches_reference():
-    from make_golden_mpd import waves
+    from stts2_mi355x.synth import waves
     from stts2_mi355x.discriminators import MultiPeriodDiscriminator, MultiResSpecDiscriminator
     fx = golden("train_step_B2_T8")
     B, T = int(fx["B"]), int(fx["T"])

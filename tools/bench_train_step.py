@@ -18,8 +18,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd"), os.path.join(ROOT, "tests"),
-                os.path.join(ROOT, "tests", "golden")]
+sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd"), os.path.join(ROOT, "tests")]
 import torch  # noqa: E402
 
 PEAK = {"fp32": 157.3e12, "bf16": 2.5e15}  # MI355X dense MFMA (MI355X_MICROARCH.md)
@@ -27,7 +26,7 @@ PEAK = {"fp32": 157.3e12, "bf16": 2.5e15}  # MI355X dense MFMA (MI355X_MICROARCH
 
 def build(B, T):
     from helpers import fill_module, make_decoder
-    from make_golden_mpd import waves
+    from stts2_mi355x.synth import waves
     from stts2_mi355x import synth
     from stts2_mi355x.discriminators import MultiPeriodDiscriminator, MultiResSpecDiscriminator
     dec, _ = make_decoder("hifigan")

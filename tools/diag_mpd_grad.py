@@ -3,13 +3,12 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd"), os.path.join(ROOT, "tests"),
-                os.path.join(ROOT, "tests", "golden")]
+sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd"), os.path.join(ROOT, "tests")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from helpers import fill_module, golden  # noqa: E402
-from make_golden_mpd import waves  # noqa: E402
+from stts2_mi355x.synth import waves  # noqa: E402
 from oracle import stts_oracle as orc  # noqa: E402
 from stts2_mi355x import training as T  # noqa: E402
 from stts2_mi355x.discriminators import MultiPeriodDiscriminator  # noqa: E402
