@@ -139,6 +139,57 @@ typedef struct {
 int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, double lr, double beta1, double beta2,
                     double eps, double weight_decay, long long step, void* stream);
 
+/* ---- ProsodyPredictor.F0Ntrain under train.py's G step (train.py:265, 318, 323; models.py:448-461) */
+
+/* Training forward of ProsodyPredictor.shared (nn.LSTM(d_hid + style_dim, d_hid / 2, bidirectional, batch_first),
+ * models.py:449) on full-length sequences: stts_bilstm_fwd's output y [B][T][2H] (same params, same workspace
+ * size) plus every step's cell state c_seq [2][B][T][H] for the backward. */
+int stts_bilstm_fwd_train(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
+                          const float* const* params, int H, float* y, float* c_seq, void* workspace,
+                          long long ws_bytes, void* stream);
+/* Its backward (what autograd computes for nn.LSTM): x frames [B][T][Cin] contiguous, y and c_seq from the training
+ * forward, dy [B][T][2H] -> dx [B][T][Cin] (NULL: not computed) and grads[8] in torch's parameter order
+ * (weight_ih_l0, weight_hh_l0, bias_ih_l0, bias_hh_l0, then the _reverse four; NULL entries skipped).  Deterministic
+ * (no atomics; the bias gradients summed over utterances in order). */
+long long stts_bilstm_bwd_workspace_bytes(int B, int T, int Cin, int H);
+int stts_bilstm_bwd(const float* x, int B, int T, int Cin, const float* const* params, int H, const float* y,
+                    const float* c_seq, const float* dy, float* dx, float* const* grads, void* workspace,
+                    long long ws_bytes, void* stream);
+
+/* nn.Dropout(p) in train mode (the predictor's AdainResBlk1d dropout, models.py:335, 358-367): y = x / (1 - p) where
+ * a counter draw u(seed, i) >= p, else 0.  The backward is the same call on dy with the same seed (the mask is
+ * redrawn, not stored).  The draws are not torch's (no implementation reproduces those); the seed comes from
+ * torch's default generator in the Python layer, so torch.manual_seed governs them. */
+int stts_dropout(const float* x, long long n, float p, unsigned long long seed, float* y, void* stream);
+
+/* ---- StyleEncoder under train.py's G step (train.py:258, 324; models.py:125-150), frames images [B][H][W][C] */
+/* Row expansion for a k x k Conv2d with padding `pad` in H: xe[b][ho][w][c k + dh] = x[b][ho + dh - pad][w][c]
+ * (0 outside), Ho = H + 2 pad - k + 1; the conv then runs as conv1d over W (stts_conv1d_fwd / _bwd) with the
+ * reference weight [Cout][Cin][k][k] read as [Cout][Cin k][k].  _bwd: its adjoint (sums over dh in order). */
+int stts_rowexp_fwd(const float* x, int B, int H, int W, int C, int k, int pad, float* xe, void* stream);
+int stts_rowexp_bwd(const float* dxe, int B, int H, int W, int C, int k, int pad, float* dx, void* stream);
+/* LearnedDownSample('half') = depthwise Conv2d(C, C, 3, stride 2, pad 1, groups C) (models.py:13-28):
+ * y [B][(H-1)/2+1][(W-1)/2+1][C]; w [C][1][3][3]; bias [C] or NULL.  _bwd: dx, dw, db (each may be NULL), dw / db
+ * as fixed-order split sums (workspace >= stts_dwconv2d_s2_workspace_bytes(C)). */
+int stts_dwconv2d_s2_fwd(const float* x, const float* w, const float* bias, int B, int H, int W, int C, float* y,
+                         void* stream);
+long long stts_dwconv2d_s2_workspace_bytes(int C);
+int stts_dwconv2d_s2_bwd(const float* x, const float* w, const float* dy, int B, int H, int W, int C, float* dx,
+                         float* dw, float* db, void* ws, long long ws_bytes, void* stream);
+/* DownSample('half') (models.py:48-62): W odd -> the last column repeated, then avg_pool2d(2):
+ * y [B][H/2][(W+1)/2][C]; _bwd its adjoint. */
+int stts_avgpool2_fwd(const float* x, int B, int H, int W, int C, float* y, void* stream);
+int stts_avgpool2_bwd(const float* dy, int B, int H, int W, int C, float* dx, void* stream);
+/* AdaptiveAvgPool2d(1) (models.py:139) over the P = H W positions: y [B][C]; _bwd: dx = dy / P. */
+int stts_spatial_mean_fwd(const float* x, int B, int P, int C, float* y, void* stream);
+int stts_spatial_mean_bwd(const float* dy, int B, int P, int C, float* dx, void* stream);
+
+/* F.smooth_l1_loss(x, y) (beta 1, mean) <- train.py:269-270 (loss_F0_rec, loss_norm_rec): loss (device, 1 double)
+ * from one workgroup's fixed-order fp64 sum; _bwd: dx = g dL/dx, dy = -dx (either may be NULL), g a device float. */
+int stts_smooth_l1_loss(const float* x, const float* y, long long n, double* loss, void* stream);
+int stts_smooth_l1_loss_bwd(const float* x, const float* y, long long n, const float* g, float* dx, float* dy,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif

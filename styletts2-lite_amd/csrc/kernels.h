@@ -120,7 +120,8 @@ extern int g_opt_splitk;  // STTS_OPT_SPLITK
 int st_pw_split(const ConvParams& p, hipStream_t stream);
 extern int g_opt_pw;
 
-// fused AdaINResBlock1 iteration (resfused.hip): bf16, C = 32 (K = 3/7/11) or 64 (K = 3).
+// fused AdaINResBlock1 iteration (resfused.hip): bf16, C = 32 (K = 3/7/11) or 64 (K = 3): a statistics pass
+// (stats_only) then the fused conv1 -> AdaIN2 -> Snake2 -> conv2 -> + x pass.
 //   y = conv2(Snake2(AdaIN2(conv1(Snake1(AdaIN1(x)))))) + x     (hifigan.py:65-74)
 // pro2.stats must already hold the statistics of conv1's output (a statistics-only conv1 launch).
 // y must not alias x (neighbouring tiles read x halos).  accb != null: y = (accb + .) / acc_div
@@ -146,6 +147,7 @@ struct ResFusedParams {
   int stats_ld;
   int stats_slots;  // as ConvParams::stats_slots
   long long stats_slot_bs;
+  int stats_only;  // 1: conv1 only over the output frames, its statistics into `stats` (no y, no conv2)
   int dbg;  // phase-skipping timing bits (STTS_OPT_DEBUG, set by st_resfused): 1 prologue math, 2 MFMAs,
             // 4 residual loads + stores, 8 window loads (results are wrong when set)
 };

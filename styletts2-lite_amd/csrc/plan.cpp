@@ -744,10 +744,11 @@ int resfused_run(Ctx& c, ResFusedParams& p) {
   p.stats_slot_bs = (long long)c.B * p.stats_ld * 2;
   ST_CHECK(st_resfused(p, c.s));
   if (prof) {
-    // algorithmic work of the two convs; bytes = x once (window + residual), running sum, y
-    const double fl = 2.0 * 2.0 * p.B * (double)p.L * p.C * p.C * p.K;
-    const double by = (double)p.B * p.L * p.C * (2.0 + (p.accb ? 1.0 : 0.0)) * c.esz;
-    const int flags = 1 | (p.accb ? 2 : 0) | (ST_ENGINE_RESFUSED << 4);
+    // algorithmic work: the statistics pass = conv1 over x (x read once); the fused pass = both convs, x once
+    // (window + residual), the running sum, y
+    const double fl = (p.stats_only ? 2.0 : 4.0) * p.B * (double)p.L * p.C * p.C * p.K;
+    const double by = (double)p.B * p.L * p.C * (p.stats_only ? 1.0 : 2.0 + (p.accb ? 1.0 : 0.0)) * c.esz;
+    const int flags = (p.stats_only ? 0 : 1) | (p.accb ? 2 : 0) | (ST_ENGINE_RESFUSED << 4);
     ST_CHECK(prof_end(c, {p.B, p.L, p.C, p.C, p.K, p.dil, p.L, flags}, fl, by));
   }
   return 0;
@@ -832,23 +833,13 @@ int resblock1(Ctx& c, const ResBlock1& rb, const Buf& X, const double* st_x, Buf
   const Buf* xc = &X;
   const double* st_c = st_x;
   if (st_resfused_eligible(C, rb.K, 1, c.dtype)) {
-    // fused iterations (resfused.hip): a statistics-only conv1 launch, then one launch for
+    // fused iterations (resfused.hip): a statistics pass of conv1, then one launch for
     // conv1 -> AdaIN2 -> Snake2 -> conv2 -> +x.  Outputs ping-pong X -> R -> XT -> R (or ACC):
     // a fused launch reads its input's halos, so it cannot write in place.
     Buf* outs[3] = {&R, &XT, &R};
     for (int d = 0; d < 3; ++d) {
       if (!st_resfused_eligible(C, rb.K, rb.dil[d], c.dtype)) return ST_EINVAL;
       double* st_xt = c.stat(C);
-      ConvParams p = conv_base(c, rb.c1[d], *xc, 0);
-      p.pro = pro_adain(c, rb.a1[d], st_c, C, L, PRO_SNAKE, rb.al1[d], 0.f);
-      p.dil = rb.dil[d];
-      p.pad = rb.dil[d] * (rb.K - 1) / 2;
-      p.Lq = L;
-      conv_out(p, c, XT, 0, L);
-      p.y = nullptr;  // statistics only
-      p.stats = st_xt;
-      p.stats_ld = C;
-      RUN(conv_run(c, p));
       ResFusedParams f;
       memset(&f, 0, sizeof(f));
       f.x = xc->p;
@@ -861,7 +852,13 @@ int resblock1(Ctx& c, const ResBlock1& rb, const Buf& X, const double* st_x, Buf
       f.dil = rb.dil[d];
       f.w1 = c.wpk(rb.c1[d]);
       f.b1 = c.P(rb.c1[d].bias);
-      f.pro1 = p.pro;
+      f.pro1 = pro_adain(c, rb.a1[d], st_c, C, L, PRO_SNAKE, rb.al1[d], 0.f);
+      f.stats_only = 1;
+      f.stats = st_xt;
+      f.stats_ld = C;
+      RUN(resfused_run(c, f));
+      f.stats_only = 0;
+      f.stats = nullptr;
       f.w2 = c.wpk(rb.c2[d]);
       f.b2 = c.P(rb.c2[d].bias);
       f.pro2 = pro_adain(c, rb.a2[d], st_xt, C, L, PRO_SNAKE, rb.al2[d], 0.f);

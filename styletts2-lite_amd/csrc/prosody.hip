@@ -172,11 +172,12 @@ __device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v))
 // chunks of 4 float4 with the next chunk in flight while the current one is consumed (measured:
 // one dword per lane per load and a 4-deep loop spent ~8 us a step on L2 round trips).
 // h_{t-1} sits in LDS as [q][BG][4] so one ds_read_b128 broadcasts 4 k of one utterance.
+// cs (training, may be null): the cell state of every step, [2][B][T][H]
 template <int BG>
 __global__ void __launch_bounds__(1024) k_bilstm_rec(const float* __restrict__ G, const float4* __restrict__ WT4,
                                                      const int* __restrict__ lengths, int B, int T, int H,
                                                      float* __restrict__ y, float* __restrict__ hn,
-                                                     float* __restrict__ cn) {
+                                                     float* __restrict__ cn, float* __restrict__ cs) {
   __shared__ float4 hs4[64 * BG];
   __shared__ float gs[BG][1024];
   float* hs = reinterpret_cast<float*>(hs4);
@@ -261,6 +262,7 @@ __global__ void __launch_bounds__(1024) k_bilstm_rec(const float* __restrict__ G
         h[i] = og * tanhf(c[i]);
         hs[((j >> 2) * BG + i) * 4 + (j & 3)] = h[i];
         y[((size_t)(b0 + i) * T + t) * 2 * H + (size_t)d * H + j] = h[i];
+        if (cs) cs[(((size_t)d * B + b0 + i) * T + t) * H + j] = c[i];
       }
     }
     __syncthreads();
@@ -741,11 +743,11 @@ int stts_bilstm_fwd(const float* x, long long xs_b, long long xs_t, long long xs
   }
   const int bg = g_lstm_bg > 0 ? g_lstm_bg : 1;  // (-1 with no co-residency: 1)
   if (bg == 4)
-    hipLaunchKernelGGL(k_bilstm_rec<4>, dim3((B + 3) / 4, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n);
+    hipLaunchKernelGGL(k_bilstm_rec<4>, dim3((B + 3) / 4, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n, nullptr);
   else if (bg == 2)
-    hipLaunchKernelGGL(k_bilstm_rec<2>, dim3((B + 1) / 2, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n);
+    hipLaunchKernelGGL(k_bilstm_rec<2>, dim3((B + 1) / 2, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n, nullptr);
   else
-    hipLaunchKernelGGL(k_bilstm_rec<1>, dim3(B, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n);
+    hipLaunchKernelGGL(k_bilstm_rec<1>, dim3(B, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B, T, H, y, h_n, c_n, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -814,5 +816,223 @@ extern "C" int stts_set_bilstm_debug(int spin_limit, int drop) {
 extern "C" int stts_set_lstm_group(int bg) {
   if (bg != -1 && bg != 0 && bg != 1 && bg != 2 && bg != 4) return ST_EINVAL;
   g_lstm_bg = bg;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// BiLSTM training (ProsodyPredictor.shared under train.py's G step: models.py:449, train.py:265, 318, 323):
+// full-length sequences (every row length T, as F0Ntrain feeds it), fp32.
+//   forward: stts_bilstm_fwd's recurrence on the per-workgroup kernel, also writing every step's cell state;
+//   backward (BPTT): the pre-activations Z = x W_ih^T + b_ih + b_hh + h_prev W_hh^T are recomputed for every
+//   step at once (frames GEMMs: h_prev is the forward output shifted by one step), a sequential kernel walks
+//   each (utterance, direction) backwards through the steps producing dZ (the gate gradients), and the
+//   weight / input gradients are frames GEMMs over dZ:
+//     dW_ih = dZ^T x, dW_hh = dZ^T h_prev, db_ih = db_hh = sum_t dZ, dx = sum_d dZ_d W_ih_d.
+// ---------------------------------------------------------------------------------------
+namespace {
+
+// h_prev [B][T][2][H]: direction 0 the output of step t - 1, direction 1 that of step t + 1 (0 at the ends)
+__global__ void __launch_bounds__(256) k_lstm_hprev(const float* __restrict__ y, int B, int T, int H,
+                                                    float* __restrict__ hp) {
+  const size_t n = (size_t)B * T * 2 * H;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int j = (int)(i % H), d = (int)((i / H) & 1);
+  const size_t bt = i / (2 * H);
+  const int t = (int)(bt % T), b = (int)(bt / T);
+  const int tp = d == 0 ? t - 1 : t + 1;
+  hp[i] = (tp >= 0 && tp < T) ? y[((size_t)b * T + tp) * 2 * H + (size_t)d * H + j] : 0.f;
+}
+
+// One workgroup per (utterance, direction), 4H lanes.  Per step (the direction's forward order reversed):
+// lanes j < H turn dh = dy + W_hh^T dZ_{next} and the cell-gradient carry into the four gate gradients of
+// hidden unit j; then every lane sums a quarter of k for W_hh^T dZ (coalesced rows of W_hh, dZ broadcast from
+// LDS), reduced in fixed order.  Lane j also sums gate row j of dZ over the steps (the bias gradient, per
+// utterance; summed over utterances in order by k_lstm_db).
+__global__ void __launch_bounds__(1024) k_bilstm_bwd_rec(const float* __restrict__ G, const float* __restrict__ HW,
+                                                         const float* __restrict__ cs, const float* __restrict__ dy,
+                                                         const float* __restrict__ W0, const float* __restrict__ W1,
+                                                         int B, int T, int H, float* __restrict__ dZ,
+                                                         float* __restrict__ dbpart) {
+  __shared__ float dz[1024];
+  __shared__ float red[4][256];
+  __shared__ float dhs[256];
+  const int b = blockIdx.x, d = blockIdx.y, j = threadIdx.x, H4 = 4 * H;
+  const float* __restrict__ W = d ? W1 : W0;  // [4H][H]
+  const int part = j / H, jj = j - part * H;
+  float dc = 0.f, dbacc = 0.f;
+  if (j < H) dhs[j] = 0.f;
+  __syncthreads();
+  for (int s = 0; s < T; ++s) {
+    const int t = d == 0 ? T - 1 - s : s;
+    if (j < H) {
+      const size_t zb = (((size_t)d * B + b) * T + t) * H4;
+      const float zi = G[zb + j] + HW[zb + j], zf = G[zb + H + j] + HW[zb + H + j];
+      const float zg = G[zb + 2 * H + j] + HW[zb + 2 * H + j], zo = G[zb + 3 * H + j] + HW[zb + 3 * H + j];
+      const float ig = sigm(zi), fg = sigm(zf), gg = tanhf(zg), og = sigm(zo);
+      const size_t cb = ((size_t)d * B + b) * T;
+      const float ct = cs[(cb + t) * H + j];
+      const int tp = d == 0 ? t - 1 : t + 1;
+      const float cp = (tp >= 0 && tp < T) ? cs[(cb + tp) * H + j] : 0.f;
+      const float dh = dy[((size_t)b * T + t) * 2 * H + (size_t)d * H + j] + dhs[j];
+      const float tc = tanhf(ct);
+      const float dct = dc + dh * og * (1.f - tc * tc);
+      const float di = dct * gg * ig * (1.f - ig), df = dct * cp * fg * (1.f - fg);
+      const float dg = dct * ig * (1.f - gg * gg), dO = dh * tc * og * (1.f - og);
+      dc = dct * fg;
+      dz[j] = di;
+      dz[H + j] = df;
+      dz[2 * H + j] = dg;
+      dz[3 * H + j] = dO;
+      float* o = dZ + (((size_t)b * T + t) * 2 + d) * H4;
+      o[j] = di;
+      o[H + j] = df;
+      o[2 * H + j] = dg;
+      o[3 * H + j] = dO;
+    }
+    __syncthreads();
+    dbacc += dz[j];
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* __restrict__ wp = W + (size_t)part * H * H + jj;
+#pragma unroll 8
+    for (int k = 0; k < H; ++k) acc[k & 3] = fmaf(wp[(size_t)k * H], dz[part * H + k], acc[k & 3]);
+    red[part][jj] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (j < H) dhs[j] = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
+    __syncthreads();
+  }
+  dbpart[((size_t)b * 2 + d) * H4 + j] = dbacc;
+}
+
+// db[d][k] = sum_b dbpart[b][d][k] in utterance order, into both bias gradients of the direction
+__global__ void __launch_bounds__(256) k_lstm_db(const float* __restrict__ part, int B, int H, float* __restrict__ db_ih0,
+                                                 float* __restrict__ db_hh0, float* __restrict__ db_ih1,
+                                                 float* __restrict__ db_hh1) {
+  const int H4 = 4 * H;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * H4) return;
+  const int d = i / H4, k = i - d * H4;
+  float v = 0.f;
+  for (int b = 0; b < B; ++b) v += part[((size_t)b * 2 + d) * H4 + k];
+  float* a = d ? db_ih1 : db_ih0;
+  float* c = d ? db_hh1 : db_hh0;
+  if (a) a[k] = v;
+  if (c) c[k] = v;
+}
+
+struct LstmBwdWs {
+  float *G, *HW, *hp, *dZ, *Wcat, *dbp;
+  long long bytes;
+};
+LstmBwdWs lstm_bwd_ws(void* base, int B, int T, int Cin, int H) {
+  LstmBwdWs w;
+  const long long H4 = 4LL * H, bt = (long long)B * T;
+  long long off = 0;
+  auto take = [&](long long elems) {
+    float* p = base ? (float*)((char*)base + off) : nullptr;
+    off += (elems * 4 + 255) / 256 * 256;
+    return p;
+  };
+  w.G = take(2 * bt * H4);
+  w.HW = take(2 * bt * H4);
+  w.hp = take(bt * 2 * H);
+  w.dZ = take(bt * 2 * H4);
+  w.Wcat = take(2 * H4 * Cin);
+  w.dbp = take((long long)B * 2 * H4);
+  w.bytes = off;
+  return w;
+}
+
+}  // namespace
+
+extern "C" int stts_bilstm_fwd_train(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T,
+                                     int Cin, const float* const* params, int H, float* y, float* c_seq,
+                                     void* workspace, long long ws_bytes, void* stream) {
+  if (B < 0 || T < 0 || Cin <= 0 || !params || !y || !c_seq) return ST_EINVAL;
+  if (H <= 0 || H > 256 || (H & 31)) return ST_EINVAL;
+  for (int i = 0; i < 8; ++i)
+    if (!params[i]) return ST_EPARAMS;
+  if (ws_bytes < stts_bilstm_workspace_bytes(B, T, H)) return ST_EWORKSPACE;
+  if (B == 0 || T == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  float* G = (float*)workspace;
+  float* WT = G + (size_t)2 * B * T * 4 * H;
+  const int H4 = 4 * H;
+  {
+    const size_t n = (size_t)2 * H * H4;
+    hipLaunchKernelGGL(k_lstm_wt, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, params[1], params[5], H, WT);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  for (int d = 0; d < 2; ++d) {
+    const float* const* p = params + 4 * d;
+    GemmArgs a{x, xs_b, xs_t, xs_c, T, Cin, p[0], 0, Cin, 1, 0, H4, 1, 0, p[2], p[3],
+               G + (size_t)d * B * T * H4, (long long)T * H4, H4, 1, T, 1, 0, nullptr};
+    ST_CHECK(launch_gemm(a, B, s));
+  }
+  hipLaunchKernelGGL(k_bilstm_rec<1>, dim3(B, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), nullptr, B,
+                     T, H, y, nullptr, nullptr, c_seq);
+  return (int)hipGetLastError();
+}
+
+extern "C" long long stts_bilstm_bwd_workspace_bytes(int B, int T, int Cin, int H) {
+  if (B < 0 || T < 0 || Cin <= 0 || H <= 0) return ST_EINVAL;
+  return lstm_bwd_ws(nullptr, B, T, Cin, H).bytes;
+}
+
+extern "C" int stts_bilstm_bwd(const float* x, int B, int T, int Cin, const float* const* params, int H,
+                               const float* y, const float* c_seq, const float* dy, float* dx, float* const* grads,
+                               void* workspace, long long ws_bytes, void* stream) {
+  if (B < 0 || T < 0 || Cin <= 0 || !params || !x || !y || !c_seq || !dy || !grads) return ST_EINVAL;
+  if (H <= 0 || H > 256 || (H & 31)) return ST_EINVAL;
+  for (int i = 0; i < 8; ++i)
+    if (!params[i]) return ST_EPARAMS;
+  const LstmBwdWs w = lstm_bwd_ws(workspace, B, T, Cin, H);
+  if (!workspace || ws_bytes < w.bytes) return ST_EWORKSPACE;
+  if (B == 0 || T == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int H4 = 4 * H;
+  const long long bt = (long long)B * T;
+  // h_prev, then Z = x W_ih^T + b_ih + b_hh (G) and h_prev W_hh^T (HW) per direction
+  {
+    const size_t n = (size_t)bt * 2 * H;
+    hipLaunchKernelGGL(k_lstm_hprev, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, y, B, T, H, w.hp);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  for (int d = 0; d < 2; ++d) {
+    const float* const* p = params + 4 * d;
+    GemmArgs a{x, (long long)T * Cin, Cin, 1, T, Cin, p[0], 0, Cin, 1, 0, H4, 1, 0, p[2], p[3],
+               w.G + (size_t)d * bt * H4, (long long)T * H4, H4, 1, T, 1, 0, nullptr};
+    ST_CHECK(launch_gemm(a, B, s));
+    GemmArgs h{w.hp + (size_t)d * H, (long long)T * 2 * H, 2 * H, 1, T, H, p[1], 0, H, 1, 0, H4, 1, 0, nullptr, nullptr,
+               w.HW + (size_t)d * bt * H4, (long long)T * H4, H4, 1, T, 1, 0, nullptr};
+    ST_CHECK(launch_gemm(h, B, s));
+  }
+  hipLaunchKernelGGL(k_bilstm_bwd_rec, dim3(B, 2), dim3(H4), 0, s, w.G, w.HW, c_seq, dy, params[1], params[5], B, T,
+                     H, w.dZ, w.dbp);
+  ST_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_lstm_db, dim3((2 * H4 + 255) / 256), dim3(256), 0, s, w.dbp, B, H, grads[2], grads[3], grads[6],
+                     grads[7]);
+  ST_CHECK_HIP(hipGetLastError());
+  for (int d = 0; d < 2; ++d) {
+    const float* dzd = w.dZ + (size_t)d * H4;
+    if (grads[4 * d + 0]) {  // dW_ih [4H][Cin] = sum over the B T rows of dZ_d (x) x
+      GemmArgs a{dzd, 0, 1, 2LL * H4, H4, (int)bt, x, 0, 1, Cin, 0, Cin, 1, 0, nullptr, nullptr, grads[4 * d + 0], 0,
+                 Cin, 1, H4, 1, 0, nullptr};
+      ST_CHECK(launch_gemm(a, 1, s));
+    }
+    if (grads[4 * d + 1]) {  // dW_hh [4H][H] = sum over the rows of dZ_d (x) h_prev_d
+      GemmArgs a{dzd, 0, 1, 2LL * H4, H4, (int)bt, w.hp + (size_t)d * H, 0, 1, 2 * H, 0, H, 1, 0, nullptr, nullptr,
+                 grads[4 * d + 1], 0, H, 1, H4, 1, 0, nullptr};
+      ST_CHECK(launch_gemm(a, 1, s));
+    }
+  }
+  if (dx) {  // dx = [dZ_0 | dZ_1] [W_ih_0; W_ih_1]
+    ST_CHECK_HIP(hipMemcpyAsync(w.Wcat, params[0], sizeof(float) * H4 * Cin, hipMemcpyDeviceToDevice, s));
+    ST_CHECK_HIP(hipMemcpyAsync(w.Wcat + (size_t)H4 * Cin, params[4], sizeof(float) * H4 * Cin,
+                                hipMemcpyDeviceToDevice, s));
+    GemmArgs a{w.dZ, (long long)T * 2 * H4, 2 * H4, 1, T, 2 * H4, w.Wcat, 0, 1, Cin, 0, Cin, 1, 0, nullptr, nullptr,
+               dx, (long long)T * Cin, Cin, 1, T, 1, 0, nullptr};
+    ST_CHECK(launch_gemm(a, B, s));
+  }
   return 0;
 }

@@ -536,6 +536,58 @@ __global__ __launch_bounds__(256) void k_adamw(AdamTable tb, AdamScalars s) {
   }
 }
 
+// ------------------------------------------------------------------ Dropout (train mode)
+// keep element i when its counter draw u(seed, i) >= p; y = keep ? x / (1 - p) : 0 (torch's scaling).  The
+// backward redraws the same mask from (seed, i): nothing is stored.
+__device__ __forceinline__ bool drop_keep(unsigned long long seed, long long i, float p) {
+  const unsigned long long z = splitmix64(seed ^ splitmix64((unsigned long long)i * 0xD1B54A32D192ED03ULL));
+  return (float)(z >> 40) * (1.0f / 16777216.0f) >= p;
+}
+
+__global__ void __launch_bounds__(256) k_dropout(const float* __restrict__ x, long long n, float p, float scale,
+                                                 unsigned long long seed, float* __restrict__ y) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
+    y[i] = drop_keep(seed, i, p) ? x[i] * scale : 0.f;
+}
+
+}  // namespace
+
+namespace {
+// ------------------------------------------------------------------ smooth L1 (train.py:269-270)
+// F.smooth_l1_loss(x, y) (beta 1, mean): one workgroup, fp64 per-lane sums reduced in a fixed tree order
+__global__ void __launch_bounds__(256) k_smooth_l1(const float* __restrict__ x, const float* __restrict__ y,
+                                                   long long n, double* __restrict__ loss) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (long long i = threadIdx.x; i < n; i += 256) {
+    const float d = x[i] - y[i], ad = fabsf(d);
+    acc += ad < 1.f ? 0.5 * (double)d * (double)d : (double)ad - 0.5;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = n ? red[0] / (double)n : 0.0;
+}
+
+// d/dx = g d / n (|d| < 1) or g sign(d) / n, d = x - y; dy = -dx.  g: the upstream gradient (a device scalar)
+__global__ void __launch_bounds__(256) k_smooth_l1_bwd(const float* __restrict__ x, const float* __restrict__ y,
+                                                       long long n, const float* __restrict__ g,
+                                                       float* __restrict__ dx, float* __restrict__ dy) {
+  const float s = g[0] / (float)n;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const float d = x[i] - y[i];
+    const float v = (fabsf(d) < 1.f ? d : (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f))) * s;
+    if (dx) dx[i] = v;
+    if (dy) dy[i] = -v;
+  }
+}
+
+}  // namespace
+
+namespace {
 }  // namespace
 
 // ================================================================== C-ABI
@@ -782,4 +834,29 @@ extern "C" int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, 
     ST_CHECK_HIP(hipGetLastError());
   }
   return 0;
+}
+
+extern "C" int stts_dropout(const float* x, long long n, float p, unsigned long long seed, float* y, void* stream) {
+  if (!x || !y || n < 0 || !(p >= 0.f && p < 1.f)) return ST_EINVAL;
+  if (n == 0) return 0;
+  const long long g = (n + NT - 1) / NT;
+  hipLaunchKernelGGL(k_dropout, dim3((unsigned)(g < 65536 ? g : 65536)), dim3(NT), 0, (hipStream_t)stream, x, n, p,
+                     1.0f / (1.0f - p), seed, y);
+  return (int)hipGetLastError();
+}
+
+extern "C" int stts_smooth_l1_loss(const float* x, const float* y, long long n, double* loss, void* stream) {
+  if (!x || !y || !loss || n < 0) return ST_EINVAL;
+  hipLaunchKernelGGL(k_smooth_l1, dim3(1), dim3(256), 0, (hipStream_t)stream, x, y, n, loss);
+  return (int)hipGetLastError();
+}
+
+extern "C" int stts_smooth_l1_loss_bwd(const float* x, const float* y, long long n, const float* g, float* dx,
+                                       float* dy, void* stream) {
+  if (!x || !y || !g || n < 0) return ST_EINVAL;
+  if (n == 0) return 0;
+  const long long gr = (n + NT - 1) / NT;
+  hipLaunchKernelGGL(k_smooth_l1_bwd, dim3((unsigned)(gr < 4096 ? gr : 4096)), dim3(NT), 0, (hipStream_t)stream, x, y,
+                     n, g, dx, dy);
+  return (int)hipGetLastError();
 }

@@ -229,3 +229,35 @@ class MultiResolutionSTFTLoss(nn.Module):
         x2 = x.reshape(-1, L).to(dev)
         y2 = y.reshape(-1, L).to(dev)
         return _MrstftFn.apply(x2, y2, self)
+
+
+class _SmoothL1Fn(torch.autograd.Function):
+    """F.smooth_l1_loss(x, y) (beta 1, mean): stts_smooth_l1_loss / _bwd."""
+
+    @staticmethod
+    def forward(ctx, x, y):
+        _require_device()
+        xc, yc = _f32(x), _f32(y)
+        if xc.shape != yc.shape:
+            raise ValueError(f"smooth_l1_loss: {tuple(xc.shape)} vs {tuple(yc.shape)}")
+        loss = torch.empty(1, dtype=torch.float64, device=xc.device)
+        check(_tl().stts_smooth_l1_loss(_ptr(xc), _ptr(yc), xc.numel(), _ptr(loss), _stream()), "stts_smooth_l1_loss")
+        ctx.save_for_backward(xc, yc)
+        return loss[0].to(torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, yc = ctx.saved_tensors
+        nx, ny = ctx.needs_input_grad
+        gd = _f32(g.reshape(1))
+        dx = torch.empty_like(xc) if nx else None
+        dy = torch.empty_like(yc) if ny else None
+        check(_tl().stts_smooth_l1_loss_bwd(_ptr(xc), _ptr(yc), xc.numel(), _ptr(gd), _ptr(dx), _ptr(dy), _stream()),
+              "stts_smooth_l1_loss_bwd")
+        return dx, dy
+
+
+def smooth_l1_loss(x, y):
+    """F.smooth_l1_loss(x, y) as train.py:269-270 calls it (loss_F0_rec = smooth_l1(F0_real, F0_fake) / 10,
+    loss_norm_rec = smooth_l1(N_real, N_fake))."""
+    return _SmoothL1Fn.apply(x, y)

@@ -10,6 +10,8 @@ load unchanged (reference inference.py:120-122, 158-168).
 * `ProsodyPredictor.forward(texts, style, text_lengths, alignment, m)` (models.py:417-446) and
   `TextEncoder` (models.py:241-295): the duration path, prosody.py.
 * `StyleEncoder.forward(mel)` (models.py:145-150): the whole 2-D ResNet runs as HIP kernels.
+* Under autograd (train.py's G step differentiates both, train.py:258, 265, 318, 323-324) F0Ntrain and the
+  StyleEncoder take the trainable HIP paths of training.py (f0ntrain, style_encoder) with their backward.
 """
 from __future__ import annotations
 
@@ -79,10 +81,17 @@ class ProsodyPredictor(nn.Module):
         return duration.squeeze(-1), en
 
     def F0Ntrain(self, x, s, dtype="fp32"):
-        """x = en [B, d_hid+style_dim, T], s [B, style_dim] -> (F0 [B,2T], N [B,2T])."""
-        from .engine import forward_only
-        forward_only(self, "ProsodyPredictor.F0Ntrain")
+        """x = en [B, d_hid+style_dim, T], s [B, style_dim] -> (F0 [B,2T], N [B,2T]).
+
+        Under autograd (grad mode on and a parameter or an input requiring grad, as train.py:265 calls it) the
+        trainable path runs: training.f0ntrain (HIP BiLSTM forward / backward, the AdainResBlk1d stacks with their
+        train-mode dropout, the projections); otherwise the fused inference engine."""
         dev = self.F0_proj.weight.device
+        if torch.is_grad_enabled() and (any(p.requires_grad for p in self.parameters())
+                                        or (isinstance(x, torch.Tensor) and x.requires_grad)
+                                        or (isinstance(s, torch.Tensor) and s.requires_grad)):
+            from .training import f0ntrain
+            return f0ntrain(self, x.to(dev, torch.float32), s.to(dev, torch.float32), dtype)
         in_dev = x.device
         with torch.no_grad():
             h, _ = self.shared(x.to(dev, torch.float32).transpose(-1, -2))  # [B, T, d_hid] frames, HIP BiLSTM
@@ -142,7 +151,12 @@ class StyleEncoder(nn.Module):
         return self._engine
 
     def forward(self, x, dtype="fp32"):
-        """mel [B,1,80,F] -> style [B, style_dim]."""
-        from .engine import forward_only
-        forward_only(self, "StyleEncoder")
+        """mel [B,1,80,F] -> style [B, style_dim].  Under autograd (train.py:258, 324) the trainable path
+        (training.style_encoder: the 2-D convs as row expansions + the conv1d engine, with backward); otherwise the
+        fused inference engine."""
+        if torch.is_grad_enabled() and (any(p.requires_grad for p in self.parameters())
+                                        or (isinstance(x, torch.Tensor) and x.requires_grad)):
+            from .training import style_encoder
+            dev = self.unshared.weight.device
+            return style_encoder(self, x.to(dev, torch.float32), dtype)
         return self.engine(dtype).forward(x)

@@ -66,6 +66,22 @@ def _tl():
         "stts_gan_loss": ([vp, i, vp, vp, ll, vp], i),
         "stts_gan_loss_bwd": ([vp, vp, vp, i, vp, vp, ll, vp], i),
         "stts_adamw_step": ([vp, i, d, d, d, d, d, ll, vp], i),
+        "stts_bilstm_workspace_bytes": ([i, i, i], ll),
+        "stts_bilstm_fwd_train": ([vp, ll, ll, ll, i, i, i, vp, i, vp, vp, vp, ll, vp], i),
+        "stts_bilstm_bwd_workspace_bytes": ([i, i, i, i], ll),
+        "stts_bilstm_bwd": ([vp, i, i, i, vp, i, vp, vp, vp, vp, vp, vp, ll, vp], i),
+        "stts_dropout": ([vp, ll, f, ull, vp, vp], i),
+        "stts_rowexp_fwd": ([vp, i, i, i, i, i, i, vp, vp], i),
+        "stts_rowexp_bwd": ([vp, i, i, i, i, i, i, vp, vp], i),
+        "stts_dwconv2d_s2_fwd": ([vp, vp, vp, i, i, i, i, vp, vp], i),
+        "stts_dwconv2d_s2_workspace_bytes": ([i], ll),
+        "stts_dwconv2d_s2_bwd": ([vp, vp, vp, i, i, i, i, vp, vp, vp, vp, ll, vp], i),
+        "stts_avgpool2_fwd": ([vp, i, i, i, i, vp, vp], i),
+        "stts_avgpool2_bwd": ([vp, i, i, i, i, vp, vp], i),
+        "stts_spatial_mean_fwd": ([vp, i, i, i, vp, vp], i),
+        "stts_spatial_mean_bwd": ([vp, i, i, i, vp, vp], i),
+        "stts_smooth_l1_loss": ([vp, vp, ll, vp, vp], i),
+        "stts_smooth_l1_loss_bwd": ([vp, vp, ll, vp, vp, vp, vp], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -559,12 +575,14 @@ def adain_resblk1d_frames(m, x, s, dtype="fp32"):
     out = (conv2(LReLU(AdaIN2(conv1(pool(LReLU(AdaIN1(x))))))) + conv1x1(up2(x))) / sqrt(2), the sum and the
     scale in conv2's epilogue."""
     up = m.upsample if isinstance(getattr(m, "upsample", None), bool) else m.upsample_type != "none"
+    # nn.Dropout(dropout_p) before each conv in train mode (models.py:335, 358-367; the predictor's blocks)
+    p_drop = float(getattr(m, "dropout_p", 0.0) or 0.0) if m.training else 0.0
     r = adain_act(x, s, m.norm1.fc.weight, m.norm1.fc.bias, None, ACT_LRELU)
     if up:
         r = _PoolFn.apply(r, weight_norm(m.pool.weight_g, m.pool.weight_v), m.pool.bias)
     c1, c2 = m.conv1, m.conv2
-    r = conv1d_frames(r, weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, 1, dtype=dtype)
-    r = adain_act(r, s, m.norm2.fc.weight, m.norm2.fc.bias, None, ACT_LRELU)
+    r = conv1d_frames(dropout(r, p_drop), weight_norm(c1.weight_g, c1.weight_v), c1.bias, 1, 1, dtype=dtype)
+    r = dropout(adain_act(r, s, m.norm2.fc.weight, m.norm2.fc.bias, None, ACT_LRELU), p_drop)
     sc = _Up2Fn.apply(x) if up else x
     if m.learned_sc:
         sc = conv1d_frames(sc, weight_norm(m.conv1x1.weight_g, m.conv1x1.weight_v), None, 1, 0, dtype=dtype)
@@ -1025,3 +1043,237 @@ def spec_discriminator_forward(m, y, dtype="fp32"):
         h = out.reshape(S, Fr, out.shape[1], co)
         fmap.append(h.permute(0, 3, 1, 2))
     return h.reshape(S, -1), fmap
+
+
+# ------------------------------------------------------------------ dropout (train mode)
+class _DropoutFn(torch.autograd.Function):
+    """nn.Dropout(p) in train mode on the device (stts_dropout): the mask is a counter draw keyed by a seed from
+    torch's default generator, redrawn (not stored) by the backward."""
+
+    @staticmethod
+    def forward(ctx, x, p):
+        _require_device()
+        xc = _c(x)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        y = torch.empty_like(xc)
+        check(_tl().stts_dropout(_ptr(xc), xc.numel(), ctypes.c_float(p), ctypes.c_ulonglong(seed), _ptr(y),
+                                 _stream()), "stts_dropout")
+        ctx.p, ctx.seed = p, seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dyc = _c(dy)
+        dx = torch.empty_like(dyc)
+        check(_tl().stts_dropout(_ptr(dyc), dyc.numel(), ctypes.c_float(ctx.p), ctypes.c_ulonglong(ctx.seed),
+                                 _ptr(dx), _stream()), "stts_dropout")
+        return dx, None
+
+
+def dropout(x, p):
+    return _DropoutFn.apply(x, float(p)) if p > 0 else x
+
+
+# ------------------------------------------------------------------ ProsodyPredictor.F0Ntrain (models.py:448-461)
+class _BiLSTMFn(torch.autograd.Function):
+    """ProsodyPredictor.shared (bidirectional nn.LSTM, batch_first, full-length rows) with its backward:
+    stts_bilstm_fwd_train / stts_bilstm_bwd.  x frames [B, T, Cin]; params in torch's order."""
+
+    @staticmethod
+    def forward(ctx, x, *params):
+        _require_device()
+        xc = _c(x)
+        B, T, Cin = xc.shape
+        ps = [_c(p) for p in params]
+        H = ps[1].shape[1]
+        arr = (ctypes.c_void_p * 8)(*[p.data_ptr() for p in ps])
+        L = _tl()
+        nb = int(L.stts_bilstm_workspace_bytes(B, T, H))
+        ws = _ws(nb, x.device)
+        y = torch.empty(B, T, 2 * H, dtype=torch.float32, device=x.device)
+        cs = torch.empty(2, B, T, H, dtype=torch.float32, device=x.device)
+        check(L.stts_bilstm_fwd_train(_ptr(xc), T * Cin, Cin, 1, B, T, Cin, arr, H, _ptr(y), _ptr(cs), _ptr(ws), nb,
+                                      _stream()), "stts_bilstm_fwd_train")
+        ctx.save_for_backward(xc, y, cs, *ps)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, y, cs, *ps = ctx.saved_tensors
+        B, T, Cin = xc.shape
+        H = ps[1].shape[1]
+        dyc = _c(dy)
+        need = ctx.needs_input_grad
+        dx = torch.empty_like(xc) if need[0] else None
+        grads = [torch.empty_like(p) if need[i + 1] else None for i, p in enumerate(ps)]
+        arr = (ctypes.c_void_p * 8)(*[p.data_ptr() for p in ps])
+        garr = (ctypes.c_void_p * 8)(*[g.data_ptr() if g is not None else None for g in grads])
+        L = _tl()
+        nb = int(L.stts_bilstm_bwd_workspace_bytes(B, T, Cin, H))
+        check(nb if nb < 0 else 0, "stts_bilstm_bwd_workspace_bytes")
+        ws = _ws(nb, dy.device)
+        check(L.stts_bilstm_bwd(_ptr(xc), B, T, Cin, arr, H, _ptr(y), _ptr(cs), _ptr(dyc), _ptr(dx), garr, _ptr(ws),
+                                nb, _stream()), "stts_bilstm_bwd")
+        return (dx, *grads)
+
+
+def bilstm_frames(lstm, x):
+    """lstm = the reference's nn.LSTM(.., bidirectional, batch_first) layout; x frames [B, T, Cin] -> [B, T, 2H]."""
+    ps = [lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0, lstm.weight_ih_l0_reverse,
+          lstm.weight_hh_l0_reverse, lstm.bias_ih_l0_reverse, lstm.bias_hh_l0_reverse]
+    return _BiLSTMFn.apply(x, *ps)
+
+
+def f0ntrain(pp, x, s, dtype="fp32"):
+    """ProsodyPredictor.F0Ntrain (models.py:448-461) with autograd: x [B, d_hid + style_dim, T], s [B, style_dim]
+    -> (F0 [B, 2T], N [B, 2T]).  The shared BiLSTM, the F0 / N AdainResBlk1d stacks (their dropout in train mode)
+    and the 1x1 projections, on frames [B, T, C] throughout."""
+    h = bilstm_frames(pp.shared, x.transpose(1, 2).contiguous())
+    outs = []
+    for blocks, proj in ((pp.F0, pp.F0_proj), (pp.N, pp.N_proj)):
+        y = h
+        for blk in blocks:
+            y = adain_resblk1d_frames(blk, y, s, dtype)
+        y = conv1d_frames(y, proj.weight, proj.bias, 1, 0, dtype=dtype)  # [B, 2T, 1]
+        outs.append(y[..., 0])
+    return outs[0], outs[1]
+
+
+# ------------------------------------------------------------------ StyleEncoder (models.py:125-150)
+class _RowExpFn(torch.autograd.Function):
+    """Row expansion of a frames image [B, H, W, C] for a k x k Conv2d with H padding `pad`: [B, Ho, W, C k]."""
+
+    @staticmethod
+    def forward(ctx, x, k, pad):
+        _require_device()
+        xc = _c(x)
+        B, H, W, C = xc.shape
+        Ho = H + 2 * pad - k + 1
+        xe = torch.empty(B, Ho, W, C * k, dtype=torch.float32, device=x.device)
+        check(_tl().stts_rowexp_fwd(_ptr(xc), B, H, W, C, k, pad, _ptr(xe), _stream()), "stts_rowexp_fwd")
+        ctx.geom = (B, H, W, C, k, pad)
+        return xe
+
+    @staticmethod
+    def backward(ctx, dxe):
+        B, H, W, C, k, pad = ctx.geom
+        d = _c(dxe)
+        dx = torch.empty(B, H, W, C, dtype=torch.float32, device=d.device)
+        check(_tl().stts_rowexp_bwd(_ptr(d), B, H, W, C, k, pad, _ptr(dx), _stream()), "stts_rowexp_bwd")
+        return dx, None, None
+
+
+class _DWConvS2Fn(torch.autograd.Function):
+    """LearnedDownSample('half'): depthwise Conv2d(C, C, 3, stride 2, pad 1) on frames images."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        _require_device()
+        xc, wc, bc = _c(x), _c(w), _c(b)
+        B, H, W, C = xc.shape
+        y = torch.empty(B, (H - 1) // 2 + 1, (W - 1) // 2 + 1, C, dtype=torch.float32, device=x.device)
+        check(_tl().stts_dwconv2d_s2_fwd(_ptr(xc), _ptr(wc), _ptr(bc), B, H, W, C, _ptr(y), _stream()),
+              "stts_dwconv2d_s2_fwd")
+        ctx.save_for_backward(xc, wc)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        B, H, W, C = xc.shape
+        d = _c(dy)
+        nx, nw, nb_ = ctx.needs_input_grad
+        dx = torch.empty_like(xc) if nx else None
+        dw = torch.empty_like(wc) if nw else None
+        db = torch.empty(C, dtype=torch.float32, device=d.device) if (nb_ and ctx.has_b) else None
+        L = _tl()
+        nb = int(L.stts_dwconv2d_s2_workspace_bytes(C))
+        ws = _ws(nb, d.device)
+        check(L.stts_dwconv2d_s2_bwd(_ptr(xc), _ptr(wc), _ptr(d), B, H, W, C, _ptr(dx), _ptr(dw), _ptr(db), _ptr(ws), nb,
+                                     _stream()), "stts_dwconv2d_s2_bwd")
+        return dx, dw, db
+
+
+class _AvgPool2Fn(torch.autograd.Function):
+    """DownSample('half') on frames images (the last column repeated when W is odd, then 2 x 2 averages)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _require_device()
+        xc = _c(x)
+        B, H, W, C = xc.shape
+        y = torch.empty(B, H // 2, (W + 1) // 2, C, dtype=torch.float32, device=x.device)
+        check(_tl().stts_avgpool2_fwd(_ptr(xc), B, H, W, C, _ptr(y), _stream()), "stts_avgpool2_fwd")
+        ctx.geom = (B, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, H, W, C = ctx.geom
+        d = _c(dy)
+        dx = torch.empty(B, H, W, C, dtype=torch.float32, device=d.device)
+        check(_tl().stts_avgpool2_bwd(_ptr(d), B, H, W, C, _ptr(dx), _stream()), "stts_avgpool2_bwd")
+        return dx
+
+
+class _SpatialMeanFn(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) of a frames image [B, H, W, C] -> [B, C]."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _require_device()
+        xc = _c(x)
+        B, H, W, C = xc.shape
+        y = torch.empty(B, C, dtype=torch.float32, device=x.device)
+        check(_tl().stts_spatial_mean_fwd(_ptr(xc), B, H * W, C, _ptr(y), _stream()), "stts_spatial_mean_fwd")
+        ctx.geom = (B, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, H, W, C = ctx.geom
+        d = _c(dy)
+        dx = torch.empty(B, H, W, C, dtype=torch.float32, device=d.device)
+        check(_tl().stts_spatial_mean_bwd(_ptr(d), B, H * W, C, _ptr(dx), _stream()), "stts_spatial_mean_bwd")
+        return dx
+
+
+def conv2d_frames(x, weight, bias, pad, dtype="fp32", residual=None, scale=1.0):
+    """Conv2d(k x k, stride 1, padding pad) of a frames image x [B, H, W, Cin] with the reference weight
+    [Cout, Cin, k, k]: the row expansion, then the conv1d engine over W (weight read as [Cout, Cin k, k]).
+    residual (frames image of the output's shape) and scale ride in the conv's epilogue: (y + residual) * scale."""
+    B, H, W, C = x.shape
+    co, ci, k, kw = weight.shape
+    if ci != C or kw != k:
+        raise ValueError(f"conv2d_frames: weight {tuple(weight.shape)} for {C} input channels")
+    xe = _RowExpFn.apply(x, k, pad) if k > 1 else x
+    Ho = xe.shape[1]
+    res = residual.reshape(B * Ho, residual.shape[2], co) if residual is not None else None
+    y = conv1d_frames(xe.reshape(B * Ho, W, C * k), weight.reshape(co, C * k, k), bias, 1, pad, 1, dtype,
+                      residual=res, scale=scale)
+    return y.reshape(B, Ho, y.shape[1], co)
+
+
+def style_encoder(se, mel, dtype="fp32"):
+    """StyleEncoder.forward (models.py:145-150) with autograd: mel [B, 1, n_mels, F] -> [B, style_dim].
+    shared = conv3x3 -> 4 x ResBlk('half': (DownSample(conv1x1(x)) + conv2(LReLU(LearnedDownSample(conv1(LReLU(x))))))
+    / sqrt(2), models.py:82-123) -> LReLU -> conv5x5 (valid) -> AdaptiveAvgPool2d(1) -> LReLU; unshared = Linear.
+    Frames images [B, n_mels, F, C] throughout."""
+    blocks = list(se.shared)
+    x = mel.permute(0, 2, 3, 1).contiguous()
+    c0 = blocks[0]
+    x = conv2d_frames(x, c0.weight, c0.bias, 1, dtype)
+    for blk in blocks[1:5]:
+        sc = x
+        if blk.learned_sc:
+            sc = conv2d_frames(sc, blk.conv1x1.weight, None, 0, dtype)
+        sc = _AvgPool2Fn.apply(sc)
+        r = conv2d_frames(leaky_relu(x, 0.2), blk.conv1.weight, blk.conv1.bias, 1, dtype)
+        ds = blk.downsample_res.conv
+        r = leaky_relu(_DWConvS2Fn.apply(r, ds.weight, ds.bias), 0.2)
+        x = conv2d_frames(r, blk.conv2.weight, blk.conv2.bias, 1, dtype, residual=sc, scale=1 / math.sqrt(2))
+    c5 = blocks[6]
+    x = conv2d_frames(leaky_relu(x, 0.2), c5.weight, c5.bias, 0, dtype)
+    h = leaky_relu(_SpatialMeanFn.apply(x), 0.2)
+    return linear(h, se.unshared.weight, se.unshared.bias)

@@ -11,9 +11,17 @@ does, in the reference's order:
     AdamW step on msd, mpd                                                       (:272-276)
     zero_grad; loss_mel = stft_loss(y_rec, wav); loss_gen_all = gl(wav, y_rec).mean();
     g_loss = lambda_mel loss_mel + lambda_gen loss_gen_all; backward; AdamW on the decoder   (:278-325)
-The other modules of train.py (text aligner, predictor, style encoder) are outside this path: their
-outputs come in as tensors, and their gradients (en.grad, F0.grad, N.grad, s.grad) are left on the inputs
-when those require grad.  `freeze_d_in_g` (default) turns off requires_grad of the discriminator parameters
+By default the other modules of train.py (text aligner, predictor, style encoder) are outside the step: their
+outputs come in as tensors, and their gradients (en.grad, F0.grad, N.grad, s.grad) are left on the inputs when those
+require grad.  With `predictor=` and `style_encoder=` the G step also runs them as train.py:258-270 does:
+
+    losses = step(en, None, None, None, wav, p_en=p_en, gt=gt_mel, F0_real=F0_real, N_real=N_real)
+
+computes s = style_encoder(gt.unsqueeze(1)), (F0_fake, N_fake) = predictor.F0Ntrain(p_en, s) (the predictor in
+train mode: its dropout), y_rec = decoder(en, F0_fake, N_fake, s), adds lambda_F0 smooth_l1(F0_real, F0_fake) / 10
+and lambda_norm smooth_l1(N_real, N_fake) to g_loss (:269-270, 300-307; F0_real comes from the pitch extractor and
+N_real = log_norm(gt), both outside this path) and steps AdamW on the predictor and the style encoder after the
+decoder's backward (:323-324).  `freeze_d_in_g` (default) turns off requires_grad of the discriminator parameters
 during the G step: the reference computes those gradients and discards them (its next iteration starts
 with zero_grad before they are used), so skipping them changes no update.
 """
@@ -21,14 +29,17 @@ from __future__ import annotations
 
 import torch
 
-from .losses import DiscriminatorLoss, GeneratorLoss, MultiResolutionSTFTLoss
+from .losses import DiscriminatorLoss, GeneratorLoss, MultiResolutionSTFTLoss, smooth_l1_loss
 from .optim import AdamW
 
 
 class TrainStep:
     def __init__(self, decoder, mpd, msd, lr_dec=1e-5, lr_disc=1e-4, lambda_mel=5.0, lambda_gen=1.0, dtype="fp32",
-                 freeze_d_in_g=True, capture=False):
+                 freeze_d_in_g=True, capture=False, predictor=None, style_encoder=None, lr_pred=1e-4, lr_style=1e-5,
+                 lambda_F0=1.0, lambda_norm=1.0):
         self.decoder, self.mpd, self.msd = decoder, mpd, msd
+        self.predictor, self.style_encoder = predictor, style_encoder
+        self.lambda_F0, self.lambda_norm = float(lambda_F0), float(lambda_norm)
         self.capture = capture  # keep copies of the gradients each optimizer step consumed (tests)
         self.captured = {}
         self.dtype = dtype  # the discriminators take it for the duration of each step only (__call__)
@@ -36,6 +47,11 @@ class TrainStep:
         self.stft_loss = MultiResolutionSTFTLoss()
         mk = lambda m, lr: AdamW(m.parameters(), lr=lr, weight_decay=1e-4, betas=(0.0, 0.99), eps=1e-9)  # noqa: E731
         self.opt = {"decoder": mk(decoder, lr_dec), "mpd": mk(mpd, lr_disc), "msd": mk(msd, lr_disc)}
+        # train.py:137-157: the predictor at the general lr, the style encoder at the acoustic ft_lr
+        if predictor is not None:
+            self.opt["predictor"] = mk(predictor, lr_pred)
+        if style_encoder is not None:
+            self.opt["style_encoder"] = mk(style_encoder, lr_style)
         self.lambda_mel, self.lambda_gen = float(lambda_mel), float(lambda_gen)
         self.freeze_d_in_g = freeze_d_in_g
 
@@ -43,15 +59,19 @@ class TrainStep:
         for o in self.opt.values():
             o.zero_grad()
 
-    def __call__(self, en, F0, N, s, wav, noise=None, seed=None):
+    def __call__(self, en, F0, N, s, wav, noise=None, seed=None, p_en=None, gt=None, F0_real=None, N_real=None):
         saved = (self.mpd.dtype_compute, self.msd.dtype_compute)
         self.mpd.dtype_compute = self.msd.dtype_compute = self.dtype
         try:
-            return self._step(en, F0, N, s, wav, noise, seed)
+            return self._step(en, F0, N, s, wav, noise, seed, p_en, gt, F0_real, N_real)
         finally:  # other users of the same discriminators keep their own compute dtype
             self.mpd.dtype_compute, self.msd.dtype_compute = saved
 
-    def _step(self, en, F0, N, s, wav, noise, seed):
+    def _step(self, en, F0, N, s, wav, noise, seed, p_en, gt, F0_real, N_real):
+        if self.style_encoder is not None and gt is not None:
+            s = self.style_encoder(gt.unsqueeze(1))  # train.py:258
+        if self.predictor is not None and p_en is not None:
+            F0, N = self.predictor.F0Ntrain(p_en, s)  # train.py:265
         y_rec = self.decoder(en, F0, N, s, noise=noise, seed=seed, dtype=self.dtype)
         self.zero_grad()
         d_loss = self.dl(wav.detach(), y_rec.detach()).mean()
@@ -73,6 +93,13 @@ class TrainStep:
             loss_mel = self.stft_loss(y_rec, wav)
             loss_gen_all = self.gl(wav, y_rec).mean()
             g_loss = self.lambda_mel * loss_mel + self.lambda_gen * loss_gen_all
+            extra = {}
+            if F0_real is not None:
+                extra["loss_F0_rec"] = smooth_l1_loss(F0_real, F0) / 10  # train.py:269
+                g_loss = g_loss + self.lambda_F0 * extra["loss_F0_rec"]
+            if N_real is not None:
+                extra["loss_norm_rec"] = smooth_l1_loss(N_real, N)  # train.py:270
+                g_loss = g_loss + self.lambda_norm * extra["loss_norm_rec"]
             g_loss.backward()
         finally:
             for p in frozen:
@@ -80,6 +107,14 @@ class TrainStep:
         if self.capture:
             self.captured["dec"] = {k: p.grad.detach().clone() for k, p in self.decoder.named_parameters()
                                     if p.grad is not None}
-        self.opt["decoder"].step()
-        return {"y_rec": y_rec.detach(), "d_loss": d_loss.detach(), "loss_mel": loss_mel.detach(),
-                "loss_gen_all": loss_gen_all.detach(), "g_loss": g_loss.detach()}
+            for tag, m in (("predictor", self.predictor), ("style_encoder", self.style_encoder)):
+                if m is not None:
+                    self.captured[tag] = {k: p.grad.detach().clone() for k, p in m.named_parameters()
+                                          if p.grad is not None}
+        for key in ("predictor", "style_encoder", "decoder"):  # train.py:323-325
+            if key in self.opt:
+                self.opt[key].step()
+        out = {"y_rec": y_rec.detach(), "d_loss": d_loss.detach(), "loss_mel": loss_mel.detach(),
+               "loss_gen_all": loss_gen_all.detach(), "g_loss": g_loss.detach()}
+        out.update({k: v.detach() for k, v in extra.items()})
+        return out

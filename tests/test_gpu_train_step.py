@@ -267,8 +267,13 @@ def test_adamw_matches_torch():
         od.step()
         oc.step()
     for a, b in zip(pd, pc):
-        # the scalars come in as doubles and are formed as torch forms them: the update is torch's, bit for bit
-        assert torch.equal(a.detach().cpu(), b.detach()), (a.detach().cpu() - b.detach()).abs().max().item()
+        # the scalars come in as doubles and are formed as torch forms them: every element within one fp32 ulp of
+        # torch's (its vectorised CPU loops may contract a product and a sum into one FMA where we do not), the
+        # spacing taken at |b| and floored at 1e-11 for elements near zero (where the ulp of the decayed parameter
+        # the update is subtracted from, not of the result, is the rounding step)
+        a, b = a.detach().cpu(), b.detach()
+        ulp = torch.nextafter(b.abs(), torch.tensor(float("inf"))) - b.abs()
+        assert ((a - b).abs() <= ulp.clamp_min(1e-11)).all(), (a - b).abs().max().item()
     sd = od.state_dict()
     assert sd["state"][0]["step"].item() == 3 and set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
 
@@ -588,9 +593,25 @@ def _run_step(dtype, B, T, sds=None):
     return out, step.captured, p0, p1, {k: t.grad for k, t in zip(("asr", "F0_curve", "N", "s"), ins)}
 
 
-# measured bounds of the bf16 step: module-normwise gradient error vs fp64, whole-module
-# cosine, smallest per-tensor cosine, AdamW update sign agreement, relative loss error
-BF16_STEP_BOUNDS = {"normwise": 5e-2, "cos": 0.995, "cos_min": 0.95, "sign": 0.97, "loss": 2e-2}
+# bounds of the bf16 step, about 2-3x the measured values (B2_T8 vs fp64 / config 5 vs the fp32
+# step): module-normwise gradient error (dec 3.5e-4 / 7.8e-4, mpd 1.0e-4 / 5.8e-5, msd 5.0e-3 / 5.4e-3, input
+# gradients 6.6e-2), whole-module cosine (>= 0.99986 for the parameters, 0.9986 for the inputs), smallest per-tensor
+# cosine (>= 0.976 / 0.909: MSD's first weight_v), AdamW update sign agreement where |g| > 1e-2 max (>= 0.994 /
+# 0.977), relative loss error (<= 2.7e-4)
+BF16_STEP_BOUNDS = {"loss": 1e-3,
+                    "normwise": {"dec": 2e-3, "mpd": 5e-4, "msd": 2e-2, "inputs": 0.2},
+                    "cos": {"dec": 0.9999, "mpd": 0.9999, "msd": 0.9995, "inputs": 0.995},
+                    "cos_min": {"dec": 0.95, "mpd": 0.995, "msd": 0.8, "inputs": 0.95},
+                    "sign": {"dec": 0.97, "mpd": 0.995, "msd": 0.95}}
+
+
+def _assert_bounds(tag, m):
+    bd = BF16_STEP_BOUNDS
+    assert m["normwise"] < bd["normwise"][tag], (tag, m)
+    assert m["cos"] > bd["cos"][tag], (tag, m)
+    assert m["cos_min"] > bd["cos_min"][tag], (tag, m)
+    if "sign" in m:
+        assert m["sign"] > bd["sign"][tag], (tag, m)
 
 
 def test_train_step_bf16_vs_fp64():
@@ -615,15 +636,11 @@ def test_train_step_bf16_vs_fp64():
         rows[dt] = row
         print(dt, {k: (v if not isinstance(v, dict) else {a: (round(b, 6) if isinstance(b, float) else b)
                                                            for a, b in v.items()}) for k, v in row.items()})
-    bd = BF16_STEP_BOUNDS
     r = rows["bf16"]
     for k in ("d_loss", "loss_mel", "loss_gen_all", "g_loss"):
-        assert r[k] < bd["loss"], (k, r[k])
+        assert r[k] < BF16_STEP_BOUNDS["loss"], (k, r[k])
     for tag in ("dec", "mpd", "msd", "inputs"):
-        m = r[tag]
-        assert m["normwise"] < bd["normwise"] and m["cos"] > bd["cos"] and m["cos_min"] > bd["cos_min"], (tag, m)
-        if tag != "inputs":
-            assert m["sign"] > bd["sign"], (tag, m["sign"])
+        _assert_bounds(tag, r[tag])
     # the fp32 step is the tight one (the fixture tests above bound it per tensor)
     for tag in ("dec", "mpd", "msd"):
         assert rows["fp32"][tag]["normwise"] < 1e-3 and rows["fp32"][tag]["cos"] > 0.999999, (tag, rows["fp32"][tag])
@@ -636,21 +653,19 @@ def test_train_step_bf16_config5_shape():
     res = {dt: _run_step(dt, B, T) for dt in ("fp32", "bf16")}
     o32, c32, p0, p32, gin32 = res["fp32"]
     o16, c16, _, p16, gin16 = res["bf16"]
-    bd = BF16_STEP_BOUNDS
     print("y_rec", _rel(o16["y_rec"], o32["y_rec"]))
     for k in ("d_loss", "loss_mel", "loss_gen_all", "g_loss"):
         e = abs(float(o16[k]) - float(o32[k])) / abs(float(o32[k]))
         print(k, float(o16[k]), float(o32[k]), e)
-        assert e < bd["loss"], k
+        assert e < BF16_STEP_BOUNDS["loss"], k
     for tag, i in (("dec", 0), ("mpd", 1), ("msd", 2)):
         m = _metrics(c16[tag], c32[tag])
         m["sign"] = _update_sign_agreement(p0[i], p16[tag], p32[tag], c32[tag])
         print(tag, m)
-        assert m["normwise"] < bd["normwise"] and m["cos"] > bd["cos"] and m["cos_min"] > bd["cos_min"], (tag, m)
-        assert m["sign"] > bd["sign"], (tag, m["sign"])
+        _assert_bounds(tag, m)
     m = _metrics(gin16, gin32)
     print("inputs", m)
-    assert m["normwise"] < bd["normwise"] and m["cos"] > bd["cos"], m
+    _assert_bounds("inputs", m)
 
 
 def test_engine_sees_adamw_update():
