@@ -49,11 +49,11 @@ ISTFT_CFG = dict(resblock_kernel_sizes=[3, 7, 11], upsample_rates=[10, 6], upsam
                  resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], upsample_kernel_sizes=[20, 12],
                  gen_istft_n_fft=20, gen_istft_hop_size=5)
 PEAK_HBM = 8.0e12        # B/s, MI355X HBM3E (MI355X_MICROARCH.md chip table)
-PEAK_MFMA = {"bf16": 2.5e15, "fp32": 157.3e12}  # dense FLOP/s
+PEAK_MFMA = {"bf16": 2.5e15, "fp32": 157.3e12, "bf16x3": 2.5e15 / 3}  # dense FLOP/s (bf16x3: 3 bf16 MFMAs a product)
 # algorithmic work per output sample (activation bytes: each conv reads its input
 # once and writes its output once, everything else fused)
-ALG = {"hifigan": {"flops": 2.913e6, "bytes": {"bf16": 9709.0, "fp32": 19417.0}},
-       "istftnet": {"flops": 2.163e6, "bytes": {"bf16": 3632.0, "fp32": 7265.0}}}
+ALG = {"hifigan": {"flops": 2.913e6, "bytes": {"bf16": 9709.0, "fp32": 19417.0, "bf16x3": 19417.0}},
+       "istftnet": {"flops": 2.163e6, "bytes": {"bf16": 3632.0, "fp32": 7265.0, "bf16x3": 7265.0}}}
 METRIC = "24 kHz audio samples/sec/GPU + real-time factor, 10-s utterance batch"
 
 
@@ -194,10 +194,11 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=400, help="asr frames per utterance (400 = 10 s)")
     ap.add_argument("--decoder", default="hifigan", choices=["hifigan", "istftnet"])
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "bf16x3"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-parity-mode", action="store_true", help="skip the fp32 figure of the same workload")
+    ap.add_argument("--no-accuracy-mode", action="store_true", help="skip the bf16x3 figure of the same workload")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-to-host (PCIe-inclusive) figure")
     ap.add_argument("--selftest-cpu", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dump-checksum", default=None, help=argparse.SUPPRESS)
@@ -310,6 +311,18 @@ def main():
                   "hbm_fraction": ALG[args.decoder]["bytes"]["fp32"] * global_batch * 600 * T * 3 / elp / PEAK_HBM,
                   "mfma_fraction": ALG[args.decoder]["flops"] * global_batch * 600 * T * 3 / elp / PEAK_MFMA["fp32"]}
         dec.engine(args.dtype)
+    accuracy = None
+    if not cpu and not args.no_accuracy_mode and args.dtype == "bf16":
+        # the split-operand accuracy mode (fp32 storage, conv operands as bf16 hi + lo on the bf16 MFMA:
+        # 10-s max-abs 2.5e-5 vs the reference, tests/test_gpu_split.py) on the same workload
+        aeng = dec.engine("bf16x3")
+        ela, _ = timed(lambda i: step(i, e=aeng), 3, 1)
+        nsm = global_batch * 600 * T * 3
+        accuracy = {"dtype": "bf16x3", "steps": 3, "ms_per_step": ela / 3 * 1e3, "value": nsm / ela,
+                    "hbm_fraction": ALG[args.decoder]["bytes"]["bf16x3"] * nsm / ela / PEAK_HBM,
+                    "mfma_fraction": ALG[args.decoder]["flops"] * nsm / ela / PEAK_MFMA["bf16x3"],
+                    "vs_parity_mode": (nsm / ela) / parity["value"] if parity else None}
+        dec.engine(args.dtype)
     e2e = None
     if not cpu and not args.no_e2e:
         # host -> host: pinned host inputs copied in, decoded, audio copied back (PCIe included)
@@ -358,6 +371,8 @@ def main():
         line["with_gather"] = with_gather
     if parity:
         line["parity_mode"] = parity
+    if accuracy:
+        line["accuracy_mode"] = accuracy
     if e2e:
         line["e2e_pcie"] = e2e
     if not cpu and not args.no_cpu_baseline and world == 1:

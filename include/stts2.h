@@ -45,6 +45,8 @@ typedef struct stts_model stts_model;
 /* compute / activation dtypes */
 #define STTS_FP32 0 /* fp32 storage, exact-fp32 MFMA (parity mode)          */
 #define STTS_BF16 1 /* bf16 storage, bf16 MFMA with fp32 accumulation      */
+#define STTS_SPLIT 2 /* accuracy mode: fp32 storage, conv operands split into bf16 hi + lo,
+                        hi*hi + hi*lo + lo*hi on the bf16 MFMA (fp32 accumulation)        */
 
 /* error codes (negative) */
 #define STTS_EINVAL (-1)
@@ -148,6 +150,8 @@ int stts_mrstft_loss(const float* x, const float* y, int B, long long L, long lo
  * channel-transposed, tap-reversed weight and padding dil (K - 1) - pad; of a strided conv (dil 1) = the
  * polyphase ConvTranspose1d of dy); dw / db always compute in fp32 (f32 MFMA over (utterance, frame)
  * row slices, fp64 fixed-order slice sums: deterministic).  dx, dw, db may each be null.
+ * The forward entries (stts_conv1d_fwd / _res / _act) also take STTS_SPLIT (fp32 frames, split-operand MFMA);
+ * the backward takes STTS_FP32 / STTS_BF16.
  * Workspace >= the matching *_workspace_bytes. */
 long long stts_conv1d_fwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride, int dil,
                                           int pad, int Lq);
@@ -155,7 +159,7 @@ int stts_conv1d_fwd(int dtype, const float* x, const float* w, const float* bias
                     int K, int stride, int dil, int pad, int Lq, float* y, void* workspace, long long ws_bytes,
                     void* stream);
 /* The same with a residual added in the epilogue: y = (conv1d(x, w, bias) + res) * scale (res fp32 [B][Lq][Cout];
- * dtype STTS fp32 and Cout % 16 == 0 or Cout <= 32; ST_EINVAL otherwise, and for res = NULL with scale != 1).  AdaINResBlock1's x = xt + x
+ * dtype STTS_FP32 / STTS_SPLIT and Cout % 16 == 0 or Cout <= 32; ST_EINVAL otherwise, and for res = NULL with scale != 1).  AdaINResBlock1's x = xt + x
  * (hifigan.py:74) rides on convs2 this way; its gradient w.r.t. res is dy itself. */
 int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, const float* bias, const float* res, float scale, int B,
                         int Lin, int Cin, int Cout, int K, int stride, int dil, int pad, int Lq, float* y,
@@ -410,6 +414,9 @@ const char* stts_error_string(int code);
  *                     1 = for the residual / running-sum launches with K >= 7 (default, where it measured
  *                     faster), 2 = for every C = 64 launch, 0 = never. */
 #define STTS_OPT_RCPP 18
+/*   STTS_OPT_RESSPLIT 1 (default) = the accuracy mode's (STTS_SPLIT) C = 32 / 64 resblock convs run on the split
+ *                     resblock engine (ressplit.hip; C = 64 in two input-channel passes); 0 = conv1d_igemm (A/B). */
+#define STTS_OPT_RESSPLIT 19
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

@@ -11,7 +11,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-enum StDtype { ST_FP32 = 0, ST_BF16 = 1 };
+// ST_SPLIT (accuracy mode): fp32 storage, every conv's operands split into bf16 hi + lo parts and
+// multiplied as hi*hi + hi*lo + lo*hi on the bf16 MFMA (fp32 accumulation)
+enum StDtype { ST_FP32 = 0, ST_BF16 = 1, ST_SPLIT = 2 };
+constexpr int ST_NDTYPES = 3;
 
 // domain error codes (negative; positive values are hipError_t)
 enum StStatus {

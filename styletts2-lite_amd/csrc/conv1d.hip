@@ -49,6 +49,11 @@ template <> struct Layout<float> {
 template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN>
 struct ConvCfg {
   static constexpr bool BF = std::is_same<MT, bf16_t>::value;
+  // ST_SPLIT (accuracy mode): fp32 activations on the bf16 MFMA path, every window and weight slice
+  // staged twice (hi, lo) and multiplied as hi*hi + hi*lo + lo*hi
+  static constexpr bool SPLIT = BF && std::is_same<T, float>::value;
+  static constexpr bool LOWP = BF && !SPLIT;  // the bf16 throughput mode's shortcuts (v_sin, reciprocal)
+  static constexpr int SPL = SPLIT ? 2 : 1;
   static constexpr int NW = WAVES_M * WAVES_N;
   static constexpr int NT = 64 * NW;
   static constexpr int BM = 32 * WM * WAVES_M;
@@ -68,13 +73,15 @@ struct ConvCfg {
     return (((size_t)rows(p) * XP * sizeof(MT)) + 15) & ~(size_t)15;
   }
   static size_t lds_bytes(const ConvParams& p, int nwslices, int nx = 1) {
-    return coef_bytes(p) + (size_t)nx * xs_bytes(p) + (size_t)nwslices * W_TAP * sizeof(MT);
+    return coef_bytes(p) + (size_t)SPL * ((size_t)nx * xs_bytes(p) + (size_t)nwslices * W_TAP * sizeof(MT));
   }
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
-// bf16: at least 2 waves per SIMD (<= 256 VGPRs); fp32 (parity mode) keeps its registers
-template <typename MT> constexpr int kMinWaves = std::is_same<MT, bf16_t>::value ? 2 : 1;
+// bf16: at least 2 waves per SIMD (<= 256 VGPRs); fp32 (parity mode) and the split accuracy mode (fp32
+// windows, hi + lo fragments) keep their registers on 4-wave tiles
+template <typename T, typename MT>
+constexpr int kMinWaves = (std::is_same<MT, bf16_t>::value && std::is_same<T, bf16_t>::value) ? 2 : 1;
 
 // 16 values <-> 8 packed pairs
 __device__ __forceinline__ f2v pr(const float (&v)[16], int i) { return f2v{v[2 * i], v[2 * i + 1]}; }
@@ -90,7 +97,7 @@ __device__ __forceinline__ void pw(float (&v)[16], int i, f2v x) {
 // therefore works straight from registers: no LDS transpose, 16-channel vector loads/stores,
 // and per-lane statistics accumulated across tiles (reduced across lanes once per utterance).
 template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW, int CPS>
-__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT>))
     conv1d_igemm_kernel(const ConvParams p) {
   using C = ConvCfg<T, MT, WAVES_M, WAVES_N, WM, WN>;
   constexpr int BM = C::BM, BN = C::BN, XP = C::XP, WPITCH = C::WPITCH, W_TAP = C::W_TAP, NT = C::NT;
@@ -105,8 +112,13 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   // chunks per step (set by the launcher): 2 = two 32-channel chunks (two windows, two weight
   // slices) per barrier pair, half the barriers and twice the MFMAs between them
   constexpr int cps = CPS;
-  MT* Ws = reinterpret_cast<MT*>(smem + C::coef_bytes(p) + (size_t)cps * C::xs_bytes(p));
+  static_assert(!C::SPLIT || CPS == 1, "split mode stages one chunk per step (hi, lo windows)");
+  MT* Ws = reinterpret_cast<MT*>(smem + C::coef_bytes(p) + (size_t)C::SPL * cps * C::xs_bytes(p));
+  // the second window slot: chunk c+1 (cps == 2) or, in split mode, the lo parts of the window
   const size_t xs_el = C::xs_bytes(p) / sizeof(MT);
+  // split mode: the lo weight slices follow the hi ones (resident: all of them; streamed: one tap group)
+  const size_t wlo = C::SPLIT ? (p.w_resident ? (size_t)p.nchunks * p.KS * W_TAP : (size_t)p.tg * W_TAP) : 0;
+  const unsigned wlo_bytes = C::SPLIT ? (unsigned)((size_t)p.nchunks * p.KS * BK * ((p.N + 31) & ~31) * sizeof(MT)) : 0u;
 
   const int ntn = (p.N + BN - 1) / BN;
   const int ntm = (p.Lq + BM - 1) / BM;
@@ -157,7 +169,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
     }
   };
 
-  const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)p.nchunks * p.KS * BK * Np * sizeof(MT)));
+  const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)C::SPL * p.nchunks * p.KS * BK * Np * sizeof(MT)));
   auto stage_w = [&](int c, int tap0, int ntap, MT* dst, int n0) {
     if constexpr (C::BF) {  // packed bf16: [chunk][tap][Np][32]
       const int units = ntap * BN * 4;
@@ -167,6 +179,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
         const int gp = g ^ ((gn >> 2) & 3);  // swizzled packed layout (st_pack_conv)
         const unsigned off = gn < Np ? (unsigned)(((((size_t)c * p.KS + tap0 + tl) * Np + gn) * BK + 8 * gp) * 2) : OOB;
         *reinterpret_cast<uint4*>(dst + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = bload16(rw, off);
+        if constexpr (C::SPLIT)
+          *reinterpret_cast<uint4*>(dst + wlo + (size_t)tl * W_TAP + n * WPITCH + 8 * g) =
+              bload16(rw, off == OOB ? OOB : off + wlo_bytes);
       }
     } else {  // packed fp32: [chunk][tap][32][Np]
       const int units = ntap * BK * (BN / 4);
@@ -183,7 +198,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   // software-pipelined through registers like the input window — group g+1's loads are issued
   // right after group g is written to LDS, so the L2 latency hides under group g's MFMAs.
   constexpr int MAXW = 4;  // 16-byte W units per thread per group (launch_cfg sizes tg to fit)
-  auto issue_w = [&](int t, int c, int tap0, uint4 (&wpre)[MAXW]) {
+  constexpr int MAXW2 = MAXW * C::SPL;  // split mode: the lo units follow
+  auto issue_w = [&](int t, int c, int tap0, uint4 (&wpre)[MAXW2]) {
     const int n0 = t_nt(t) * BN;
     const int ntap = min(p.tg, p.KS - tap0);
 #pragma unroll
@@ -202,15 +218,18 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
           off = (unsigned)(((((size_t)c * p.KS + tap0 + tl) * BK + kq) * Np + gn) * 4);
       }
       wpre[k] = bload16(rw, off);
+      if constexpr (C::SPLIT) wpre[MAXW + k] = bload16(rw, off == OOB ? OOB : off + wlo_bytes);
     }
   };
-  auto put_w = [&](int ntap, const uint4 (&wpre)[MAXW], MT* Wd) {
+  auto put_w = [&](int ntap, const uint4 (&wpre)[MAXW2], MT* Wd) {
 #pragma unroll
     for (int k = 0; k < MAXW; ++k) {
       const int u = tid + k * NT;
       if constexpr (C::BF) {
         const int tl = u / (BN * 4), rem = u % (BN * 4), n = rem >> 2, g = rem & 3;
         if (tl < ntap) *reinterpret_cast<uint4*>(Wd + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = wpre[k];
+        if constexpr (C::SPLIT)
+          if (tl < ntap) *reinterpret_cast<uint4*>(Wd + wlo + (size_t)tl * W_TAP + n * WPITCH + 8 * g) = wpre[MAXW + k];
       } else {
         const int tl = u / (BK * (BN / 4)), rem = u % (BK * (BN / 4)), kq = rem / (BN / 4), g = rem % (BN / 4);
         if (tl < ntap) *reinterpret_cast<uint4*>(Wd + (size_t)tl * W_TAP + kq * WPITCH + 4 * g) = wpre[k];
@@ -314,7 +333,16 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
       for (int j = 0; j < 8; ++j) v[j] = 0.f;
     }
     MT* dst = Xd + r * XP + 8 * g8;
-    if constexpr (C::BF) {
+    if constexpr (C::SPLIT) {  // hi = bf16(v) (round to nearest even), lo = bf16(v - hi): v - hi is exact
+      bf16x8 o, ol;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = (bf16_t)v[j];
+        ol[j] = (bf16_t)(v[j] - (float)o[j]);
+      }
+      *reinterpret_cast<bf16x8*>(dst) = o;
+      *reinterpret_cast<bf16x8*>(dst + xs_el) = ol;
+    } else if constexpr (C::BF) {
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (bf16_t)v[j];
@@ -370,7 +398,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   auto st_tile = [&](int st) { return tbeg + st / npt; };
   auto st_chunk = [&](int st) { return (st % npt) * cps; };
   typename RawT<T>::type preA[MAXU], preB[MAXU];
-  uint4 wpA[MAXW], wpB[MAXW];
+  uint4 wpA[MAXW2], wpB[MAXW2];
   if (nsteps > 0) {
     issue(tbeg, 0, preA);
     if (!resident) issue_w(tbeg, 0, 0, wpA);
@@ -384,8 +412,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
   }
   // always_inline: left to itself the compiler outlines the fp32 instantiations' step into a
   // called function, which puts the register sets (passed by reference) in scratch memory
-  auto step = [&](int st, typename RawT<T>::type (&pre)[MAXU], uint4 (&wpre)[MAXW],
-                  typename RawT<T>::type (&pre2)[MAXU], uint4 (&wpre2)[MAXW]) __attribute__((always_inline)) {
+  auto step = [&](int st, typename RawT<T>::type (&pre)[MAXU], uint4 (&wpre)[MAXW2],
+                  typename RawT<T>::type (&pre2)[MAXU], uint4 (&wpre2)[MAXW2]) __attribute__((always_inline)) {
     const int t = st_tile(st), c = st_chunk(st);
     const bool last = c + cps >= p.nchunks;     // the tile's epilogue follows this step
     const bool has2 = cps == 2 && c + 1 < p.nchunks;
@@ -407,7 +435,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
             }
             coef[ci] = be - m * a;   // x * a + (beta - mean * a)  ==  (x - mean) * a + beta
             coef[cinp + ci] = a;
-            coef[2 * cinp + ci] = C::BF ? al * 0.15915494309189535f : al;  // bf16: alpha in revolutions
+            coef[2 * cinp + ci] = FAST_SIN ? al * 0.15915494309189535f : al;  // bf16: alpha in revolutions
             coef[3 * cinp + ci] = 1.0f / al;  // the reference's (1 / alpha), once per channel
           }
         }
@@ -500,7 +528,35 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
         // 1-D convs (row_off == 0): no per-tap division on the scalar unit
         const int toff = p.row_off == 0 ? tap * p.dil : (tap / p.kw) * p.row_off + (tap % p.kw) * p.dil;
         const MT* wt = wb + (size_t)tl * W_TAP;
-        if constexpr (C::BF) {
+        if constexpr (C::SPLIT) {
+#pragma unroll
+          for (int kk = 0; kk < BK / 16; ++kk) {
+            bf16x8 af[WM], bw[WN], afl[WM], bwl[WN];
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi) {
+              const int r = (wm * WM + mi) * 32 + l32;
+              const MT* xa = Xc + (r * p.stride + toff) * XP + kk * 16 + hi * 8;
+              af[mi] = *reinterpret_cast<const bf16x8*>(xa);
+              afl[mi] = *reinterpret_cast<const bf16x8*>(xa + xs_el);
+            }
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni) {
+              const int n = (wn * WN + ni) * 32 + l32;
+              const MT* wa = wt + n * WPITCH + kk * 16 + hi * 8;
+              bw[ni] = *reinterpret_cast<const bf16x8*>(wa);
+              bwl[ni] = *reinterpret_cast<const bf16x8*>(wa + wlo);
+            }
+            // the two small cross terms first, then hi*hi (lo*lo, ~2^-18 of the product, is dropped)
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+              for (int ni = 0; ni < WN; ++ni) {
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[ni], afl[mi], acc[mi][ni], 0, 0, 0);
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bwl[ni], af[mi], acc[mi][ni], 0, 0, 0);
+                acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[ni], af[mi], acc[mi][ni], 0, 0, 0);
+              }
+          }
+        } else if constexpr (C::BF) {
 #pragma unroll
           for (int kk = 0; kk < BK / 16; ++kk) {
             bf16x8 af[WM], bw[WN];
@@ -609,7 +665,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, kMinWaves<MT>)
                   if constexpr (PREF) raw16_to_f32(racc[PREF ? mi : 0][PREF ? ni : 0], r);
                   else load16(accb + (size_t)orow * p.acc_ld + co0, r);
                   if (p.acc_div != 0.f) {
-                    if constexpr (C::BF) {  // bf16 mode multiplies by the reciprocal
+                    if constexpr (C::LOWP) {  // bf16 mode multiplies by the reciprocal
                       const float id = 1.0f / p.acc_div;
                       const f2v inv = f2v{id, id};
 #pragma unroll
@@ -710,7 +766,7 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
   constexpr int LDS_MAX = 160 * 1024;
   constexpr int WBUDGET = 48 * 1024;
   constexpr int WRES_BUDGET = 120 * 1024;
-  const size_t wtap = (size_t)C::W_TAP * sizeof(MT);
+  const size_t wtap = (size_t)C::SPL * C::W_TAP * sizeof(MT);
   // weights resident across tiles when every chunk x tap slice of the column tile fits
   const int nres = p.nchunks * p.KS;
   if ((size_t)nres * wtap <= (size_t)WRES_BUDGET && C::lds_bytes(p, nres) <= (size_t)LDS_MAX) {
@@ -730,14 +786,14 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
   // two chunks per step (bf16 wide configs with one tap group, when the second window and weight
   // slice fit the LDS): half the barriers and twice the MFMAs between them
   p.cps = 1;
-  if (C::BF && !NARROW && p.nchunks >= 2 && (p.w_resident || p.tg >= p.KS) &&
+  if (C::LOWP && !NARROW && p.nchunks >= 2 && (p.w_resident || p.tg >= p.KS) &&
       C::lds_bytes(p, p.w_resident ? nres : 2 * p.tg, 2) <= (size_t)LDS_MAX)
     p.cps = 2;
   const size_t lds = C::lds_bytes(p, p.w_resident ? nres : p.cps * p.tg, p.cps);
   if (lds > (size_t)LDS_MAX) return ST_EINVAL;
   auto kern1 = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 1>;
   auto kern = kern1;
-  if constexpr (C::BF && !NARROW) {
+  if constexpr (C::LOWP && !NARROW) {
     if (p.cps == 2) kern = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 2>;
   }
   static bool attr_set[2] = {false, false};
@@ -777,7 +833,7 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
   // stride 2 with N <= 32 (the MSD (3, 9) layers of the training step, N = 32): BM 128 x BN 32, every
   // column live, instead of the 64 x 128 tile with three quarters of its columns idle (STTS_OPT_EXP 1024:
   // the old tile, for A/B)
-  if constexpr (ConvCfg<T, MT, 1, 1, 1, 1>::BF) {
+  if constexpr (ConvCfg<T, MT, 1, 1, 1, 1>::LOWP) {
     if (p.stride == 2 && p.N <= 32 && !(g_opt_exp & 1024)) return launch_cfg<T, MT, 4, 1, 1, 1>(p, stream);
   }
   if (p.stride > 1) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);  // BM 64 x BN 128 (short window)
@@ -789,9 +845,9 @@ int launch_typed(const ConvParams& p, hipStream_t stream) {
     if (big < ncu / 2) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);
   }
   if (p.N <= 32) return launch_cfg<T, MT, 4, 1, 2, 1>(p, stream);     // BM 256 x BN 32, 4 waves
-  if constexpr (!ConvCfg<T, MT, 1, 1, 1, 1>::BF) {
-    // fp32 (parity mode): 4-wave tiles, so a wave may hold its fp32 windows and weight slices in
-    // up to 512 registers (the 8-wave tiles are capped at 256 and spill)
+  if constexpr (!ConvCfg<T, MT, 1, 1, 1, 1>::LOWP) {
+    // fp32 (parity mode) and split: 4-wave tiles, so a wave may hold its fp32 windows and weight slices
+    // (split: hi and lo) in up to 512 registers (the 8-wave tiles are capped at 256 and spill)
     if (p.N <= 64) return launch_cfg<T, MT, 2, 2, 2, 1>(p, stream);   // BM 128 x BN 64
     return launch_cfg<T, MT, 2, 2, 2, 2>(p, stream);                  // BM 128 x BN 128
   } else {
@@ -821,6 +877,7 @@ int st_conv1d_engine(const ConvParams& p, int dtype) {
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return ST_ENGINE_RESCONV;
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
   if (st_pw_split_eligible(q, dtype) || st_pw_eligible(q, dtype)) return ST_ENGINE_PW;
+  if (st_ressplit_eligible(q, dtype)) return ST_ENGINE_RESSPLIT;
   return ST_ENGINE_IGEMM;
 }
 
@@ -840,9 +897,11 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return st_bigconv(q, stream);
   if (st_pw_split_eligible(q, dtype)) return st_pw_split(q, stream);
   if (st_pw_eligible(q, dtype)) return st_pw(q, stream);
+  if (st_ressplit_eligible(q, dtype)) return st_ressplit(q, stream);
   if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);
   if (dtype == ST_BF16) {
     return launch_typed<bf16_t, bf16_t>(q, stream);
   }
+  if (dtype == ST_SPLIT) return launch_typed<float, bf16_t>(q, stream);
   return ST_EDTYPE;
 }

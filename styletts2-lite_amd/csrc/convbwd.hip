@@ -544,7 +544,7 @@ EngineGeo engine_geo(const Geo& g, bool fwd) {
 }
 
 WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
-  const size_t esz = dtype == ST_FP32 ? 4 : 2;
+  const size_t esz = dtype == ST_BF16 ? 2 : 4;  // ST_SPLIT: fp32 frames, bf16 hi + lo weights
   const EngineGeo e = engine_geo(g, fwd);
   WsLayout w;
   memset(&w, 0, sizeof(w));
@@ -558,7 +558,7 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
   w.packed = off;
   off += al(st_packed_conv_elems(e.ci, e.co_p, g.K, e.transposed, e.u) * esz);
   w.yout = off;
-  if (dtype != ST_FP32 || e.co_p != e.co) off += al((size_t)g.B * e.Lout * e.co_p * esz);
+  if (dtype == ST_BF16 || e.co_p != e.co) off += al((size_t)g.B * e.Lout * e.co_p * esz);
   if (!fwd) {
     const Slices sl = slices_of(g);
     w.part = off;
@@ -586,12 +586,13 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   const WsLayout L = ws_layout(g, dtype, fwd);
   const int K = g.K, B = g.B;
   const int ldx = ldpad(e.ci);
+  const int adt = dtype == ST_BF16 ? ST_BF16 : ST_FP32;  // frames storage (the split mode keeps fp32)
   void* xd = ws + L.xin;
   void* wd = ws + L.packed;
-  if (dtype == ST_FP32 && ldx == e.ci)
+  if (adt == ST_FP32 && ldx == e.ci)
     xd = (void*)xf;  // fp32 frames with 8-aligned rows are the engine's input as they are
   else
-    ST_CHECK(st_frames_convert(xf, B, e.Lin, e.ci, e.ci, xd, ldx, nullptr, 0, dtype, s));
+    ST_CHECK(st_frames_convert(xf, B, e.Lin, e.ci, e.ci, xd, ldx, nullptr, 0, adt, s));
   const float* wsrc = w;
   if (e.wm != W_PLAIN || e.co_p != e.co) {
     float* wt = (float*)(ws + L.wstage);
@@ -653,7 +654,7 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
     p.Lq = (e.Lout - 1 + g.pad) / e.u + 1;
   }
   p.Lout = e.Lout;
-  const bool direct = dtype == ST_FP32 && e.co_p == e.co;
+  const bool direct = adt == ST_FP32 && e.co_p == e.co;
   void* yd = direct ? (void*)y : (void*)(ws + L.yout);
   p.y = yd;
   p.y_bs = (long long)e.Lout * e.co_p;
@@ -664,13 +665,13 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
     p.epi_slope = slope;
   }
   if (res) {  // y = conv + res (fp32 frames [B][Lout][co], the same layout as y)
-    if (dtype != ST_FP32 || e.co_p != e.co) return ST_EINVAL;
+    if (adt != ST_FP32 || e.co_p != e.co) return ST_EINVAL;
     p.res = res;
     p.res_bs = (long long)e.Lout * e.co;
     p.res_ld = e.co;
   }
   ST_CHECK(st_conv1d(p, dtype, s));
-  if (!direct) ST_CHECK(st_frames_to_f32(yd, B, e.Lout, e.co, e.co_p, y, dtype, s));
+  if (!direct) ST_CHECK(st_frames_to_f32(yd, B, e.Lout, e.co, e.co_p, y, adt, s));
   return 0;
 }
 
@@ -732,7 +733,7 @@ void launch_wgrad(const Geo& g, const Slices& sl, const float* x, const float* d
 
 extern "C" long long stts_conv1d_fwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride,
                                                      int dil, int pad, int Lq) {
-  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  if (dtype != ST_FP32 && dtype != ST_BF16 && dtype != ST_SPLIT) return ST_EDTYPE;
   const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
   if (!geo_ok(g)) return ST_EINVAL;
   return (long long)ws_layout(g, dtype, true).total;

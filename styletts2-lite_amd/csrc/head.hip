@@ -23,17 +23,19 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 // weights: the packed conv buffer's column 0 (packing in misc.hip k_pack_conv; 32-channel chunks,
 // 7 taps, Np = 32): bf16 [chunk][tap][Np][32] whose row 0 is column 0 with unit swizzle
-// (0 >> 2) & 3 = 0, or fp32 [chunk][tap][32][Np]
-template <typename T>
+// (0 >> 2) & 3 = 0 (ST_SPLIT: the hi copy, then the lo copy), or fp32 [chunk][tap][32][Np]
+// WL: weight layout 0 = fp32, 1 = bf16, 2 = ST_SPLIT (bf16 hi parts, then the lo parts: hi + lo in fp32)
+template <int WL, int C>
 __device__ __forceinline__ float wcol0(const void* w, int tap, int ci) {
   const size_t ct = (size_t)(ci / 32) * 7 + tap;
-  if constexpr (std::is_same<T, bf16_t>::value)
-    return (float)reinterpret_cast<const bf16_t*>(w)[ct * 32 * 32 + ci % 32];
-  else
-    return reinterpret_cast<const float*>(w)[(ct * 32 + ci % 32) * 32];
+  if constexpr (WL == 0) return reinterpret_cast<const float*>(w)[(ct * 32 + ci % 32) * 32];
+  const bf16_t* wb = reinterpret_cast<const bf16_t*>(w);
+  float v = (float)wb[ct * 32 * 32 + ci % 32];
+  if constexpr (WL == 2) v += (float)wb[(size_t)(C / 32) * 7 * 32 * 32 + ct * 32 * 32 + ci % 32];
+  return v;
 }
 
-template <typename T, int C>
+template <typename T, int C, int WL>
 __global__ void __launch_bounds__(HT) k_conv_post(const T* __restrict__ x, long long x_bs, int x_ld, int L,
                                                   const void* __restrict__ w, const float* __restrict__ bias,
                                                   const float* __restrict__ alpha, float* __restrict__ y) {
@@ -41,7 +43,7 @@ __global__ void __launch_bounds__(HT) k_conv_post(const T* __restrict__ x, long 
   __shared__ float al[2][C];      // Snake: alpha (bf16: in revolutions), 1 / alpha
   __shared__ float z[HT * 7 + 1];
   const int tid = threadIdx.x, b = blockIdx.y;
-  for (int i = tid; i < 7 * C; i += HT) wl[i / C][i % C] = wcol0<T>(w, i / C, i % C);
+  for (int i = tid; i < 7 * C; i += HT) wl[i / C][i % C] = wcol0<WL, C>(w, i / C, i % C);
   for (int i = tid; i < C; i += HT) {
     const float a = alpha[i];
     al[0][i] = std::is_same<T, bf16_t>::value ? a * 0.15915494309189535f : a;
@@ -95,10 +97,10 @@ __global__ void __launch_bounds__(HT) k_conv_post(const T* __restrict__ x, long 
   }
 }
 
-template <typename T, int C>
+template <typename T, int C, int WL>
 int launch_head(const ConvParams& p, hipStream_t s) {
   dim3 grid((p.Lq + HQ - 1) / HQ, p.B);
-  hipLaunchKernelGGL((k_conv_post<T, C>), grid, dim3(HT), 0, s, reinterpret_cast<const T*>(p.x), p.x_bs, p.x_ld,
+  hipLaunchKernelGGL((k_conv_post<T, C, WL>), grid, dim3(HT), 0, s, reinterpret_cast<const T*>(p.x), p.x_bs, p.x_ld,
                      p.Lq, p.w, p.bias, p.pro.alpha, reinterpret_cast<float*>(p.y));
   return (int)hipGetLastError();
 }
@@ -113,7 +115,8 @@ bool st_head_eligible(const ConvParams& p) {
 }
 
 int st_head(const ConvParams& p, int dtype, hipStream_t s) {
-  if (dtype == ST_BF16) return p.Cin == 32 ? launch_head<bf16_t, 32>(p, s) : launch_head<bf16_t, 64>(p, s);
-  if (dtype == ST_FP32) return p.Cin == 32 ? launch_head<float, 32>(p, s) : launch_head<float, 64>(p, s);
+  if (dtype == ST_BF16) return p.Cin == 32 ? launch_head<bf16_t, 32, 1>(p, s) : launch_head<bf16_t, 64, 1>(p, s);
+  if (dtype == ST_FP32) return p.Cin == 32 ? launch_head<float, 32, 0>(p, s) : launch_head<float, 64, 0>(p, s);
+  if (dtype == ST_SPLIT) return p.Cin == 32 ? launch_head<float, 32, 2>(p, s) : launch_head<float, 64, 2>(p, s);
   return ST_EDTYPE;
 }

@@ -598,7 +598,7 @@ __global__ void __launch_bounds__(256) k_wn_fold(const float* __restrict__ v, co
 template <typename MT>
 __global__ void __launch_bounds__(256) k_pack_conv(const float* __restrict__ w, int Cin, int Cout, int K,
                                                    int transposed, int u, int taps, int nchunks, int N, int Np,
-                                                   MT* out) {
+                                                   MT* out, MT* out_lo) {
   const size_t total = (size_t)nchunks * taps * 32 * Np;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
@@ -637,6 +637,7 @@ __global__ void __launch_bounds__(256) k_pack_conv(const float* __restrict__ w, 
     }
   }
   out[i] = (MT)val;
+  if (out_lo) out_lo[i] = (MT)(val - (float)(MT)val);  // ST_SPLIT: the bf16 rounding residual (exact in fp32)
 }
 
 
@@ -969,10 +970,13 @@ int st_pack_conv(const float* w, int Cin, int Cout, int K, int transposed, int u
   dim3 grid((unsigned)((total + 255) / 256));
   if (dtype == ST_FP32)
     hipLaunchKernelGGL(k_pack_conv<float>, grid, dim3(256), 0, s, w, Cin, Cout, K, transposed, u, taps, nchunks, N, Np,
-                       reinterpret_cast<float*>(out));
+                       reinterpret_cast<float*>(out), (float*)nullptr);
   else if (dtype == ST_BF16)
     hipLaunchKernelGGL(k_pack_conv<bf16_t>, grid, dim3(256), 0, s, w, Cin, Cout, K, transposed, u, taps, nchunks, N,
-                       Np, reinterpret_cast<bf16_t*>(out));
+                       Np, reinterpret_cast<bf16_t*>(out), (bf16_t*)nullptr);
+  else if (dtype == ST_SPLIT)  // bf16 layout, the hi parts then the lo parts (same bytes as fp32)
+    hipLaunchKernelGGL(k_pack_conv<bf16_t>, grid, dim3(256), 0, s, w, Cin, Cout, K, transposed, u, taps, nchunks, N,
+                       Np, reinterpret_cast<bf16_t*>(out), reinterpret_cast<bf16_t*>(out) + total);
   else
     return ST_EDTYPE;
   return (int)hipGetLastError();

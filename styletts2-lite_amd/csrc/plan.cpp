@@ -57,7 +57,7 @@ struct WConv {
   int rs = -1, src_rows = 0;
   size_t bias_aux = 0;
   bool aux_bias = false;
-  size_t off[2] = {0, 0};
+  size_t off[ST_NDTYPES] = {0, 0, 0};
   // fold > 1: a stride-`fold` conv (padding fpad0) packed as the stride-1 conv over phase-folded frames
   // (fold consecutive input rows side by side): fold Cin channels, fK taps, padding fpad (k_fold_w)
   int fold = 0, fpad0 = 0, fK = 0, fpad = 0;
@@ -172,10 +172,10 @@ struct stts_model {
   std::vector<WConv*> convs;
   std::vector<Small*> smalls;
   std::vector<AdainBlk*> pools;
-  size_t conv_bytes[2] = {0, 0};
-  size_t aux_off[2] = {0, 0}, aux_bytes = 0, scratch_off[2] = {0, 0}, scratch_bytes = 0;
-  size_t total_bytes[2] = {0, 0};
-  const char* packed[2] = {nullptr, nullptr};
+  size_t conv_bytes[ST_NDTYPES] = {0, 0, 0};
+  size_t aux_off[ST_NDTYPES] = {0, 0, 0}, aux_bytes = 0, scratch_off[ST_NDTYPES] = {0, 0, 0}, scratch_bytes = 0;
+  size_t total_bytes[ST_NDTYPES] = {0, 0, 0};
+  const char* packed[ST_NDTYPES] = {nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -524,8 +524,8 @@ void finalize_layout(Model& m) {
     a->hoff = m.Htot;
     m.Htot += 2 * a->C;
   }
-  for (int dt = 0; dt < 2; ++dt) {
-    const size_t esz = dt == ST_FP32 ? 4 : 2;
+  for (int dt = 0; dt < ST_NDTYPES; ++dt) {
+    const size_t esz = dt == ST_BF16 ? 2 : 4;  // ST_SPLIT: bf16 hi + lo
     size_t off = 0;
     for (auto* c : m.convs) {
       c->off[dt] = off;
@@ -559,7 +559,7 @@ void finalize_layout(Model& m) {
     if (c->fold) sc = std::max(sc, rup((size_t)c->Cin * c->Cout * c->K * 4, ALIGN) + (size_t)c->pCin() * c->Cout * c->fK * 4);
   }
   m.scratch_bytes = rup(sc, ALIGN);
-  for (int dt = 0; dt < 2; ++dt) {
+  for (int dt = 0; dt < ST_NDTYPES; ++dt) {
     m.aux_off[dt] = m.conv_bytes[dt];
     m.scratch_off[dt] = m.aux_off[dt] + m.aux_bytes;
     m.total_bytes[dt] = m.scratch_off[dt] + m.scratch_bytes;
@@ -578,7 +578,7 @@ static int g_opt_stats_slots = 0;  // STTS_OPT_STATS_SLOTS (0 = automatic)
 
 struct Ctx {
   Model* m;
-  int dtype;
+  int dtype;  // activation storage (ST_FP32 in the split accuracy mode)
   size_t esz;
   int B;
   hipStream_t s;
@@ -601,6 +601,7 @@ struct Ctx {
   float* H = nullptr;
   const char* packed;
   char* aux;
+  int cdtype = 0;  // conv engines / packed weights: the run's dtype (ST_SPLIT in the accuracy mode)
 
   char* alloc(size_t bytes) {
     char* p = dry ? nullptr : ws + off;
@@ -620,7 +621,7 @@ struct Ctx {
     stats_off += rup((size_t)slots * B * C * 2 * sizeof(double), ALIGN);
     return p;
   }
-  const void* wpk(const WConv& c) const { return packed + c.off[dtype]; }
+  const void* wpk(const WConv& c) const { return packed + c.off[cdtype]; }
   const float* aux_f(size_t o) const { return reinterpret_cast<const float*>(aux + o); }
   const float* P(int i) const { return m->P[i]; }
 };
@@ -719,7 +720,7 @@ int conv_run(Ctx& c, ConvParams& p) {
   if (prof) ST_CHECK(prof_begin(c));
   p.stats_slots = p.stats ? c.slots : 1;
   p.stats_slot_bs = (long long)c.B * p.stats_ld * 2;
-  int r = st_conv1d(p, c.dtype, c.s);
+  int r = st_conv1d(p, c.cdtype, c.s);
   if (r) return r;
   // statistics slots are summed by the consumers' prologues (adain_coeffs): no fold launch
   if (prof) {
@@ -730,7 +731,7 @@ int conv_run(Ctx& c, ConvParams& p) {
     const double outs = (p.y ? 1 : 0) + (p.res ? 1 : 0) + (p.accb ? 1 : 0);
     double elems = (double)p.B * ((double)p.Lin * p.Cin + (double)p.Lout * p.Cout * outs);
     const double by = elems * c.esz + (p.y_f32 ? (double)p.B * p.Lout * p.Cout * (4.0 - c.esz) : 0.0);
-    const int flags = (p.res ? 1 : 0) | (p.accb ? 2 : 0) | (st_conv1d_engine(p, c.dtype) << 4);
+    const int flags = (p.res ? 1 : 0) | (p.accb ? 2 : 0) | (st_conv1d_engine(p, c.cdtype) << 4);
     ST_CHECK(prof_end(c, {p.B, p.Lq, p.N, p.Cin, p.KS, p.dil, p.Lout, flags}, fl, by));
   }
   return 0;
@@ -1035,6 +1036,10 @@ int decoder_forward(Ctx& c, const DecIO& io) {
       Cs[s] = m.init_ch >> (s + 1);
       smax = std::max(smax, (long long)Ls[s] * Cs[s]);
     }
+  }
+  if (c.cdtype == ST_SPLIT) {  // the fp32 partials of the two-pass C = 64 split resblock convs (ressplit.hip)
+    c.splitk_elems = (long long)B * smax;
+    c.splitk = reinterpret_cast<float*>(c.alloc((size_t)B * smax * 4));
   }
   Buf G[6];
   for (int i = 0; i < 6; ++i) {
@@ -1546,8 +1551,10 @@ int check_params(const Model& m) {
 
 template <typename F>
 int with_ctx(Model* m, int dtype, int B, void* ws, long long ws_bytes, void* stream, F&& body, size_t* need) {
-  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
-  Ctx c{m, dtype, (size_t)(dtype == ST_FP32 ? 4 : 2), B, (hipStream_t)stream, true, nullptr};
+  if (dtype != ST_FP32 && dtype != ST_BF16 && dtype != ST_SPLIT) return ST_EDTYPE;
+  const int adt = dtype == ST_BF16 ? ST_BF16 : ST_FP32;  // activation storage
+  Ctx c{m, adt, (size_t)(adt == ST_FP32 ? 4 : 2), B, (hipStream_t)stream, true, nullptr};
+  c.cdtype = dtype;
   c.slots = g_opt_stats_slots > 0 ? g_opt_stats_slots : (B <= 4 ? 16 : (B <= 16 ? 4 : 1));  // tools/slots_sweep.py
   c.packed = m->packed[dtype];
   c.aux = m->packed[dtype] ? const_cast<char*>(m->packed[dtype]) + m->aux_off[dtype] : nullptr;
@@ -1562,7 +1569,8 @@ int with_ctx(Model* m, int dtype, int B, void* ws, long long ws_bytes, void* str
   if (!m->packed[dtype]) return ST_ENOTPACKED;
   if ((long long)total > ws_bytes || !ws) return ST_EWORKSPACE;
   const size_t stats_begin = c.stats_begin;
-  Ctx r{m, dtype, c.esz, B, (hipStream_t)stream, false, reinterpret_cast<char*>(ws)};
+  Ctx r{m, adt, c.esz, B, (hipStream_t)stream, false, reinterpret_cast<char*>(ws)};
+  r.cdtype = dtype;
   r.slots = c.slots;
   r.packed = c.packed;
   r.aux = c.aux;
@@ -1619,19 +1627,19 @@ long long stts_param_numel(const stts_model* m, int i) {
 int stts_set_param(stts_model* m, int i, const float* p) {
   if (!m || i < 0 || i >= (int)m->P.names.size()) return ST_EINVAL;
   m->P.ptr[i] = p;
-  m->packed[0] = m->packed[1] = nullptr;  // weights changed: repack required
+  for (auto& pk : m->packed) pk = nullptr;  // weights changed: repack required
   return 0;
 }
 
 long long stts_packed_bytes(const stts_model* m, int dtype) {
   if (!m) return ST_EINVAL;
-  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  if (dtype != ST_FP32 && dtype != ST_BF16 && dtype != ST_SPLIT) return ST_EDTYPE;
   return (long long)m->total_bytes[dtype];
 }
 
 int stts_pack(stts_model* m, int dtype, void* packed, long long bytes, void* stream) {
   if (!m || !packed) return ST_EINVAL;
-  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  if (dtype != ST_FP32 && dtype != ST_BF16 && dtype != ST_SPLIT) return ST_EDTYPE;
   if (bytes < (long long)m->total_bytes[dtype]) return ST_EWORKSPACE;
   ST_CHECK(check_params(*m));
   ST_CHECK(pack_model(*m, dtype, reinterpret_cast<char*>(packed), (hipStream_t)stream));
@@ -1860,6 +1868,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_PLAINRC: g_opt_plainrc = value ? 1 : 0; return 0;
     case STTS_OPT_MSDFOLD: g_opt_msdfold = value ? 1 : 0; return 0;
     case STTS_OPT_RCPP: g_opt_rcpp = (value >= 0 && value <= 2) ? value : 1; return 0;
+    case STTS_OPT_RESSPLIT: g_opt_ressplit = value ? 1 : 0; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1889,6 +1898,7 @@ int stts_get_option(int key) {
     case STTS_OPT_PLAINRC: return g_opt_plainrc;
     case STTS_OPT_MSDFOLD: return g_opt_msdfold;
     case STTS_OPT_RCPP: return g_opt_rcpp;
+    case STTS_OPT_RESSPLIT: return g_opt_ressplit;
     default: return ST_EINVAL;
   }
 }

@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 KIND_HIFIGAN, KIND_ISTFTNET, KIND_F0N, KIND_STYLE, KIND_MPD, KIND_VOCOS, KIND_MSD = 0, 1, 2, 3, 4, 5, 6
-DTYPES = {"fp32": 0, "bf16": 1}
+DTYPES = {"fp32": 0, "bf16": 1, "bf16x3": 2}  # bf16x3: the split-operand accuracy mode (STTS_SPLIT)
 
 _LIB = None
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -171,11 +171,12 @@ OPT_WGRAD = 15
 OPT_PLAINRC = 16
 OPT_MSDFOLD = 17
 OPT_RCPP = 18
+OPT_RESSPLIT = 19
 # the production defaults of every STTS_OPT_* (include/stts2.h)
 OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
                 OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1, OPT_SKEW: 0, OPT_FRONT: 1, OPT_PW: 1, OPT_SPLITK: 1,
                 OPT_EXP: 0, OPT_UPS: 1, OPT_WGRAD: 1, OPT_PLAINRC: 1, OPT_MSDFOLD: 1,
-                OPT_RCPP: 1}
+                OPT_RCPP: 1, OPT_RESSPLIT: 1}
 
 
 def set_option(key: int, value: int) -> None:
@@ -606,7 +607,7 @@ def profile_read():
 
 
 ENGINE_KERNELS = ("conv1d_igemm_kernel", "k_resconv", "k_bigconv", "k_resfused", "k_conv_post",
-                  "k_pwgemm")  # engine ids 0..5
+                  "k_pwgemm", "k_ressplit", "?")  # engine ids 0..6
 
 
 def profile_launches():

@@ -22,14 +22,15 @@ def predictor():
 
 
 @pytest.mark.parametrize("T,B", [(8, 2), (40, 1)])
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
 def test_f0n_convstacks(T, B, dtype):
     pp = predictor()
     g = golden(f"f0n_T{T}_B{B}")
     s = torch.from_numpy(np.stack([synth.normal(f"f0n:s:{b}", (128,)) for b in range(B)])).cuda()
     xl = torch.from_numpy(g["tap_lstm"]).transpose(1, 2).contiguous().cuda()  # [B, T, 512]
     F0, N = pp.f0n_engine(dtype).forward_nlc(xl, s)
-    tol = 2e-4 if dtype == "fp32" else 0.1
+    tol = {"fp32": 2e-4, "bf16x3": 5e-4}.get(dtype, 0.1)  # bf16x3: the split accuracy mode
+    print(f"f0n T={T} {dtype}: F0 {np.abs(F0.cpu().numpy() - g['F0']).max():.3e} N {np.abs(N.cpu().numpy() - g['N']).max():.3e}")
     assert np.abs(F0.cpu().numpy() - g["F0"]).max() < tol
     assert np.abs(N.cpu().numpy() - g["N"]).max() < tol
 

@@ -17,7 +17,7 @@ def _inference():
 
 
 @pytest.mark.parametrize("Fr,B", [(80, 2), (241, 1)])
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
 def test_style_encoder(Fr, B, dtype):
     from stts2_mi355x.models import StyleEncoder
     se = fill_module(StyleEncoder(dim_in=64, style_dim=128, max_conv_dim=512)).eval().cuda()
@@ -27,4 +27,4 @@ def test_style_encoder(Fr, B, dtype):
     err = np.abs(out - ref).max()
     scale = np.abs(ref).max()
     print(f"style F={Fr} {dtype}: max-abs {err:.3e} (ref absmax {scale:.3f})")
-    assert err < (1e-4 if dtype == "fp32" else 0.05 * scale)
+    assert err < {"fp32": 1e-4, "bf16x3": 2e-4}.get(dtype, 0.05 * scale)  # bf16x3: the split accuracy mode

@@ -41,7 +41,7 @@ def main():
     dec = dec.to(dev)
     B = int(os.environ.get("PHASE_B", "32"))
     args = tuple(torch.from_numpy(x).to(dev) for x in synth.decoder_inputs(B, 400))
-    eng = dec.engine("bf16")
+    eng = dec.engine(os.environ.get("PHASE_DT", "bf16"))
     modes = [int(m) for m in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2, 4, 3, 6, 7]
     kernels = ("k_bigconv",) if "bigconv" in sys.argv else ("conv1d_igemm_kernel",) if "igemm" in sys.argv \
         else ("k_resconv", "k_bigconv")
