@@ -150,8 +150,8 @@ int stts_mrstft_loss(const float* x, const float* y, int B, long long L, long lo
  * channel-transposed, tap-reversed weight and padding dil (K - 1) - pad; of a strided conv (dil 1) = the
  * polyphase ConvTranspose1d of dy); dw / db always compute in fp32 (f32 MFMA over (utterance, frame)
  * row slices, fp64 fixed-order slice sums: deterministic).  dx, dw, db may each be null.
- * The forward entries (stts_conv1d_fwd / _res / _act) also take STTS_SPLIT (fp32 frames, split-operand MFMA);
- * the backward takes STTS_FP32 / STTS_BF16.
+ * Every entry also takes STTS_SPLIT (fp32 frames; y and dx with split-operand MFMA, bf16 hi + lo, three MFMAs;
+ * dw / db in fp32 as for STTS_FP32).  stts_conv_transpose1d_* likewise.
  * Workspace >= the matching *_workspace_bytes. */
 long long stts_conv1d_fwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride, int dil,
                                           int pad, int Lq);
@@ -369,7 +369,9 @@ const char* stts_error_string(int code);
  *                     batches) and for C = 128 with 7 / 11 taps; C = 128 with 3 taps on bigconv.hip
  *                     (measured faster); 1 =
  *                     bigconv.hip everywhere; 3 = bigconv2.hip, 4-wave blocks; 4 = bigconv2.hip,
- *                     8-wave blocks (A/B, tests). */
+ *                     8-wave blocks (A/B, tests); 5 = as 2, but C = 256 on 8-wave blocks whose second half runs
+ *                     one 32-channel group behind the first (three window buffers), so the two waves of a SIMD
+ *                     reach their tile epilogues a group apart. */
 #define STTS_OPT_BIGCONV 7
 /*   STTS_OPT_HEAD     1 (default) = the HiFi-GAN output head (Snake -> conv_post -> tanh) runs as one
  *                     streaming pass (head.hip); 0 = on the igemm engine (A/B). */
@@ -417,6 +419,10 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_RESSPLIT 1 (default) = the accuracy mode's (STTS_SPLIT) C = 32 / 64 resblock convs run on the split
  *                     resblock engine (ressplit.hip; C = 64 in two input-channel passes); 0 = conv1d_igemm (A/B). */
 #define STTS_OPT_RESSPLIT 19
+/*   STTS_OPT_BF16F    1 (default) = bf16 training-step convs (stts_conv1d_fwd / _bwd dx) that run on the general engine
+ *                     read and write the caller's fp32 frames directly, rounding the window to bf16 while staging it;
+ *                     0 = fp32 -> bf16 frame conversion before and bf16 -> fp32 after each such conv (A/B). */
+#define STTS_OPT_BF16F 20
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

@@ -38,8 +38,12 @@ enum { PK_SNAKE = 0, PK_LRELU = 1 };
 // C = N = u Cout columns, tap t reads input row q + t - 1 (left pad 1); the epilogue maps GEMM
 // row q / column n to output frame q u + n / Cout - opad, channel n % Cout.
 // CO: channels of the bias / statistics arrays (C; Cout for UPS)
-template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C, bool UPS = false, int CO = C>
+// OFS: the second half of the waves (wu >= NW / 2) runs one group behind the first (3 window buffers), so the
+// two waves of each SIMD reach their tile epilogues one group apart and one's epilogue runs beside the other's
+// MFMAs (STTS_OPT_BIGCONV 5 / 6)
+template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C, bool UPS = false, int CO = C, bool OFS = false>
 struct B2 {
+  static constexpr int NXB = OFS ? 3 : 2;  // window buffers
   static constexpr int NCOEF = PRO == PK_SNAKE ? 5 : 2;  // coefficient rows per input channel
   static constexpr int NCBW = (C / 32 < NW) ? C / 32 : NW;  // 32-channel output blocks per block tile
   static constexpr int FH = NW / NCBW;   // frame halves per tile (waves per co block)
@@ -61,11 +65,11 @@ struct B2 {
   static constexpr int OFF_ST = OFF_BIAS + CO * 4;    // [CO][2] f32
   static constexpr int OFF_W = (OFF_ST + 2 * CO * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
   static constexpr int BPC = NW == 4 ? 2 : 1;                     // blocks per CU
-  static constexpr int PDMAX_LDS = ((160 * 1024 / BPC - OFF_W - 2 * WROWS * 64) / (NW * 2048)) - 1;
+  static constexpr int PDMAX_LDS = ((160 * 1024 / BPC - OFF_W - NXB * WROWS * 64) / (NW * 2048)) - 1;
   static constexpr int PD0 = PDMAX_LDS < K ? PDMAX_LDS : K;
   static constexpr int PD = PD0 < 5 ? PD0 : 5, RS = PD + 1;
-  static constexpr int OFF_X = OFF_W + NW * RS * 2048; // [2][WROWS][64 B]
-  static constexpr int LDS = OFF_X + 2 * WROWS * 64;
+  static constexpr int OFF_X = OFF_W + NW * RS * 2048; // [NXB][WROWS][64 B]
+  static constexpr int LDS = OFF_X + NXB * WROWS * 64;
   static_assert(FH * NCBW == NW && NCH * NCO == C, "wave grid");
   static_assert(LDS * BPC <= 160 * 1024, "LDS budget");
   static_assert(K >= PD && PD >= 2, "weight prefetch stays within one group");
@@ -165,9 +169,10 @@ __device__ __forceinline__ uint4 f32_to_bf8v(const float* v) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C>
+          bool UPS = false, int CO = C, bool OFS = false>
 __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
-  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS>;
+  constexpr int NXB = G::NXB;
   constexpr int TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
   constexpr int NCF = G::NCOEF;
   // input-channel groups: C / 32 for the square resblock convs, ceil(Cin / 32) for the front-end
@@ -242,7 +247,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     const Rsrc rx = make_rsrc(reinterpret_cast<const bf16_t*>(p.x) + (size_t)b * p.x_bs,
                               (unsigned)((size_t)p.Lin * p.x_ld * 2));
     const int gr0 = mt * TM - G::PAD;
-    char* dst = smem + G::OFF_X + (gg & 1) * (G::WROWS * 64);
+    char* dst = smem + G::OFF_X + (gg % NXB) * (G::WROWS * 64);
 #pragma unroll
     for (int j = 0; j < NWIN; ++j) {
       const int pidx = (j * NW + wu) * 64 + lane;
@@ -288,7 +293,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     if (dbg & 1) return;
     const int gr0 = mt * TM - G::PAD;
     const float* cf = coef + (b & 1) * NCF * CINP + gi * 32 + 8 * my_u;
-    char* buf = smem + G::OFF_X + (gg & 1) * (G::WROWS * 64);
+    char* buf = smem + G::OFF_X + (gg % NXB) * (G::WROWS * 64);
     if constexpr (PRO == PK_LRELU) {
     // (in chunks of at most 3 units: C = 128's 5 units at once spill)
     constexpr int JC = NWIN < 3 ? NWIN : 3;
@@ -511,7 +516,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     asm volatile("" : "+v"(l));
     const int r0 = fh * 256 + l + t * DIL;
     u = ((2 * half + hi) ^ ((r0 >> 2) & 3)) * 16;  // rows r0 + 32 f share the swizzle
-    return smem + G::OFF_X + (gg & 1) * (G::WROWS * 64) + r0 * 64;
+    return smem + G::OFF_X + (gg % NXB) * (G::WROWS * 64) + r0 * 64;
   };
   auto rd_b = [&](bf16x8 (&fb)[8], int gg, int t, int half) __attribute__((always_inline)) {
     int u;
@@ -569,55 +574,82 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       for (int r = 0; r < 16; ++r) acc[f][r] = bb[r];
   };
 
-  // ---------------- main loop: one iteration per 32-channel group; K taps unrolled
+  // ---------------- main loop: one iteration (slot) per 32-channel group; K taps unrolled.  In slot sl every wave
+  // DMAs and transforms its share of window sl + 1; a wave computes group gw = sl - off (OFS: off = 1 for the
+  // second half of the waves, which so runs one slot behind on window buffers sl - 1; one extra slot at the end)
   init_acc(cur.ch);
   // STTS_OPT_EXP bit 1: static MFMA-issue priority for the second-dispatched half of the waves
   // (MI355X_MICROARCH.md, two waves per SIMD, item 4)
   if ((p.exp & 1) && wu >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  for (int gg = 0; gg < NGG; ++gg) {
+  const int off = (OFS && wu >= NW / 2) ? 1 : 0;
+  constexpr int XS = OFS ? 1 : 0;  // extra slots
+  GCur prv = cur;  // the group of the previous slot (the lagging half's compute group)
+  for (int sl = 0; sl < NGG + XS; ++sl) {
     lap(6);
-    if (!(dbg & 32)) barrier_lds();  // group gg's window transformed by every wave; group gg-1's reads all done
+    if (!(dbg & 32)) barrier_lds();  // window sl transformed by every wave; its reads of two slots back all done
     lap(2);
-    if (gg > 0) cur = advance(cur);
+    if (sl > 0) {
+      prv = cur;
+      if (sl < NGG) cur = advance(cur);
+    }
     // the next group (past the end: the last group again, a harmless reload keeping counts uniform)
-    const GCur nxt = gg + 1 < NGG ? advance(cur) : cur;
-    const int gi = cur.gi, tt = cur.tt;
-    if (gi == 0) {
-      const int b = cur.b;
-      if (b != cur_b) {  // the block left utterance cur_b: every epilogue of it ran >= 1 barrier ago
+    const GCur nxt = sl + 1 < NGG ? advance(cur) : cur;
+    const int gw = sl - off;            // this wave's compute group
+    const bool active = gw >= 0 && gw < NGG;
+    const GCur me = off ? prv : cur;    // its cursor, and the group after it
+    const GCur mnx = off ? cur : nxt;
+    const int gi = me.gi;
+    // utterance bookkeeping on the lagging half's cursor: it closes a tile one slot after the leading half, so
+    // every epilogue of an utterance has run >= 1 barrier before this (OFS = false: both are `cur`)
+    const GCur lag = OFS ? prv : cur;
+    if (lag.gi == 0 && sl >= XS) {
+      const int b = lag.b;
+      if (b != cur_b) {  // the block left utterance cur_b
         if (want_stats) flush(cur_b);
         cur_b = b;
       }
-      // the next tile opens another utterance: its coefficients, first read by the transform of its
-      // group 0 during this tile's last group, >= 1 barrier from here (NG >= 4)
-      if (tt + 1 < tend && cur.mt == ntm - 1 && cur.ch == NCH - 1) set_coef(b + 1);
     }
-    issue_x(gg + 1, nxt.gi, nxt.b, nxt.mt);  // buffer (gg+1)&1, whose last reads were group gg-1's
-    // this wave's weights of step gg K: younger VMEM ops are the weight DMAs of the next PD - 1 steps
+    if (cur.gi == 0 && sl < NGG) {
+      // the next tile opens another utterance: its coefficients, first read by the transform of its group 0
+      // during this tile's last group, >= 1 barrier from here (NG >= 4)
+      if (cur.tt + 1 < tend && cur.mt == ntm - 1 && cur.ch == NCH - 1) set_coef(cur.b + 1);
+    }
+    // (the extra slot re-issues a harmless window DMA, untransformed and never read, so that every slot's
+    // vmcnt waits count the same younger operations)
+    const bool windows = sl < NGG;
+    issue_x(sl + 1, nxt.gi, nxt.b, nxt.mt);  // buffer (sl+1) % NXB, last read NXB - 1 slots ago
+    if (!active) {  // the lagging half's first slot: only its share of window 1
+      if (windows) {
+        vm_wait<0>();
+        transform(sl + 1, nxt.gi, nxt.b, nxt.mt);
+      }
+      continue;
+    }
+    // this wave's weights of step gw K: younger VMEM ops are the weight DMAs of the next PD - 1 steps
     // and the window DMAs just issued
     // (in the group after an epilogue, that epilogue's NST stores are younger too: counted, so the
     // wait does not also drain the stores' write acknowledgements)
-    const bool post_epi = gi == 0 && gg > 0;
+    const bool post_epi = gi == 0 && gw > 0;
     lap(6);
     if (post_epi) vm_wait<2 * (PD - 1) + NWIN + NST>();
     else vm_wait<2 * (PD - 1) + NWIN>();
     lap(0);
-    rd_a(gg * K, fa[0]);
-    rd_b(fb0, gg, 0, 0);
+    rd_a(gw * K, fa[0]);
+    rd_b(fb0, gw, 0, 0);
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-      const int s = gg * K + t;
+      const int s = gw * K + t;
       // into slot (s+PD) % RS = (s-1) % RS, whose fragments tap s-1 consumed; step s+PD is tap
       // t+PD of this group or tap t+PD-K of the next (PD <= K)
-      if (t + PD < K) issue_w(s + PD, gi, cur.ch, t + PD);
-      else if (gg + 1 < NGG) issue_w(s + PD, nxt.gi, nxt.ch, t + PD - K);
-      else issue_w(s + PD, gi, cur.ch, K - 1);
+      if (t + PD < K) issue_w(s + PD, gi, me.ch, t + PD);
+      else if (gw + 1 < NGG) issue_w(s + PD, mnx.gi, mnx.ch, t + PD - K);
+      else issue_w(s + PD, gi, me.ch, K - 1);
       {
         const bf16x8(&a)[2] = fa[t & 1];
         // half 0 of tap t; reads of half 1
         {
           int u;
-          const char* row = brow(gg, t, 1, u);
+          const char* row = brow(gw, t, 1, u);
 #pragma unroll
           for (int f = 0; f < 8; ++f) {
             acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], fb0[f], acc[f], 0, 0, 0);
@@ -628,7 +660,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
         // half 1 of tap t; reads of half 0 of tap t+1 and, once its DMA is in, of its weights
         if (t + 1 < K) {
           int u;
-          const char* row = brow(gg, t + 1, 0, u);
+          const char* row = brow(gw, t + 1, 0, u);
 #pragma unroll
           for (int f = 0; f < 4; ++f) {
             acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb1[f], acc[f], 0, 0, 0);
@@ -636,7 +668,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           }
           interleave(4);
           // weights of step s+1: younger VMEM ops are the weight DMAs of steps s+2..s+PD and, while
-          // step s+1 precedes this group's window DMAs (t + 1 < PD), those
+          // step s+1 precedes this slot's window DMAs (t + 1 < PD), those
           lap(6);
           if (t + 1 < PD) {
             if (post_epi) vm_wait<2 * (PD - 1) + NWIN + NST>();
@@ -657,24 +689,24 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb1[f], acc[f], 0, 0, 0);
         }
       }
-      // the next group's window: this wave's DMAs of it are older than the weight DMAs of taps
-      // 0..t.  With two waves per SIMD (NW = 8) the second half transforms one tap earlier, so each
-      // SIMD's transforms run beside its partner's MFMAs instead of beside each other
+      // the next window: this wave's DMAs of it are older than the weight DMAs of taps 0..t.  With two
+      // waves per SIMD (NW = 8) the second half transforms one tap earlier, so each SIMD's transforms run
+      // beside its partner's MFMAs instead of beside each other
       constexpr int TX = K - 1;
       constexpr int TX2 = (NW == 8) ? K - 2 : K - 1;
-      if ((t == TX && (NW != 8 || wu < 4)) || (t == TX2 && NW == 8 && wu >= 4)) {
+      if (windows && ((t == TX && (NW != 8 || wu < 4)) || (t == TX2 && NW == 8 && wu >= 4))) {
         lap(6);
         if (t == K - 1) vm_wait<2 * K>();
         else vm_wait<2 * (K - 1)>();
         lap(1);
-        transform(gg + 1, nxt.gi, nxt.b, nxt.mt);
+        transform(sl + 1, nxt.gi, nxt.b, nxt.mt);
         lap(3);
       }
     }
     if (gi == NG - 1) {
       lap(6);
-      if (!(dbg & 4)) epilogue(cur.b, cur.mt, cur.ch);
-      init_acc(nxt.ch);
+      if (!(dbg & 4)) epilogue(me.b, me.mt, me.ch);
+      init_acc(mnx.ch);
       lap(4);
     }
   }
@@ -691,10 +723,10 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C>
+          bool UPS = false, int CO = C, bool OFS = false>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
-  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -717,29 +749,30 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-template <int C, int NW, int K>
+template <int C, int NW, int K, bool OFS = false>
 int launch_b2_k(const ConvParams& p, hipStream_t s) {
   if (!p.res) {  // conv1 of an iteration: dilation 1 / 3 / 5, no residual
     if (p.accb) return ST_EINVAL;
     switch (p.dil) {
-      case 1: return launch_b2<C, NW, K, 1, false, false>(p, s);
-      case 3: return launch_b2<C, NW, K, 3, false, false>(p, s);
-      case 5: return launch_b2<C, NW, K, 5, false, false>(p, s);
+      case 1: return launch_b2<C, NW, K, 1, false, false, PK_SNAKE, C, false, false, C, OFS>(p, s);
+      case 3: return launch_b2<C, NW, K, 3, false, false, PK_SNAKE, C, false, false, C, OFS>(p, s);
+      case 5: return launch_b2<C, NW, K, 5, false, false, PK_SNAKE, C, false, false, C, OFS>(p, s);
       default: return ST_EINVAL;
     }
   }
   if (p.dil != 1) return ST_EINVAL;  // conv2: dilation 1, residual, optionally the resblock sum
-  if (p.accb) return launch_b2<C, NW, K, 1, true, true>(p, s);
-  return (g_opt_exp & 2) ? launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, true>(p, s)
-                         : launch_b2<C, NW, K, 1, true, false>(p, s);
+  if (p.accb) return launch_b2<C, NW, K, 1, true, true, PK_SNAKE, C, false, false, C, OFS>(p, s);
+  if constexpr (!OFS)
+    if (g_opt_exp & 2) return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, true>(p, s);
+  return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, false, false, C, OFS>(p, s);
 }
 
-template <int C, int NW>
+template <int C, int NW, bool OFS = false>
 int launch_b2_c(const ConvParams& p, hipStream_t s) {
   switch (p.KS) {
-    case 3: return launch_b2_k<C, NW, 3>(p, s);
-    case 7: return launch_b2_k<C, NW, 7>(p, s);
-    case 11: return launch_b2_k<C, NW, 11>(p, s);
+    case 3: return launch_b2_k<C, NW, 3, OFS>(p, s);
+    case 7: return launch_b2_k<C, NW, 7, OFS>(p, s);
+    case 11: return launch_b2_k<C, NW, 11, OFS>(p, s);
     default: return ST_EINVAL;
   }
 }
@@ -757,7 +790,7 @@ bool st_bigconv2_eligible(const ConvParams& p) {
   if (p.res ? p.dil != 1 : (p.accb != nullptr)) return false;
   // mode 2 (default) keeps v1 where it measured faster: C = 128 with 3 taps (12 taps per tile, so
   // the per-tile window transform and epilogue dominate; profiles/r02_ab_bigconv_pipelined.txt)
-  if (g_opt_bigconv == 2 && p.Cout == 128 && p.KS == 3) return false;  // (modes 3 / 4: v2 everywhere)
+  if ((g_opt_bigconv == 2 || g_opt_bigconv == 5) && p.Cout == 128 && p.KS == 3) return false;  // (modes 3 / 4: v2 everywhere)
   return true;  // on top of st_bigconv_eligible
 }
 
@@ -804,6 +837,9 @@ int st_bigconv2_front(const ConvParams& p, hipStream_t s) {
 
 
 int st_bigconv2(const ConvParams& p, hipStream_t stream) {
+  // STTS_OPT_BIGCONV 5: C = 256 on 8-wave blocks with the second half one group behind (OFS; a third window
+  // buffer: C = 128's 512-row windows leave no room for it), the mode-2 choice elsewhere
+  if (g_opt_bigconv == 5 && p.Cout == 256) return launch_b2_c<256, 8, true>(p, stream);
   // mode 3, or mode 2 with fewer 8-wave tiles than CUs (small batches: B = 1 at C = 256 has 32):
   // 4-wave blocks, two per CU, twice the tiles (profiles/r02_ab_b1.txt: C = 256 k11 75 -> 61 us)
   const int tm8 = p.Cout == 128 ? 512 : 256;
@@ -813,7 +849,7 @@ int st_bigconv2(const ConvParams& p, hipStream_t stream) {
   // the other's MFMAs, 371 -> 346 us (k7 conv1) and 445 -> 404 us (k7 conv2) at B = 32, while C = 256
   // and C = 128 k3 are faster with 8-wave blocks / v1 (profiles/r02_ab_bigconv_modes.txt)
   const bool two = g_opt_bigconv == 3 ||
-                   (g_opt_bigconv == 2 && (tiles8 < b2_num_cu() || (p.Cout == 128 && p.KS >= 7)));
+                   ((g_opt_bigconv == 2 || g_opt_bigconv == 5) && (tiles8 < b2_num_cu() || (p.Cout == 128 && p.KS >= 7)));
   if (p.Cout == 128) return two ? launch_b2_c<128, 4>(p, stream) : launch_b2_c<128, 8>(p, stream);
   if (p.Cout == 256) return two ? launch_b2_c<256, 4>(p, stream) : launch_b2_c<256, 8>(p, stream);
   return ST_EINVAL;

@@ -15,6 +15,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // multiplied as hi*hi + hi*lo + lo*hi on the bf16 MFMA (fp32 accumulation)
 enum StDtype { ST_FP32 = 0, ST_BF16 = 1, ST_SPLIT = 2 };
 constexpr int ST_NDTYPES = 3;
+// internal (not a C-ABI dtype): bf16 MFMA operands staged from fp32 frames, fp32 outputs (the training
+// step's convs on the general engine: no frames conversion passes around them)
+constexpr int ST_BF16F = 3;
 
 // domain error codes (negative; positive values are hipError_t)
 enum StStatus {

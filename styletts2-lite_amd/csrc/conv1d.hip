@@ -46,12 +46,14 @@ template <> struct Layout<float> {
   static constexpr int WP = 0;   // W: [tap][k][BN]
 };
 
-template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN>
+// SPF: with fp32 frames on the bf16 MFMA path (T = float, MT = bf16), true = the split accuracy mode,
+// false = plain bf16 operands converted while staging (ST_BF16F: the training step's fp32 frames)
+template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool SPF = true>
 struct ConvCfg {
   static constexpr bool BF = std::is_same<MT, bf16_t>::value;
   // ST_SPLIT (accuracy mode): fp32 activations on the bf16 MFMA path, every window and weight slice
   // staged twice (hi, lo) and multiplied as hi*hi + hi*lo + lo*hi
-  static constexpr bool SPLIT = BF && std::is_same<T, float>::value;
+  static constexpr bool SPLIT = BF && std::is_same<T, float>::value && SPF;
   static constexpr bool LOWP = BF && !SPLIT;  // the bf16 throughput mode's shortcuts (v_sin, reciprocal)
   static constexpr int SPL = SPLIT ? 2 : 1;
   static constexpr int NW = WAVES_M * WAVES_N;
@@ -78,9 +80,9 @@ struct ConvCfg {
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
-// bf16: at least 2 waves per SIMD (<= 256 VGPRs); fp32 (parity mode) and the split accuracy mode (fp32
-// windows, hi + lo fragments) keep their registers on 4-wave tiles
-template <typename T, typename MT>
+// bf16 frames: at least 2 waves per SIMD (<= 256 VGPRs); fp32 frames (the parity mode, the split accuracy
+// mode, ST_BF16F) keep their registers (fp32 window prefetch sets) on 4-wave tiles
+template <typename T, typename MT, bool SPF>
 constexpr int kMinWaves = (std::is_same<MT, bf16_t>::value && std::is_same<T, bf16_t>::value) ? 2 : 1;
 
 // 16 values <-> 8 packed pairs
@@ -96,10 +98,10 @@ __device__ __forceinline__ void pw(float (&v)[16], int i, f2v x) {
 // 16*((m>>2)&1) + (m&3) + 4*(m>>3)), 16 CONSECUTIVE channels 16*(lane>>5) + r.  The epilogue
 // therefore works straight from registers: no LDS transpose, 16-channel vector loads/stores,
 // and per-lane statistics accumulated across tiles (reduced across lanes once per utterance).
-template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW, int CPS>
-__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT>))
+template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW, int CPS, bool SPF = true>
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>))
     conv1d_igemm_kernel(const ConvParams p) {
-  using C = ConvCfg<T, MT, WAVES_M, WAVES_N, WM, WN>;
+  using C = ConvCfg<T, MT, WAVES_M, WAVES_N, WM, WN, SPF>;
   constexpr int BM = C::BM, BN = C::BN, XP = C::XP, WPITCH = C::WPITCH, W_TAP = C::W_TAP, NT = C::NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -760,9 +762,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT>))
 
 int g_num_cu = 0;
 
-template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW = false>
+template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW = false, bool SPF = true>
 int launch_cfg(ConvParams p, hipStream_t stream) {
-  using C = ConvCfg<T, MT, WAVES_M, WAVES_N, WM, WN>;
+  using C = ConvCfg<T, MT, WAVES_M, WAVES_N, WM, WN, SPF>;
   constexpr int LDS_MAX = 160 * 1024;
   constexpr int WBUDGET = 48 * 1024;
   constexpr int WRES_BUDGET = 120 * 1024;
@@ -791,10 +793,10 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
     p.cps = 2;
   const size_t lds = C::lds_bytes(p, p.w_resident ? nres : p.cps * p.tg, p.cps);
   if (lds > (size_t)LDS_MAX) return ST_EINVAL;
-  auto kern1 = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 1>;
+  auto kern1 = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 1, SPF>;
   auto kern = kern1;
   if constexpr (C::LOWP && !NARROW) {
-    if (p.cps == 2) kern = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 2>;
+    if (p.cps == 2) kern = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 2, SPF>;
   }
   static bool attr_set[2] = {false, false};
   if (!attr_set[p.cps - 1]) {
@@ -820,41 +822,41 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-template <typename T, typename MT>
+template <typename T, typename MT, bool SPF = true>
 int launch_typed(const ConvParams& p, hipStream_t stream) {
   const bool narrow = (p.Cout % 16 != 0) || p.y_f32 || (p.y_ld % 8 != 0) || (p.res && p.res_ld % 8 != 0) ||
                       (p.accb && p.acc_ld % 8 != 0);
   if (narrow) {
     // per-element epilogue: residual/scale/tanh supported; accumulate/reflect/zero-columns are not
     if (p.accb || p.reflect_front || p.zc_period || p.N > 32 || p.stride > 1) return ST_EINVAL;
-    return launch_cfg<T, MT, 4, 1, 2, 1, true>(p, stream);
+    return launch_cfg<T, MT, 4, 1, 2, 1, true, SPF>(p, stream);
   }
   if (p.epi_tanh) return ST_EINVAL;  // tanh only on narrow heads
   // stride 2 with N <= 32 (the MSD (3, 9) layers of the training step, N = 32): BM 128 x BN 32, every
   // column live, instead of the 64 x 128 tile with three quarters of its columns idle (STTS_OPT_EXP 1024:
   // the old tile, for A/B)
-  if constexpr (ConvCfg<T, MT, 1, 1, 1, 1>::LOWP) {
-    if (p.stride == 2 && p.N <= 32 && !(g_opt_exp & 1024)) return launch_cfg<T, MT, 4, 1, 1, 1>(p, stream);
+  if constexpr (ConvCfg<T, MT, 1, 1, 1, 1, SPF>::LOWP) {
+    if (p.stride == 2 && p.N <= 32 && !(g_opt_exp & 1024)) return launch_cfg<T, MT, 4, 1, 1, 1, false, SPF>(p, stream);
   }
-  if (p.stride > 1) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);  // BM 64 x BN 128 (short window)
+  if (p.stride > 1) return launch_cfg<T, MT, 2, 2, 1, 2, false, SPF>(p, stream);  // BM 64 x BN 128 (short window)
   if (p.N > 64 && g_opt_small_tiles) {
     // few tiles (small batches: the 400-frame front-end at B = 1 makes 16 tiles of 256 x 128 for 256
     // CUs): BM 64 x BN 128 tiles, 4x the workgroups
     const long long big = (long long)((p.N + 127) / 128) * ((p.Lq + 255) / 256) * p.B;
     const int ncu = g_num_cu ? g_num_cu : 256;
-    if (big < ncu / 2) return launch_cfg<T, MT, 2, 2, 1, 2>(p, stream);
+    if (big < ncu / 2) return launch_cfg<T, MT, 2, 2, 1, 2, false, SPF>(p, stream);
   }
-  if (p.N <= 32) return launch_cfg<T, MT, 4, 1, 2, 1>(p, stream);     // BM 256 x BN 32, 4 waves
-  if constexpr (!ConvCfg<T, MT, 1, 1, 1, 1>::LOWP) {
-    // fp32 (parity mode) and split: 4-wave tiles, so a wave may hold its fp32 windows and weight slices
-    // (split: hi and lo) in up to 512 registers (the 8-wave tiles are capped at 256 and spill)
-    if (p.N <= 64) return launch_cfg<T, MT, 2, 2, 2, 1>(p, stream);   // BM 128 x BN 64
-    return launch_cfg<T, MT, 2, 2, 2, 2>(p, stream);                  // BM 128 x BN 128
+  if (p.N <= 32) return launch_cfg<T, MT, 4, 1, 2, 1, false, SPF>(p, stream);     // BM 256 x BN 32, 4 waves
+  if constexpr (std::is_same<T, float>::value) {
+    // fp32 frames (parity mode, split, ST_BF16F): 4-wave tiles, so a wave may hold its fp32 windows and weight
+    // slices (split: hi and lo) in up to 512 registers (the 8-wave tiles are capped at 256 and spill)
+    if (p.N <= 64) return launch_cfg<T, MT, 2, 2, 2, 1, false, SPF>(p, stream);   // BM 128 x BN 64
+    return launch_cfg<T, MT, 2, 2, 2, 2, false, SPF>(p, stream);                  // BM 128 x BN 128
   } else {
     // BM 256 x BN 64, 8 waves.  (N = 192 keeps BN 128: the window prologue is paid per tile, so
     // three 64-column tiles measured slower than a half-empty 128-column one.)
-    if (p.N <= 64) return launch_cfg<T, MT, 8, 1, 1, 2>(p, stream);
-    return launch_cfg<T, MT, 4, 2, 2, 2>(p, stream);                  // BM 256 x BN 128, 8 waves
+    if (p.N <= 64) return launch_cfg<T, MT, 8, 1, 1, 2, false, SPF>(p, stream);
+    return launch_cfg<T, MT, 4, 2, 2, 2, false, SPF>(p, stream);                  // BM 256 x BN 128, 8 waves
   }
 }
 
@@ -902,6 +904,7 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (dtype == ST_BF16) {
     return launch_typed<bf16_t, bf16_t>(q, stream);
   }
-  if (dtype == ST_SPLIT) return launch_typed<float, bf16_t>(q, stream);
+  if (dtype == ST_SPLIT) return launch_typed<float, bf16_t, true>(q, stream);
+  if (dtype == ST_BF16F) return launch_typed<float, bf16_t, false>(q, stream);
   return ST_EDTYPE;
 }

@@ -23,6 +23,7 @@
 #include "common.h"
 #include "kernels.h"
 
+int g_opt_bf16f = 0;  // STTS_OPT_BF16F: bf16 training convs on the general engine read / write fp32 frames
 int g_opt_wgw = 1;  // k_wgrad_bf16w for the stride-1 convs (STTS_OPT_WGRAD); 0 = the per-tap kernel everywhere
 
 namespace {
@@ -545,12 +546,14 @@ EngineGeo engine_geo(const Geo& g, bool fwd) {
 
 WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
   const size_t esz = dtype == ST_BF16 ? 2 : 4;  // ST_SPLIT: fp32 frames, bf16 hi + lo weights
+  // bf16 runs on the general engine read / write fp32 frames directly (ST_BF16F): the padded input copy may be fp32
+  const size_t xesz = 4;
   const EngineGeo e = engine_geo(g, fwd);
   WsLayout w;
   memset(&w, 0, sizeof(w));
   size_t off = 0;
   w.xin = off;
-  off += al((size_t)g.B * e.Lin * ldpad(e.ci) * esz);
+  off += al((size_t)g.B * e.Lin * ldpad(e.ci) * xesz);
   w.wstage = off;
   if (e.wm != W_PLAIN || e.co_p != e.co) off += al((size_t)e.co_p * e.ci * g.K * 4);
   w.bpad = off;
@@ -558,7 +561,7 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
   w.packed = off;
   off += al(st_packed_conv_elems(e.ci, e.co_p, g.K, e.transposed, e.u) * esz);
   w.yout = off;
-  if (dtype == ST_BF16 || e.co_p != e.co) off += al((size_t)g.B * e.Lout * e.co_p * esz);
+  if (dtype == ST_BF16 || e.co_p != e.co) off += al((size_t)g.B * e.Lout * e.co_p * xesz);
   if (!fwd) {
     const Slices sl = slices_of(g);
     w.part = off;
@@ -586,13 +589,8 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   const WsLayout L = ws_layout(g, dtype, fwd);
   const int K = g.K, B = g.B;
   const int ldx = ldpad(e.ci);
-  const int adt = dtype == ST_BF16 ? ST_BF16 : ST_FP32;  // frames storage (the split mode keeps fp32)
   void* xd = ws + L.xin;
   void* wd = ws + L.packed;
-  if (adt == ST_FP32 && ldx == e.ci)
-    xd = (void*)xf;  // fp32 frames with 8-aligned rows are the engine's input as they are
-  else
-    ST_CHECK(st_frames_convert(xf, B, e.Lin, e.ci, e.ci, xd, ldx, nullptr, 0, adt, s));
   const float* wsrc = w;
   if (e.wm != W_PLAIN || e.co_p != e.co) {
     float* wt = (float*)(ws + L.wstage);
@@ -654,9 +652,6 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
     p.Lq = (e.Lout - 1 + g.pad) / e.u + 1;
   }
   p.Lout = e.Lout;
-  const bool direct = adt == ST_FP32 && e.co_p == e.co;
-  void* yd = direct ? (void*)y : (void*)(ws + L.yout);
-  p.y = yd;
   p.y_bs = (long long)e.Lout * e.co_p;
   p.y_ld = e.co_p;
   p.out_scale = scale;
@@ -665,12 +660,26 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
     p.epi_slope = slope;
   }
   if (res) {  // y = conv + res (fp32 frames [B][Lout][co], the same layout as y)
-    if (adt != ST_FP32 || e.co_p != e.co) return ST_EINVAL;
     p.res = res;
     p.res_bs = (long long)e.Lout * e.co;
     p.res_ld = e.co;
   }
-  ST_CHECK(st_conv1d(p, dtype, s));
+  // frames storage: bf16 runs whose launch goes to the general engine read and write the fp32 frames directly
+  // (ST_BF16F: the window is rounded to bf16 while staged), saving the two conversion passes around the conv;
+  // the specialised engines (resconv, pwgemm) take bf16 frames
+  int edt = dtype;
+  if (dtype == ST_BF16 && g_opt_bf16f && st_conv1d_engine(p, ST_BF16) == ST_ENGINE_IGEMM) edt = ST_BF16F;
+  const int adt = (edt == ST_BF16) ? ST_BF16 : ST_FP32;
+  if (res && (adt != ST_FP32 || e.co_p != e.co)) return ST_EINVAL;
+  if (adt == ST_FP32 && ldx == e.ci)
+    xd = (void*)xf;  // fp32 frames with 8-aligned rows are the engine's input as they are
+  else
+    ST_CHECK(st_frames_convert(xf, B, e.Lin, e.ci, e.ci, xd, ldx, nullptr, 0, adt, s));
+  p.x = xd;
+  const bool direct = adt == ST_FP32 && e.co_p == e.co;
+  void* yd = direct ? (void*)y : (void*)(ws + L.yout);
+  p.y = yd;
+  ST_CHECK(st_conv1d(p, edt, s));
   if (!direct) ST_CHECK(st_frames_to_f32(yd, B, e.Lout, e.co, e.co_p, y, adt, s));
   return 0;
 }
@@ -777,7 +786,7 @@ extern "C" int stts_conv1d_fwd(int dtype, const float* x, const float* w, const 
 
 extern "C" long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride,
                                                      int dil, int pad, int Lq) {
-  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  if (dtype != ST_FP32 && dtype != ST_BF16 && dtype != ST_SPLIT) return ST_EDTYPE;
   const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
   if (!geo_ok(g)) return ST_EINVAL;
   if (g.stride > 1 && g.dil > 1) return ST_EINVAL;
@@ -844,7 +853,7 @@ size_t convT_ws(const Geo& gc, int dtype) {
 
 extern "C" long long stts_conv_transpose1d_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K,
                                                            int stride, int pad, int Lout) {
-  if (dtype != ST_FP32 && dtype != ST_BF16) return ST_EDTYPE;
+  if (dtype != ST_FP32 && dtype != ST_BF16 && dtype != ST_SPLIT) return ST_EDTYPE;
   const Geo gc = convT_geo(B, Lin, Cin, Cout, K, stride, pad, Lout);
   if (!geo_ok(gc)) return ST_EINVAL;
   if (stride == 1 && K - 1 < pad) return ST_EINVAL;

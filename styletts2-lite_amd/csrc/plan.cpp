@@ -1856,7 +1856,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_DEBUG: g_opt_debug = value; return 0;
     case STTS_OPT_STATS_SLOTS: g_opt_stats_slots = value > 0 ? value : 0; return 0;
     case STTS_OPT_SMALL_TILES: g_opt_small_tiles = value != 0; return 0;
-    case STTS_OPT_BIGCONV: g_opt_bigconv = (value >= 1 && value <= 4) ? value : 2; return 0;
+    case STTS_OPT_BIGCONV: g_opt_bigconv = (value >= 1 && value <= 5) ? value : 2; return 0;
     case STTS_OPT_HEAD: g_opt_head = value ? 1 : 0; return 0;
     case STTS_OPT_SKEW: g_opt_skew = value; return 0;
     case STTS_OPT_FRONT: g_opt_front = (value >= 0 && value <= 2) ? value : 1; return 0;
@@ -1869,6 +1869,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_MSDFOLD: g_opt_msdfold = value ? 1 : 0; return 0;
     case STTS_OPT_RCPP: g_opt_rcpp = (value >= 0 && value <= 2) ? value : 1; return 0;
     case STTS_OPT_RESSPLIT: g_opt_ressplit = value ? 1 : 0; return 0;
+    case STTS_OPT_BF16F: g_opt_bf16f = value ? 1 : 0; return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1899,6 +1900,7 @@ int stts_get_option(int key) {
     case STTS_OPT_MSDFOLD: return g_opt_msdfold;
     case STTS_OPT_RCPP: return g_opt_rcpp;
     case STTS_OPT_RESSPLIT: return g_opt_ressplit;
+    case STTS_OPT_BF16F: return g_opt_bf16f;
     default: return ST_EINVAL;
   }
 }

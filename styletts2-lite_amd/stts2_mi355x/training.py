@@ -22,7 +22,8 @@ from torch import nn
 
 from .engine import _ptr, _require_device, _stream, check, lib
 
-_DT = {"fp32": 0, "bf16": 1}
+# bf16x3: the split-operand mode (fp32 frames, forward / dx operands as bf16 hi + lo, three MFMAs; dw in fp32)
+_DT = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 _TRAIN_READY = False
 # algorithmic conv work of the autograd path (measurement: tools/bench_train_step.py): 2 B Lq Cout Cin K flops per
 # conv forward, the same again per dx and per dw (the transposed conv: 2 B Lin Cin Cout K)
@@ -178,7 +179,7 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="fp32"):
     conv engines.  dtype 'bf16' runs the forward and dx with bf16 operands (fp32 accumulation);
     dw / db are always fp32."""
     if dtype not in _DT:
-        raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
+        raise ValueError(f"dtype {dtype!r}: expected one of {list(_DT)}")
     return conv1d_frames(x.transpose(1, 2), weight, bias, stride, padding, dilation, dtype).transpose(1, 2)
 
 
@@ -228,7 +229,7 @@ def conv1d_frames(x, weight, bias=None, stride=1, padding=0, dilation=1, dtype="
     `residual` (frames [B, Lq, Cout], fp32 runs) is added and the sum multiplied by `scale` in the
     conv epilogue; `act_slope`: leaky_relu(., act_slope) applied in the epilogue instead (FUSE_LRELU)."""
     if dtype not in _DT:
-        raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
+        raise ValueError(f"dtype {dtype!r}: expected one of {list(_DT)}")
     if residual is None and scale != 1.0:
         raise ValueError("conv1d_frames: `scale` applies to the residual sum; pass a residual or scale 1")
     stride, padding, dilation = int(stride), int(padding), int(dilation)
@@ -300,7 +301,7 @@ class _ConvT1dFn(torch.autograd.Function):
 def conv_transpose1d_frames(x, weight, bias=None, stride=1, padding=0, output_padding=0, dtype="fp32"):
     """F.conv_transpose1d (groups 1, dilation 1) on frames [B, Lin, Cin] -> [B, Lout, Cout]."""
     if dtype not in _DT:
-        raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
+        raise ValueError(f"dtype {dtype!r}: expected one of {list(_DT)}")
     return _ConvT1dFn.apply(x, weight, bias, int(stride), int(padding), int(output_padding), dtype)
 
 
@@ -951,7 +952,7 @@ def decoder_forward(dec, asr, F0_curve, N, s, noise=None, seed=None, utt_offset=
     as the reference).  Activations stay in frames [B, L, C] end to end."""
     _require_device()
     if dtype not in _DT:
-        raise ValueError(f"dtype {dtype!r}: expected 'fp32' or 'bf16'")
+        raise ValueError(f"dtype {dtype!r}: expected one of {list(_DT)}")
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if noise is None else 0
     if dec.training:

@@ -143,11 +143,12 @@ def test_resconv_engine_matches_general_engine(case):
 WIDE_CASES = [c for c in RB_CASES if c[1] in (128, 256)]
 
 
-@pytest.mark.parametrize("mode", [2, 3, 4])
+@pytest.mark.parametrize("mode", [2, 3, 4, 5])
 @pytest.mark.parametrize("case", WIDE_CASES, ids=[c[0] for c in WIDE_CASES])
 def test_bigconv_v2_matches_v1(case, mode):
     """bf16: the C = 128 / 256 resblock engine v2 (bigconv2.hip; mode 2 = automatic, mode 3 =
-    4-wave blocks two per CU, mode 4 = 8-wave blocks) against v1 (bigconv.hip) on the same launch:
+    4-wave blocks two per CU, mode 4 = 8-wave blocks, mode 5 = C = 256 on 8-wave blocks whose second half
+    runs one group behind) against v1 (bigconv.hip) on the same launch:
     same bf16 operands and transform, fp32 accumulation in a different order, statistics from the
     fp32 epilogue values."""
     try:
@@ -229,12 +230,14 @@ def test_front_engine_matches_igemm(case, cap):
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("mode", [4, 5])
 @pytest.mark.parametrize("case", WIDE_CASES, ids=[c[0] for c in WIDE_CASES])
-def test_bigconv_8wave_many_tiles_per_workgroup(case):
+def test_bigconv_8wave_many_tiles_per_workgroup(case, mode):
     """The 8-wave bigconv2 blocks (STTS_OPT_BIGCONV = 4; at these small sizes the automatic mode
-    picks 4-wave blocks) with the grid capped at 3 workgroups: long tile walks across utterances."""
+    picks 4-wave blocks; 5: the one-group offset halves at C = 256) with the grid capped at 3 workgroups:
+    long tile walks across utterances (coefficient switches, statistics flushes one slot late)."""
     try:
-        E.set_option(E.OPT_BIGCONV, 4)
+        E.set_option(E.OPT_BIGCONV, mode)
         _, y0, s0 = run_case(case, "bf16")
         E.set_option(E.OPT_GRID_CAP, 3)
         _, y, s = run_case(case, "bf16")

@@ -699,3 +699,28 @@ def test_engine_sees_adamw_update():
     assert _rel(y1, y0) > 1e-3 and _rel(m1[0], m0[0]) > 1e-3  # the update moved the outputs
     assert _rel(y1, y2) < 1e-5, _rel(y1, y2)  # the fp32 decode's statistics: fp64 atomics
     assert torch.equal(m1[0], m2[0]), _rel(m1[0], m2[0])
+
+
+def test_train_step_bf16x3_vs_fp64():
+    """TrainStep(dtype='bf16x3') (fp32 frames, every conv forward / dx as split bf16 hi + lo operands on the
+    bf16 MFMA, weight gradients in fp32) at the fixture's size against the oracle's step in fp64: it carries
+    fp32-class accuracy (module-normwise gradient error <= 1e-3 like the fp32 step, losses 1e-4)."""
+    B, T = 2, 8
+    out, cap, p0, p1, gin = _run_step("bf16x3", B, T)
+    d64 = lambda sd: {k: v.double() for k, v in sd.items()}  # noqa: E731
+    asr, f0, n, s, wav, noise = (t.double() for t in _train_inputs(B, T))
+    y64, l64, g64, par64 = orc.train_step(*(d64(sd) for sd in p0), HIFI_CFG, asr, f0, n, s, wav, noise)
+    print("y_rec", _rel(out["y_rec"], y64))
+    assert _rel(out["y_rec"], y64) < 1e-4
+    for k in ("d_loss", "loss_mel", "loss_gen_all", "g_loss"):
+        e = abs(float(out[k]) - l64[k]) / abs(l64[k])
+        print(k, e)
+        assert e < 1e-4, (k, e)
+    for tag, i in (("dec", 0), ("mpd", 1), ("msd", 2)):
+        m = _metrics(cap[tag], g64[tag])
+        m["sign"] = _update_sign_agreement(p0[i], p1[tag], par64[tag], g64[tag])
+        print(tag, m)
+        assert m["normwise"] < 1e-3 and m["cos"] > 0.999999 and m["sign"] > 0.99, (tag, m)
+    m = _metrics(gin, g64["inputs"])
+    print("inputs", m)
+    assert m["normwise"] < 1e-2 and m["cos"] > 0.9999, m

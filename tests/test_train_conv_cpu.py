@@ -15,9 +15,8 @@ def test_workspace_queries_validate_geometry():
         assert fn(0, 2, 300, 64, 64, 7, 1, 3, 9, Lq) > 0
         assert fn(1, 2, 300, 64, 64, 7, 1, 3, 9, Lq) > 0
         assert fn(0, 2, 300, 64, 64, 7, 1, 3, 9, Lq + 1) == -1   # ST_EINVAL
-        # STTS_SPLIT (2): the forward takes it, the backward does not
-        assert fn(2, 2, 300, 64, 64, 7, 1, 3, 9, Lq) == (-2 if fn is L.stts_conv1d_bwd_workspace_bytes else
-                                                          fn(0, 2, 300, 64, 64, 7, 1, 3, 9, Lq))
+        # STTS_SPLIT (2): fp32 frames, the fp32 workspace
+        assert fn(2, 2, 300, 64, 64, 7, 1, 3, 9, Lq) == fn(0, 2, 300, 64, 64, 7, 1, 3, 9, Lq)
         assert fn(3, 2, 300, 64, 64, 7, 1, 3, 9, Lq) == -2       # ST_EDTYPE
     Lq = out_length(100, 3, 2, 2, 2)
     assert L.stts_conv1d_bwd_workspace_bytes(0, 1, 100, 8, 8, 3, 2, 2, 2, Lq) == -1  # stride 2 with dilation 2

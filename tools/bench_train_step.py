@@ -9,6 +9,12 @@ forward, dx and dw the step launches) and its rate against the dense MFMA peak o
 --cpu-baseline also the oracle's step (oracle.train_step, torch CPU autograd) on the host cores.
 
     python tools/bench_train_step.py [--steps 10] [--warmup 3] [--dtypes fp32,bf16] [--cpu-baseline]
+                                     [--opt KEY=VALUE ...] [--no-grad-check]
+
+Each dtype line also carries `grad_vs_fp32`: one captured step of fresh modules (same formula weights, inputs and
+noise) in that dtype against the same step in fp32, per module (decoder, MPD, MSD): the normwise gradient error
+max |g - g_fp32| / max |g_fp32|, the cosine of the whole gradient vector, and the first-step AdamW update-sign
+agreement with fp32 (the bounds the tests hold: tests/test_gpu_train_step.py BF16_STEP_BOUNDS).
 """
 import argparse
 import json
@@ -21,7 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd"), os.path.join(ROOT, "tests")]
 import torch  # noqa: E402
 
-PEAK = {"fp32": 157.3e12, "bf16": 2.5e15}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK = {"fp32": 157.3e12, "bf16": 2.5e15, "bf16x3": 2.5e15 / 3}  # MI355X dense MFMA (MI355X_MICROARCH.md); bf16x3: 3 MFMAs a product
 
 
 def build(B, T):
@@ -72,6 +78,39 @@ def run_gpu(dtype, B, T, steps, warmup):
             "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)}
 
 
+def captured_step(dtype, B, T):
+    from stts2_mi355x.synth import source_noise
+    from stts2_mi355x.trainstep import TrainStep
+    dec, mpd, msd, (asr, f0, n, s, wav) = build(B, T)
+    dec, mpd, msd = dec.cuda().eval(), mpd.cuda().train(), msd.cuda().train()
+    p0 = {tag: {k: v.detach().clone() for k, v in m.named_parameters()} for tag, m in
+          (("dec", dec), ("mpd", mpd), ("msd", msd))}
+    ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
+    noise = torch.from_numpy(source_noise(B, 600 * T, tag="train_noise")).cuda()
+    step = TrainStep(dec, mpd, msd, dtype=dtype, capture=True)
+    step(*ins, wav.cuda(), noise=noise)
+    torch.cuda.synchronize()
+    upd = {tag: {k: (p.detach() - p0[tag][k]) for k, p in m.named_parameters()} for tag, m in
+           (("dec", dec), ("mpd", mpd), ("msd", msd))}
+    return step.captured, upd
+
+
+def grad_check(dtype, B, T, ref):
+    got, upd = captured_step(dtype, B, T)
+    gref, uref = ref
+    out = {}
+    for tag in ("dec", "mpd", "msd"):
+        a = torch.cat([got[tag][k].reshape(-1).double() for k in sorted(gref[tag])])
+        b = torch.cat([gref[tag][k].reshape(-1).double() for k in sorted(gref[tag])])
+        ua = torch.cat([upd[tag][k].reshape(-1) for k in sorted(uref[tag])])
+        ub = torch.cat([uref[tag][k].reshape(-1) for k in sorted(uref[tag])])
+        sig = ub.abs() > 0
+        out[tag] = {"normwise": float((a - b).abs().max() / b.abs().max()),
+                    "cos": float((a @ b) / (a.norm() * b.norm())),
+                    "update_sign_agreement": float((torch.sign(ua[sig]) == torch.sign(ub[sig])).float().mean())}
+    return out
+
+
 def run_cpu(B, T):
     from helpers import HIFI_CFG
     from oracle import stts_oracle as orc
@@ -95,12 +134,24 @@ def main():
     ap.add_argument("--T", type=int, default=155)
     ap.add_argument("--cpu-baseline", action="store_true")
     ap.add_argument("--no-fold", action="store_true", help="strided convs on the engines' strided path")
+    ap.add_argument("--opt", action="append", default=[], help="STTS_OPT_* KEY=VALUE held for the run (A/B)")
+    ap.add_argument("--no-grad-check", action="store_true")
     a = ap.parse_args()
     if a.no_fold:
         from stts2_mi355x import training
         training.FOLD_STRIDED = False
+    from stts2_mi355x import engine as E
+    for kv in a.opt:
+        k, v = (int(x) for x in kv.split("="))
+        E.set_option(k, v)
+    ref = None if a.no_grad_check else captured_step("fp32", a.B, a.T)
     for dt in a.dtypes.split(","):
-        print(json.dumps(run_gpu(dt, a.B, a.T, a.steps, a.warmup)), flush=True)
+        line = run_gpu(dt, a.B, a.T, a.steps, a.warmup)
+        if a.opt:
+            line["options"] = a.opt
+        if ref is not None and dt != "fp32":
+            line["grad_vs_fp32"] = grad_check(dt, a.B, a.T, ref)
+        print(json.dumps(line), flush=True)
     if a.cpu_baseline:
         torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())))
         print(json.dumps(run_cpu(a.B, a.T)), flush=True)
