@@ -245,7 +245,9 @@ __device__ __forceinline__ float4 ld4(const float* __restrict__ row, int c, int 
 // ST > 1 (the discriminators' strided convs, dilation 1): the window is stored phase-split, ST blocks of PR
 // rows, block ph holding window rows ph, ph + ST, ...; tap t then reads block (t mod ST) from row t / ST on,
 // again consecutive rows for the transposed fragment reads.
-template <int K, int ST = 1>
+// C32 (Cout <= 32: the MSD / MPD discriminator convs): the second output-channel block would be empty, so the
+// fi = 1 waves take the odd taps of the fi = 0 block instead (each wave (K + 1) / 2 taps and accumulators)
+template <int K, int ST = 1, bool C32 = false>
 __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x, const float* __restrict__ dy, int Lin,
                                                      int Cin, int Lq, int Cout, int dil, int pad, int B, int S,
                                                      int ntci, float* __restrict__ part) {
@@ -314,13 +316,15 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x
       }
     }
   };
-  f32x16 acc[K];
+  constexpr int KA = C32 ? (K + 1) / 2 : K;  // accumulators (taps) per wave
+  f32x16 acc[KA];
 #pragma unroll
-  for (int t = 0; t < K; ++t)
+  for (int t = 0; t < KA; ++t)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  const int cob = C32 ? 0 : fi;
   // a wave whose 32-channel block lies past Cout / Cin computes nothing (wave-uniform)
-  const bool live = co0 + 32 * fi < Cout && ci0 + 32 * fj < Cin;
+  const bool live = co0 + 32 * cob < Cout && ci0 + 32 * fj < Cin;
   const int nch = u1 - u0;
   if (nch > 0) {
     load(u0);
@@ -333,13 +337,15 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x
     if (live) {
 #pragma unroll
       for (int ks = 0; ks < WGW_CH / 16; ++ks) {
-        const bf16x8 a = tr_frag(cur, ks, fi, lane);
+        const bf16x8 a = tr_frag(cur, ks, cob, lane);
 #pragma unroll
-        for (int t = 0; t < K; ++t) {
+        for (int ta = 0; ta < KA; ++ta) {
+          const int t = C32 ? 2 * ta + fi : ta;  // (C32: the wave's taps fi, fi + 2, ...)
+          if (C32 && t >= K) continue;           // (wave-uniform)
           const int tj = t * dil;
           const int row = ST == 1 ? tj : (tj % ST) * PR + tj / ST;
           const bf16x8 bx = tr_frag(cur + (WGW_CH + row) * WGB_STRIDE, ks, fj, lane);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx, acc[t], 0, 0, 0);
+          acc[ta] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bx, acc[ta], 0, 0, 0);
         }
       }
     }
@@ -349,13 +355,16 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x
   if (!live) return;
   float* pt = part + (size_t)sl * K * Cout * Cin;
 #pragma unroll
-  for (int t = 0; t < K; ++t)
+  for (int ta = 0; ta < KA; ++ta) {
+    const int t = C32 ? 2 * ta + fi : ta;
+    if (C32 && t >= K) continue;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int co = co0 + 32 * fi + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      const int co = co0 + 32 * cob + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
       const int ci = ci0 + 32 * fj + (lane & 31);
-      if (co < Cout && ci < Cin) pt[((size_t)t * Cout + co) * Cin + ci] = acc[t][e];
+      if (co < Cout && ci < Cin) pt[((size_t)t * Cout + co) * Cin + ci] = acc[ta][e];
     }
+  }
 }
 
 // slices for k_wgrad_bf16w: about 256 workgroups, >= 2 chunks per slice
@@ -687,8 +696,12 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
 template <int K, int ST = 1>
 void launch_wgw(const Geo& g, const float* x, const float* dy, float* part, int S, hipStream_t s) {
   const int ntci = (g.Cin + 63) / 64, ntco = (g.Cout + 63) / 64;
-  hipLaunchKernelGGL((k_wgrad_bf16w<K, ST>), dim3(ntco * ntci, S), dim3(256), 0, s, x, dy, g.Lin, g.Cin, g.Lq, g.Cout,
-                     g.dil, g.pad, g.B, S, ntci, part);
+  if (g.Cout <= 32 && !(g_opt_exp & 4096))  // (STTS_OPT_EXP bit 4096: every tap on the fi = 0 waves, A/B)
+    hipLaunchKernelGGL((k_wgrad_bf16w<K, ST, true>), dim3(ntco * ntci, S), dim3(256), 0, s, x, dy, g.Lin, g.Cin, g.Lq,
+                       g.Cout, g.dil, g.pad, g.B, S, ntci, part);
+  else
+    hipLaunchKernelGGL((k_wgrad_bf16w<K, ST>), dim3(ntco * ntci, S), dim3(256), 0, s, x, dy, g.Lin, g.Cin, g.Lq, g.Cout,
+                       g.dil, g.pad, g.B, S, ntci, part);
 }
 
 // dw as per-slice partials + the in-order reduction into dw [Cout][Cin][K]
