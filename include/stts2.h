@@ -171,6 +171,19 @@ int stts_conv1d_fwd_res(int dtype, const float* x, const float* w, const float* 
 int stts_conv1d_fwd_act(int dtype, const float* x, const float* w, const float* bias, int B, int Lin, int Cin, int Cout,
                         int K, int stride, int dil, int pad, int Lq, float slope, float* y, void* workspace,
                         long long ws_bytes, void* stream);
+/* SpecDiscriminator's (3, kw) Conv2d(C = 32 -> Cout, stride (1, stride), padding (1, pad)) (discriminators.py:
+ * 37-45, 58-61) over the image x [S][H frames][W bins][C] in one launch, the time expansion done by the engine's
+ * window loads: the conv1d over W of x3 [S H][W][3 C] with x3[s][h][.][dh C + c] = x[s][h + dh - 1][.][c] (zero
+ * outside 0 <= h + dh - 1 < H), which is never materialised.  w [Cout][3 C][K] is dh-major (the Conv2d weight
+ * [Cout][C][3][K] permuted to [Cout][3][C][K]); y [S H][Lq][Cout]; lrelu != 0 applies leaky_relu(., slope) in
+ * the epilogue (as stts_conv1d_fwd_act).  Its backward is stts_conv1d_bwd on the materialised c-major image
+ * (stts_time_expand3: channel c 3 + dh) with the Conv2d weight as it lies ([Cout][3 C][K]), then
+ * stts_time_expand3_bwd.  C must be 32 (ST_EINVAL). */
+long long stts_conv1d_fwd_tx_workspace_bytes(int dtype, int S, int H, int W, int C, int Cout, int K, int stride,
+                                             int pad, int Lq);
+int stts_conv1d_fwd_tx(int dtype, const float* x, const float* w, const float* bias, int S, int H, int W, int C,
+                       int Cout, int K, int stride, int pad, int Lq, int lrelu, float slope, float* y, void* workspace,
+                       long long ws_bytes, void* stream);
 long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride, int dil,
                                           int pad, int Lq);
 int stts_conv1d_bwd(int dtype, const float* x, const float* w, const float* dy, int B, int Lin, int Cin, int Cout,

@@ -253,17 +253,30 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
   // every unit of a thread is the same 8-channel group: u = tid + k*NT, NT % 4 == 0
   const int g8 = tid & 3;
 
+  // the utterance and channel offset chunk c of utterance b loads from (tx_H: the time-expanded MSD input)
+  auto src_of = [&](int b, int c, int& bb, int& cx) __attribute__((always_inline)) {
+    bb = b;
+    cx = c * BK;
+    if (p.tx_H) {
+      const int h = b % p.tx_H + c - 1;
+      const bool ok = (unsigned)h < (unsigned)p.tx_H;
+      bb = ok ? b + c - 1 : b;
+      cx = ok ? 0 : -1;  // -1: the whole chunk is the expansion's zero row
+    }
+  };
   auto issue = [&](int t, int c, typename RawT<T>::type (&pre)[MAXU]) {
     const int mt = t_mt(t), b = t_b(t);
-    const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * p.x_bs;
+    int bb, cx;
+    src_of(b, c, bb, cx);
+    const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)bb * p.x_bs;
     const Rsrc rx = make_rsrc(xb, (unsigned)((size_t)p.Lin * p.x_ld * sizeof(T)));
-    const int gr0 = mt * BM * p.stride - p.pad, ci0 = c * BK;
+    const int gr0 = mt * BM * p.stride - p.pad;
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int u = tid + k * NT;
       const int r = u >> 2;
-      const int gr = gr0 + r, ch = ci0 + 8 * g8;
-      const unsigned e = (u < units) ? (unsigned)(gr * p.x_ld + ch) : OOB;  // gr < 0 wraps: OOB
+      const int gr = gr0 + r, ch = cx + 8 * g8;
+      const unsigned e = (u < units && cx >= 0) ? (unsigned)(gr * p.x_ld + ch) : OOB;  // gr < 0 wraps: OOB
       bload_raw(rx, e, pre[k], (const T*)nullptr);
     }
   };
@@ -370,14 +383,15 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
       if (u < units) put(u, v, gr >= 0 && gr < p.Lin, ci0, k, Xd);
     }
     if (units > MAXU * NT) {  // large windows (2-D style convs): synchronous remainder
-      const int b = t_b(t);
-      const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * p.x_bs;
+      int bb, cx;
+      src_of(t_b(t), c, bb, cx);
+      const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)bb * p.x_bs;
       const Rsrc rx = make_rsrc(xb, (unsigned)((size_t)p.Lin * p.x_ld * sizeof(T)));
       for (int u = tid + MAXU * NT; u < units; u += NT) {
         const int r = u >> 2;
-        const int gr = gr0 + r, ch = ci0 + 8 * g8;
+        const int gr = gr0 + r, ch = cx + 8 * g8;
         typename RawT<T>::type raw;
-        bload_raw(rx, (unsigned)(gr * p.x_ld + ch), raw, (const T*)nullptr);
+        bload_raw(rx, cx >= 0 ? (unsigned)(gr * p.x_ld + ch) : OOB, raw, (const T*)nullptr);
         float v[8];
         raw_to_f32(raw, v);
         put(u, v, gr >= 0 && gr < p.Lin, ci0, k, Xd);
@@ -873,6 +887,7 @@ unsigned long long* g_dbg_stamps = nullptr;  // stts_set_debug_buffer
 int st_conv1d_engine(const ConvParams& p, int dtype) {
   ConvParams q = p;
   if (q.kw <= 0) q.kw = q.KS;
+  if (q.tx_H) return ST_ENGINE_IGEMM;
   if (g_opt_head && st_head_eligible(q)) return ST_ENGINE_HEAD;
   if (st_front_eligible(q, dtype) || st_ups_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
   if (st_resconv_ups_eligible(q, dtype)) return ST_ENGINE_RESCONV;
@@ -891,6 +906,14 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (q.kw <= 0) q.kw = q.KS;
   q.dbg = g_opt_debug;
   q.stamps = g_dbg_stamps;
+  if (q.tx_H) {  // the time-expanded MSD input: general engine only (chunk dh = one 32-channel chunk)
+    if (q.tx_H < 1 || q.nchunks != 3 || q.Cin != 96 || q.x_ld != 32 || q.B % q.tx_H) return ST_EINVAL;
+    if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);
+    if (dtype == ST_BF16) return launch_typed<bf16_t, bf16_t>(q, stream);
+    if (dtype == ST_SPLIT) return launch_typed<float, bf16_t, true>(q, stream);
+    if (dtype == ST_BF16F) return launch_typed<float, bf16_t, false>(q, stream);
+    return ST_EDTYPE;
+  }
   if (g_opt_head && st_head_eligible(q)) return st_head(q, dtype, stream);
   if (st_front_eligible(q, dtype)) return st_bigconv2_front(q, stream);
   if (st_ups_eligible(q, dtype)) return st_bigconv2_ups(q, stream);

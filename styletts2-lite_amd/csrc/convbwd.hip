@@ -593,11 +593,13 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
 // channel-transposed and tap-reversed, W_TRANS: as a ConvTranspose1d weight [in][out][K]).
 int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* w, const float* bias, float* y,
                char* ws, hipStream_t s, const float* res = nullptr, float scale = 1.f, bool lrelu = false,
-               float slope = 0.f) {
+               float slope = 0.f, int tx_H = 0) {
   const EngineGeo e = engine_geo(g, fwd);
   const WsLayout L = ws_layout(g, dtype, fwd);
   const int K = g.K, B = g.B;
-  const int ldx = ldpad(e.ci);
+  // tx_H: xf is the MSD image [B = S H][Lin][32] that the engine time-expands to the ci = 96 channels itself
+  const int cix = tx_H ? 32 : e.ci;
+  const int ldx = tx_H ? 32 : ldpad(e.ci);
   void* xd = ws + L.xin;
   void* wd = ws + L.packed;
   const float* wsrc = w;
@@ -664,6 +666,7 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   p.y_bs = (long long)e.Lout * e.co_p;
   p.y_ld = e.co_p;
   p.out_scale = scale;
+  p.tx_H = tx_H;
   if (lrelu) {  // leaky ReLU in the epilogue (the engines that lack it decline the launch: igemm takes it)
     p.epi_lrelu = 1;
     p.epi_slope = slope;
@@ -680,10 +683,10 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   if (dtype == ST_BF16 && g_opt_bf16f && st_conv1d_engine(p, ST_BF16) == ST_ENGINE_IGEMM) edt = ST_BF16F;
   const int adt = (edt == ST_BF16) ? ST_BF16 : ST_FP32;
   if (res && (adt != ST_FP32 || e.co_p != e.co)) return ST_EINVAL;
-  if (adt == ST_FP32 && ldx == e.ci)
+  if (adt == ST_FP32 && ldx == cix)
     xd = (void*)xf;  // fp32 frames with 8-aligned rows are the engine's input as they are
   else
-    ST_CHECK(st_frames_convert(xf, B, e.Lin, e.ci, e.ci, xd, ldx, nullptr, 0, adt, s));
+    ST_CHECK(st_frames_convert(xf, B, e.Lin, cix, cix, xd, ldx, nullptr, 0, adt, s));
   p.x = xd;
   const bool direct = adt == ST_FP32 && e.co_p == e.co;
   void* yd = direct ? (void*)y : (void*)(ws + L.yout);
@@ -795,6 +798,24 @@ extern "C" int stts_conv1d_fwd(int dtype, const float* x, const float* w, const 
   if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
   const Geo g{B, Lin, Cin, Cout, K, stride, dil, pad, Lq};
   return run_engine(dtype, g, true, x, w, bias, y, (char*)workspace, (hipStream_t)stream);
+}
+
+extern "C" long long stts_conv1d_fwd_tx_workspace_bytes(int dtype, int S, int H, int W, int C, int Cout, int K,
+                                                        int stride, int pad, int Lq) {
+  if (C != 32 || S < 1 || H < 1 || (long long)S * H > 0x7fffffffLL) return ST_EINVAL;
+  return stts_conv1d_fwd_workspace_bytes(dtype, S * H, W, 3 * C, Cout, K, stride, 1, pad, Lq);
+}
+
+extern "C" int stts_conv1d_fwd_tx(int dtype, const float* x, const float* w, const float* bias, int S, int H, int W,
+                                  int C, int Cout, int K, int stride, int pad, int Lq, int lrelu, float slope, float* y,
+                                  void* workspace, long long ws_bytes, void* stream) {
+  const long long need = stts_conv1d_fwd_tx_workspace_bytes(dtype, S, H, W, C, Cout, K, stride, pad, Lq);
+  if (need < 0) return (int)need;
+  if (!x || !w || !y) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  const Geo g{S * H, W, 3 * C, Cout, K, stride, 1, pad, Lq};
+  return run_engine(dtype, g, true, x, w, bias, y, (char*)workspace, (hipStream_t)stream, nullptr, 1.f, lrelu != 0,
+                    slope, H);
 }
 
 extern "C" long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride,

@@ -60,6 +60,11 @@ struct ConvParams {
   int w_resident;  // weights of the column tile stay in LDS across tiles (set by the launcher)
   float* splitk_ws;          // fp32 scratch for split-K partials of small launches (plan workspace), or null
   long long splitk_ws_elems;
+  // time expansion (the MSD's (3, kw) Conv2d over [S][H][W][C] frames, conv1d.hip only): with tx_H > 0 the
+  // input is x [S H][Lin = W][C = 32] and 32-channel chunk dh (0..2) reads utterance b + dh - 1, zero when
+  // (b mod tx_H) + dh - 1 falls outside [0, tx_H): the K dimension is dh-major (k = dh C + c), and the
+  // time-expanded image x3[..][dh C + c] = x[b + dh - 1][..][c] is never materialised
+  int tx_H;
 };
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);

@@ -72,7 +72,8 @@ def lib():
     L.stts_gan_losses_scratch_bytes.argtypes = [c_vp]
     L.stts_gan_losses_scratch_bytes.restype = c_ll
     L.stts_msd_losses.restype = c_int
-    for fn in ("stts_conv1d_fwd_workspace_bytes", "stts_conv1d_bwd_workspace_bytes"):
+    for fn in ("stts_conv1d_fwd_workspace_bytes", "stts_conv1d_bwd_workspace_bytes",
+               "stts_conv1d_fwd_tx_workspace_bytes"):
         getattr(L, fn).argtypes = [c_int] * 10
         getattr(L, fn).restype = c_ll
     L.stts_conv1d_fwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
@@ -80,6 +81,8 @@ def lib():
     L.stts_conv1d_fwd_act.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [ctypes.c_float, c_vp, c_vp, c_ll,
                                                                                   c_vp]
     L.stts_conv1d_fwd_act.restype = c_int
+    L.stts_conv1d_fwd_tx.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 10 + [ctypes.c_float, c_vp, c_vp, c_ll, c_vp]
+    L.stts_conv1d_fwd_tx.restype = c_int
     L.stts_conv1d_fwd_res.argtypes = [c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_float] + [c_int] * 9 + [c_vp, c_vp,
                                                                                                    c_ll, c_vp]
     L.stts_pool_workspace_bytes.argtypes = [c_int, c_int, c_int]

@@ -871,6 +871,74 @@ class _TimeExpandFn(torch.autograd.Function):
         return dy
 
 
+# the MSD's (3, kw) Conv2d over C = 32 channels as one launch that time-expands in its window loads
+# (stts_conv1d_fwd_tx); False = the materialised x3 + conv1d_frames (tests compare both)
+FUSE_TX = True
+
+
+class _ConvTxFn(torch.autograd.Function):
+    """SpecDiscriminator's Conv2d(C, Cout, (3, kw), stride (1, s), padding (1, pad)) + optional leaky ReLU on the
+    image h [S, H, W, C] -> frames [S H, Lq, Cout], with the time expansion inside the conv (stts_conv1d_fwd_tx,
+    weight permuted to dh-major).  The backward materialises x3 (c-major, the weight as it lies) for
+    stts_conv1d_bwd and folds dx3 back with stts_time_expand3_bwd."""
+
+    @staticmethod
+    def forward(ctx, h, w, bias, stride, pad, dtype, act):
+        _require_device()
+        hf = _f32(h)
+        S, H, W, C = hf.shape
+        co, ci, kh, kw = w.shape
+        if ci != C or kh != 3:
+            raise ValueError(f"weight {tuple(w.shape)} does not take the [S, H, W, {C}] image")
+        Lq = out_length(W, kw, stride, pad, 1)
+        dt = _DT[dtype]
+        wc = _f32(w)
+        wtx = wc.permute(0, 2, 1, 3).contiguous()  # [Cout][3][C][kw]: K index dh C + c
+        bc = _f32(bias) if bias is not None else None
+        nb = lib().stts_conv1d_fwd_tx_workspace_bytes(dt, S, H, W, C, co, kw, stride, pad, Lq)
+        check(int(nb) if nb < 0 else 0, "stts_conv1d_fwd_tx_workspace_bytes")
+        ws = _ws(nb, hf.device)
+        y = torch.empty(S * H, Lq, co, dtype=torch.float32, device=hf.device)
+        check(lib().stts_conv1d_fwd_tx(dt, _ptr(hf), _ptr(wtx), _ptr(bc), S, H, W, C, co, kw, stride, pad, Lq,
+                                       int(act is not None), ctypes.c_float(act if act is not None else 0.0), _ptr(y),
+                                       _ptr(ws), int(nb), _stream()), "stts_conv1d_fwd_tx")
+        ctx.save_for_backward(hf, wc, y if act is not None else None)
+        ctx.geo = (S, H, W, C, co, kw, stride, pad, Lq, dt, bias is not None)
+        ctx.act = act
+        _count("fwd", 2.0 * S * H * Lq * co * 3 * C * kw)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        hf, wc, ya = ctx.saved_tensors
+        S, H, W, C, co, kw, stride, pad, Lq, dt, has_bias = ctx.geo
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        dyf = _f32(gy)
+        if ctx.act is not None:
+            dpre = torch.empty_like(dyf)
+            check(lib().stts_leaky_relu_bwd(_ptr(ya), _ptr(dyf), ya.numel(), ctypes.c_float(ctx.act), _ptr(dpre),
+                                            _stream()), "stts_leaky_relu_bwd")
+            dyf = dpre
+        dev = dyf.device
+        B, Cin = S * H, 3 * C
+        x3 = torch.empty(S, H, W, Cin, dtype=torch.float32, device=dev)
+        check(_tl().stts_time_expand3(_ptr(hf), S, H, W, C, _ptr(x3), _stream()), "stts_time_expand3")
+        nb = lib().stts_conv1d_bwd_workspace_bytes(dt, B, W, Cin, co, kw, stride, 1, pad, Lq)
+        check(int(nb) if nb < 0 else 0, "stts_conv1d_bwd_workspace_bytes")
+        ws = _ws(nb, dev)
+        dx3 = torch.empty(B, W, Cin, dtype=torch.float32, device=dev) if need_x else None
+        dw = torch.empty(co, Cin, kw, dtype=torch.float32, device=dev) if need_w else None
+        db = torch.empty(co, dtype=torch.float32, device=dev) if (need_b and has_bias) else None
+        check(lib().stts_conv1d_bwd(dt, _ptr(x3), _ptr(wc), _ptr(dyf), B, W, Cin, co, kw, stride, 1, pad, Lq,
+                                    _ptr(dx3), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()), "stts_conv1d_bwd")
+        _count("bwd", 2.0 * B * Lq * co * Cin * kw * ((dx3 is not None) + (dw is not None)))
+        dh = None
+        if dx3 is not None:
+            dh = torch.empty(S, H, W, C, dtype=torch.float32, device=dev)
+            check(_tl().stts_time_expand3_bwd(_ptr(dx3), S, H, W, C, _ptr(dh), _stream()), "stts_time_expand3_bwd")
+        return dh, (dw.reshape(co, C, 3, kw) if dw is not None else None), db, None, None, None, None
+
+
 class _StftMagFn(torch.autograd.Function):
     """|torch.stft(x, n_fft, hop, win, hann(win))| (discriminators.py:11-27) as the [S, F, nb] image."""
 
@@ -1031,11 +1099,17 @@ def spec_discriminator_forward(m, y, dtype="fp32"):
     fmap = []
     layers = list(m.discriminators) + [m.out]
     for j, layer in enumerate(layers):
-        x3 = _TimeExpandFn.apply(h)  # [S, F, W, 3C]
-        W3 = x3.shape[2]
         w = _wn_w(layer)
         co, ci, kh, kw = w.shape
         act = j < len(layers) - 1
+        if (FUSE_TX and (FUSE_LRELU or not act) and ci == 32 and kh == 3 and layer.padding[0] == 1
+                and layer.stride[0] == 1):
+            out = _ConvTxFn.apply(h, w, layer.bias, layer.stride[1], layer.padding[1], dtype, 0.1 if act else None)
+            h = out.reshape(S, Fr, out.shape[1], co)
+            fmap.append(h.permute(0, 3, 1, 2))
+            continue
+        x3 = _TimeExpandFn.apply(h)  # [S, F, W, 3C]
+        W3 = x3.shape[2]
         out = conv1d_frames(x3.reshape(S * Fr, W3, 3 * ci), w.reshape(co, ci * kh, kw), layer.bias,
                             layer.stride[1], layer.padding[1], dtype=dtype,
                             act_slope=0.1 if (act and FUSE_LRELU) else None)

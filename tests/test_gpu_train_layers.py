@@ -232,3 +232,45 @@ def test_discriminator_p_bf16_close():
     worst = max(perr, key=perr.get)
     print("bf16 DiscriminatorP parameter gradients: worst", worst, f"{perr[worst]:.2e}")
     assert perr[worst] < 1e-1, (worst, perr[worst])
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
+@pytest.mark.parametrize("co,kw,stride,pad,act", [(32, 9, 2, 4, 0.1), (32, 3, 1, 1, 0.1), (1, 3, 1, 1, None)])
+def test_msd_time_expanded_conv(dtype, co, kw, stride, pad, act):
+    """SpecDiscriminator's (3, kw) Conv2d over C = 32 channels with the time expansion inside the conv's window
+    loads (stts_conv1d_fwd_tx, training.FUSE_TX) against the materialised x3 + conv1d path in the same dtype
+    (same products, another K order: 1e-5 of the max; bf16 1e-4, its output one bf16 ulp) and, in fp32, against
+    torch's fp64 Conv2d (1e-5), output and the gradients of image, weight and bias."""
+    from stts2_mi355x import training as T
+    g = torch.Generator().manual_seed(co * 100 + kw + stride)
+    S, H, W, C = 2, 37, 257, 32
+    h = torch.randn(S, H, W, C, generator=g)
+    w = torch.randn(co, C, 3, kw, generator=g) / (3 * C * kw) ** 0.5
+    b = torch.randn(co, generator=g) * 0.1
+    gy = torch.randn(S * H, (W + 2 * pad - kw) // stride + 1, co, generator=g)
+    res = []
+    for fused in (True, False):
+        hd, wd, bd = (t.cuda().requires_grad_(True) for t in (h, w, b))
+        if fused:
+            y = T._ConvTxFn.apply(hd, wd, bd, stride, pad, dtype, act)
+        else:
+            x3 = T._TimeExpandFn.apply(hd)
+            y = T.conv1d_frames(x3.reshape(S * H, W, 3 * C), wd.reshape(co, 3 * C, kw), bd, stride, pad, dtype=dtype,
+                                act_slope=act)
+        (y * gy.cuda()).sum().backward()
+        res.append([t.detach().cpu() for t in (y, hd.grad, wd.grad, bd.grad)])
+    for name, a, r in zip(("y", "dh", "dw", "db"), res[0], res[1]):
+        assert a.shape == r.shape, name
+        # bf16 convs store bf16 outputs: the other K order can round an output one bf16 ulp apart (2^-8 relative
+        # near the max, measured 3.4e-3); the gradients are fp32 sums
+        tol = 1e-2 if (dtype == "bf16" and name == "y") else (1e-4 if dtype == "bf16" else 1e-5)
+        assert _rel(a, r) < tol, (name, _rel(a, r))
+    if dtype == "fp32":
+        hr, wr, br = (t.double().requires_grad_(True) for t in (h, w, b))
+        yr = F.conv2d(hr.permute(0, 3, 1, 2), wr, br, stride=(1, stride), padding=(1, pad))
+        if act is not None:
+            yr = F.leaky_relu(yr, act)
+        yr = yr.permute(0, 2, 3, 1).reshape(S * H, -1, co)
+        (yr * gy.double()).sum().backward()
+        for name, a, r in zip(("y", "dh", "dw", "db"), res[0], (yr, hr.grad, wr.grad, br.grad)):
+            assert _rel(a, r) < 1e-5, (name, _rel(a, r))

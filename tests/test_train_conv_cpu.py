@@ -21,6 +21,13 @@ def test_workspace_queries_validate_geometry():
     Lq = out_length(100, 3, 2, 2, 2)
     assert L.stts_conv1d_bwd_workspace_bytes(0, 1, 100, 8, 8, 3, 2, 2, 2, Lq) == -1  # stride 2 with dilation 2
     assert L.stts_conv1d_fwd_workspace_bytes(0, 1, 100, 8, 8, 3, 2, 2, 2, Lq) > 0
+    # the MSD's time-expanded conv (stts_conv1d_fwd_tx): the conv1d of S H rows over 3 C = 96 channels; C = 32 only
+    Lq = out_length(257, 9, 2, 4, 1)
+    tx = L.stts_conv1d_fwd_tx_workspace_bytes
+    assert tx(1, 2, 37, 257, 32, 32, 9, 2, 4, Lq) == L.stts_conv1d_fwd_workspace_bytes(1, 74, 257, 96, 32, 9, 2, 1, 4, Lq)
+    assert tx(1, 2, 37, 257, 16, 32, 9, 2, 4, Lq) == -1
+    assert tx(1, 2, 37, 257, 32, 32, 9, 2, 4, Lq + 1) == -1
+    assert tx(3, 2, 37, 257, 32, 32, 9, 2, 4, Lq) == -2
 
 
 def test_module_refuses_groups_and_padding_modes():
