@@ -184,6 +184,23 @@ long long stts_conv1d_fwd_tx_workspace_bytes(int dtype, int S, int H, int W, int
 int stts_conv1d_fwd_tx(int dtype, const float* x, const float* w, const float* bias, int S, int H, int W, int C,
                        int Cout, int K, int stride, int pad, int Lq, int lrelu, float slope, float* y, void* workspace,
                        long long ws_bytes, void* stream);
+/* Its input gradient without the expanded image: dx [S][H][W][C] from dy [S H][Lq][Cout] (Cout must be 32) as
+ * the dx of a conv C -> 3 Cout whose output chunk j is dy's row h + j - 1, expanded by the engine's loads:
+ * wd [3 Cout][C][K] with wd[j Cout + co][c][k] = w[co][c][2 - j][k] (the Conv2d weight's rows reversed, dh-major;
+ * torch: w.flip(2).permute(2, 0, 1, 3)). */
+long long stts_conv1d_bwd_tx_workspace_bytes(int dtype, int S, int H, int W, int C, int Cout, int K, int stride,
+                                             int pad, int Lq);
+int stts_conv1d_bwd_tx(int dtype, const float* dy, const float* wd, int S, int H, int W, int C, int Cout, int K,
+                       int stride, int pad, int Lq, float* dx, void* workspace, long long ws_bytes, void* stream);
+/* And its weight / bias gradient from the image x [S][H][W][C] (C = 32) without expanding it, STTS_BF16 only
+ * (STTS_EDTYPE otherwise: the fp32 / split modes run stts_conv1d_bwd on the stts_time_expand3 image), and only
+ * for the (K, stride) pairs of the window weight-gradient kernel ((3, 1), (9, 2) and the other stride-1 K <= 11;
+ * STTS_EINVAL otherwise or with STTS_OPT_WGRAD 0).  dw [Cout][3 C][K] dh-major (dw[co][dh C + c][k] = the
+ * Conv2d weight's gradient at [co][c][dh][k]); db [Cout] or NULL.  Workspace: stts_conv1d_bwd_workspace_bytes
+ * (STTS_BF16, S H, W, 3 C, Cout, K, stride, 1, pad, Lq). */
+int stts_conv1d_wgrad_tx(int dtype, const float* x, const float* dy, int S, int H, int W, int C, int Cout, int K,
+                         int stride, int pad, int Lq, float* dw, float* db, void* workspace, long long ws_bytes,
+                         void* stream);
 long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride, int dil,
                                           int pad, int Lq);
 int stts_conv1d_bwd(int dtype, const float* x, const float* w, const float* dy, int B, int Lin, int Cin, int Cout,
@@ -432,10 +449,13 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_RESSPLIT 1 (default) = the accuracy mode's (STTS_SPLIT) C = 32 / 64 resblock convs run on the split
  *                     resblock engine (ressplit.hip; C = 64 in two input-channel passes); 0 = conv1d_igemm (A/B). */
 #define STTS_OPT_RESSPLIT 19
-/*   STTS_OPT_BF16F    1 (default) = bf16 training-step convs (stts_conv1d_fwd / _bwd dx) that run on the general engine
- *                     read and write the caller's fp32 frames directly, rounding the window to bf16 while staging it;
- *                     0 = fp32 -> bf16 frame conversion before and bf16 -> fp32 after each such conv (A/B). */
+/*   STTS_OPT_BF16F    1 = bf16 training-step convs (stts_conv1d_fwd / _bwd dx) that run on the general engine read
+ *                     the caller's fp32 frames directly, rounding the window to bf16 while staging it (4-wave tiles);
+ *                     0 (default) = fp32 -> bf16 frame conversion before each such conv (1 % slower step on). */
 #define STTS_OPT_BF16F 20
+/*   STTS_OPT_YF32     1 (default) = bf16 training-step convs on the general engine store the caller's fp32 output frames
+ *                     from the accumulators (no bf16 rounding of y, no conversion pass); 0 = bf16 output + conversion. */
+#define STTS_OPT_YF32 21
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

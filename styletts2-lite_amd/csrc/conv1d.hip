@@ -645,7 +645,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
               if (p.zc_period && (o % p.zc_period) >= p.zc_valid) {  // padded-image border column
 #pragma unroll
                 for (int j = 0; j < 16; ++j) v[j] = 0.f;
-                store16(yT + (size_t)orow * p.y_ld + co0, v);
+                if (p.y_f32) store16(yF + (size_t)orow * p.y_ld + co0, v);
+                else store16(yT + (size_t)orow * p.y_ld + co0, v);
               } else {
                 {
                   float bb[16];
@@ -703,7 +704,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
 #pragma unroll
                   for (int j = 0; j < 16; ++j) v[j] = 0.5f * v[j] * (1.0f + erff(v[j] * 0.7071067811865476f));
                 }
-                store16(yT + (size_t)orow * p.y_ld + co0, v);
+                // y_f32: fp32 frames straight from the accumulators (the bf16 training convs, no conversion pass)
+                if (p.y_f32) store16(yF + (size_t)orow * p.y_ld + co0, v);
+                else store16(yT + (size_t)orow * p.y_ld + co0, v);
                 if constexpr (!C::BF) {
 #pragma unroll
                   for (int j = 0; j < 16; ++j) v[j] = to_f32(from_f32<T>(v[j]));
@@ -838,8 +841,9 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
 
 template <typename T, typename MT, bool SPF = true>
 int launch_typed(const ConvParams& p, hipStream_t stream) {
-  const bool narrow = (p.Cout % 16 != 0) || p.y_f32 || (p.y_ld % 8 != 0) || (p.res && p.res_ld % 8 != 0) ||
+  const bool narrow = (p.Cout % 16 != 0) || (p.y_ld % 8 != 0) || (p.res && p.res_ld % 8 != 0) ||
                       (p.accb && p.acc_ld % 8 != 0);
+  if (!narrow && p.y_f32 && p.reflect_front) return ST_EINVAL;  // the reflect row stores T
   if (narrow) {
     // per-element epilogue: residual/scale/tanh supported; accumulate/reflect/zero-columns are not
     if (p.accb || p.reflect_front || p.zc_period || p.N > 32 || p.stride > 1) return ST_EINVAL;

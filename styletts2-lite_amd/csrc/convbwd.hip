@@ -23,7 +23,8 @@
 #include "common.h"
 #include "kernels.h"
 
-int g_opt_bf16f = 0;  // STTS_OPT_BF16F: bf16 training convs on the general engine read / write fp32 frames
+int g_opt_bf16f = 0;
+int g_opt_yf32 = 1;  // STTS_OPT_BF16F: bf16 training convs on the general engine read / write fp32 frames
 int g_opt_wgw = 1;  // k_wgrad_bf16w for the stride-1 convs (STTS_OPT_WGRAD); 0 = the per-tap kernel everywhere
 
 namespace {
@@ -247,10 +248,12 @@ __device__ __forceinline__ float4 ld4(const float* __restrict__ row, int c, int 
 // again consecutive rows for the transposed fragment reads.
 // C32 (Cout <= 32: the MSD / MPD discriminator convs): the second output-channel block would be empty, so the
 // fi = 1 waves take the odd taps of the fi = 0 block instead (each wave (K + 1) / 2 taps and accumulators)
+// txH > 0: x is the MSD image [B = S H][Lin][32] time-expanded on the fly, channel ci = dh 32 + c reading
+// utterance row b + dh - 1 (zero outside the signal's H rows), as stts_conv1d_fwd_tx
 template <int K, int ST = 1, bool C32 = false>
 __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x, const float* __restrict__ dy, int Lin,
                                                      int Cin, int Lq, int Cout, int dil, int pad, int B, int S,
-                                                     int ntci, float* __restrict__ part) {
+                                                     int ntci, float* __restrict__ part, int txH) {
   constexpr int DMAX = ST == 1 ? WGW_DILMAX : 1;
   constexpr int PR = WGW_CH + ((K - 1) * DMAX + ST - 1) / ST;  // rows per phase block
   constexpr int WMAX = ST * PR;                                // x window rows (LDS)
@@ -274,6 +277,15 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x
     const int b = u / ncb, qc = (u - b * ncb) * WGW_CH;
     const float* dyb = dy + (size_t)b * Lq * Cout;
     const float* xb = x + (size_t)b * Lin * Cin;
+    int xld = Cin, cb = 0;  // the source rows' channel count and this thread's channel base in them
+    bool okt = true;
+    if (txH) {  // this thread's 16 channels lie in one 32-channel row chunk dh
+      const int dh = (ci0 + c16) >> 5, hh = b % txH + dh - 1;
+      okt = (unsigned)hh < (unsigned)txH && ci0 + c16 < Cin;
+      xb = x + (size_t)(okt ? b + dh - 1 : b) * Lin * 32;
+      xld = 32;
+      cb = 32 * dh;
+    }
     const int q = qc + rr;
     const bool okd = q < Lq;
     const int cc = co0 + c16;
@@ -287,12 +299,12 @@ __global__ __launch_bounds__(256) void k_wgrad_bf16w(const float* __restrict__ x
       const int wr = rr + 64 * i;                  // LDS row: phase block wr / PR, row wr % PR
       const int j = ST == 1 ? wr : (wr % PR) * ST + wr / PR;  // window row
       const int xr = qc * ST - pad + j;
-      const bool ok = wr < WMAX && j < WR && xr >= 0 && xr < Lin;
-      const int c0 = ci0 + c16;
+      const bool ok = okt && wr < WMAX && j < WR && xr >= 0 && xr < Lin;
+      const int c0 = ci0 + c16 - cb;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = c0 + 4 * j;
-        px[i][j] = ld4(xb + (size_t)(ok ? xr : 0) * Cin, c, Cin, ok);
+        px[i][j] = ld4(xb + (size_t)(ok ? xr : 0) * xld, c, xld, ok);
       }
     }
   };
@@ -588,6 +600,17 @@ WsLayout ws_layout(const Geo& g, int dtype, bool fwd) {
   return w;
 }
 
+// db[co] = column sums of dy [B Lq][Cout]: per-slice fp64 partials, reduced in order
+int bias_grad(const Geo& g, const float* dy, float* db, double* part2, hipStream_t s) {
+  const Slices sl = slices_of(g);
+  hipLaunchKernelGGL(k_colsum, dim3((unsigned)((g.Cout + 63) / 64), sl.S2), dim3(256), 0, s, dy,
+                     (long long)g.B * g.Lq, g.Cout, sl.S2, part2);
+  ST_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_slice_reduce<double>, dim3((unsigned)((g.Cout + 255) / 256)), dim3(256), 0, s, part2, sl.S2, 1,
+                     g.Cout, 1, db);
+  return (int)hipGetLastError();
+}
+
 // one engine launch: y fp32 [B][Lout][co] from xf fp32 frames [B][Lin][ci].  w is the forward
 // weight [Cout][Cin][K]; wm says how the engine's weight derives from it (W_PLAIN: as is, W_FLIP:
 // channel-transposed and tap-reversed, W_TRANS: as a ConvTranspose1d weight [in][out][K]).
@@ -688,45 +711,51 @@ int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* 
   else
     ST_CHECK(st_frames_convert(xf, B, e.Lin, cix, cix, xd, ldx, nullptr, 0, adt, s));
   p.x = xd;
-  const bool direct = adt == ST_FP32 && e.co_p == e.co;
+  // bf16 launches on the general engine write fp32 frames from the accumulators (y_f32, STTS_OPT_YF32): no
+  // conversion pass after the conv; the specialised engines store bf16
+  const bool yf = adt == ST_BF16 && e.co_p == e.co && !res && g_opt_yf32 && st_conv1d_engine(p, edt) == ST_ENGINE_IGEMM;
+  const bool direct = (adt == ST_FP32 && e.co_p == e.co) || yf;
   void* yd = direct ? (void*)y : (void*)(ws + L.yout);
   p.y = yd;
+  p.y_f32 = yf ? 1 : 0;
   ST_CHECK(st_conv1d(p, edt, s));
   if (!direct) ST_CHECK(st_frames_to_f32(yd, B, e.Lout, e.co, e.co_p, y, adt, s));
   return 0;
 }
 
 template <int K, int ST = 1>
-void launch_wgw(const Geo& g, const float* x, const float* dy, float* part, int S, hipStream_t s) {
+void launch_wgw(const Geo& g, const float* x, const float* dy, float* part, int S, hipStream_t s, int txH) {
   const int ntci = (g.Cin + 63) / 64, ntco = (g.Cout + 63) / 64;
   if (g.Cout <= 32 && !(g_opt_exp & 4096))  // (STTS_OPT_EXP bit 4096: every tap on the fi = 0 waves, A/B)
     hipLaunchKernelGGL((k_wgrad_bf16w<K, ST, true>), dim3(ntco * ntci, S), dim3(256), 0, s, x, dy, g.Lin, g.Cin, g.Lq,
-                       g.Cout, g.dil, g.pad, g.B, S, ntci, part);
+                       g.Cout, g.dil, g.pad, g.B, S, ntci, part, txH);
   else
     hipLaunchKernelGGL((k_wgrad_bf16w<K, ST>), dim3(ntco * ntci, S), dim3(256), 0, s, x, dy, g.Lin, g.Cin, g.Lq, g.Cout,
-                       g.dil, g.pad, g.B, S, ntci, part);
+                       g.dil, g.pad, g.B, S, ntci, part, txH);
 }
 
-// dw as per-slice partials + the in-order reduction into dw [Cout][Cin][K]
-int wgrad_bf16(const Geo& g, const float* x, const float* dy, float* part, float* dw, hipStream_t s) {
+// dw as per-slice partials + the in-order reduction into dw [Cout][Cin][K] (txH: x time-expanded on the fly, the
+// window kernel only)
+int wgrad_bf16(const Geo& g, const float* x, const float* dy, float* part, float* dw, hipStream_t s, int txH = 0) {
+  if (txH && !(g_opt_wgw && wgw_eligible(g.K, g.stride, g.dil))) return ST_EINVAL;
   if (g_opt_wgw && wgw_eligible(g.K, g.stride, g.dil)) {
     const int Sb = wgw_slices(g.B, g.Lq, g.Cin, g.Cout, g.K);
     if (g.stride == 2) {
-      if (g.K == 3) launch_wgw<3, 2>(g, x, dy, part, Sb, s);
-      else if (g.K == 4) launch_wgw<4, 2>(g, x, dy, part, Sb, s);
-      else launch_wgw<9, 2>(g, x, dy, part, Sb, s);
+      if (g.K == 3) launch_wgw<3, 2>(g, x, dy, part, Sb, s, txH);
+      else if (g.K == 4) launch_wgw<4, 2>(g, x, dy, part, Sb, s, txH);
+      else launch_wgw<9, 2>(g, x, dy, part, Sb, s, txH);
     } else if (g.stride == 3) {
-      if (g.K == 5) launch_wgw<5, 3>(g, x, dy, part, Sb, s);
-      else launch_wgw<6, 3>(g, x, dy, part, Sb, s);
+      if (g.K == 5) launch_wgw<5, 3>(g, x, dy, part, Sb, s, txH);
+      else launch_wgw<6, 3>(g, x, dy, part, Sb, s, txH);
     } else {
       switch (g.K) {
-        case 1: launch_wgw<1>(g, x, dy, part, Sb, s); break;
-        case 2: launch_wgw<2>(g, x, dy, part, Sb, s); break;
-        case 3: launch_wgw<3>(g, x, dy, part, Sb, s); break;
-        case 5: launch_wgw<5>(g, x, dy, part, Sb, s); break;
-        case 7: launch_wgw<7>(g, x, dy, part, Sb, s); break;
-        case 9: launch_wgw<9>(g, x, dy, part, Sb, s); break;
-        default: launch_wgw<11>(g, x, dy, part, Sb, s); break;
+        case 1: launch_wgw<1>(g, x, dy, part, Sb, s, txH); break;
+        case 2: launch_wgw<2>(g, x, dy, part, Sb, s, txH); break;
+        case 3: launch_wgw<3>(g, x, dy, part, Sb, s, txH); break;
+        case 5: launch_wgw<5>(g, x, dy, part, Sb, s, txH); break;
+        case 7: launch_wgw<7>(g, x, dy, part, Sb, s, txH); break;
+        case 9: launch_wgw<9>(g, x, dy, part, Sb, s, txH); break;
+        default: launch_wgw<11>(g, x, dy, part, Sb, s, txH); break;
       }
     }
     ST_CHECK_HIP(hipGetLastError());
@@ -818,6 +847,26 @@ extern "C" int stts_conv1d_fwd_tx(int dtype, const float* x, const float* w, con
                     slope, H);
 }
 
+extern "C" long long stts_conv1d_bwd_tx_workspace_bytes(int dtype, int S, int H, int W, int C, int Cout, int K,
+                                                        int stride, int pad, int Lq) {
+  if (Cout != 32 || S < 1 || H < 1 || (long long)S * H > 0x7fffffffLL) return ST_EINVAL;
+  return stts_conv1d_bwd_workspace_bytes(dtype, S * H, W, C, 3 * Cout, K, stride, 1, pad, Lq);
+}
+
+extern "C" int stts_conv1d_bwd_tx(int dtype, const float* dy, const float* wd, int S, int H, int W, int C, int Cout,
+                                  int K, int stride, int pad, int Lq, float* dx, void* workspace, long long ws_bytes,
+                                  void* stream) {
+  const long long need = stts_conv1d_bwd_tx_workspace_bytes(dtype, S, H, W, C, Cout, K, stride, pad, Lq);
+  if (need < 0) return (int)need;
+  if (!dy || !wd || !dx) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  // the input gradient of the tx conv is the dx of the conv C -> 3 Cout whose output chunk j is dy's row
+  // h + j - 1 (the expansion of dy, done by the engine's loads): weight chunk j = the Conv2d's row dh = 2 - j
+  const Geo g{S * H, W, C, 3 * Cout, K, stride, 1, pad, Lq};
+  return run_engine(dtype, g, false, dy, wd, nullptr, dx, (char*)workspace, (hipStream_t)stream, nullptr, 1.f, false,
+                    0.f, H);
+}
+
 extern "C" long long stts_conv1d_bwd_workspace_bytes(int dtype, int B, int Lin, int Cin, int Cout, int K, int stride,
                                                      int dil, int pad, int Lq) {
   if (dtype != ST_FP32 && dtype != ST_BF16 && dtype != ST_SPLIT) return ST_EDTYPE;
@@ -859,15 +908,26 @@ extern "C" int stts_conv1d_bwd(int dtype, const float* x, const float* w, const 
                        Cin, dw);
     ST_CHECK_HIP(hipGetLastError());
   }
-  if (db) {
-    double* part2 = (double*)(ws + L.part2);
-    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((Cout + 63) / 64), sl.S2), dim3(256), 0, s, dy,
-                       (long long)B * Lq, Cout, sl.S2, part2);
-    ST_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_slice_reduce<double>, dim3((unsigned)((Cout + 255) / 256)), dim3(256), 0, s, part2, sl.S2, 1,
-                       Cout, 1, db);
-    ST_CHECK_HIP(hipGetLastError());
-  }
+  if (db) ST_CHECK(bias_grad(g, dy, db, (double*)(ws + L.part2), s));
+  return 0;
+}
+
+extern "C" int stts_conv1d_wgrad_tx(int dtype, const float* x, const float* dy, int S, int H, int W, int C, int Cout,
+                                    int K, int stride, int pad, int Lq, float* dw, float* db, void* workspace,
+                                    long long ws_bytes, void* stream) {
+  if (dtype != ST_BF16) return ST_EDTYPE;
+  const long long need = stts_conv1d_fwd_tx_workspace_bytes(dtype, S, H, W, C, Cout, K, stride, pad, Lq) < 0
+                             ? ST_EINVAL
+                             : stts_conv1d_bwd_workspace_bytes(dtype, S * H, W, 3 * C, Cout, K, stride, 1, pad, Lq);
+  if (need < 0) return (int)need;
+  if (!x || !dy || !dw) return ST_EINVAL;
+  if (!workspace || ws_bytes < need) return ST_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const Geo g{S * H, W, 3 * C, Cout, K, stride, 1, pad, Lq};
+  char* ws = (char*)workspace;
+  const WsLayout L = ws_layout(g, dtype, false);
+  ST_CHECK(wgrad_bf16(g, x, dy, (float*)(ws + L.part), dw, s, H));
+  if (db) ST_CHECK(bias_grad(g, dy, db, (double*)(ws + L.part2), s));
   return 0;
 }
 

@@ -73,7 +73,7 @@ def lib():
     L.stts_gan_losses_scratch_bytes.restype = c_ll
     L.stts_msd_losses.restype = c_int
     for fn in ("stts_conv1d_fwd_workspace_bytes", "stts_conv1d_bwd_workspace_bytes",
-               "stts_conv1d_fwd_tx_workspace_bytes"):
+               "stts_conv1d_fwd_tx_workspace_bytes", "stts_conv1d_bwd_tx_workspace_bytes"):
         getattr(L, fn).argtypes = [c_int] * 10
         getattr(L, fn).restype = c_ll
     L.stts_conv1d_fwd.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
@@ -83,6 +83,10 @@ def lib():
     L.stts_conv1d_fwd_act.restype = c_int
     L.stts_conv1d_fwd_tx.argtypes = [c_int, c_vp, c_vp, c_vp] + [c_int] * 10 + [ctypes.c_float, c_vp, c_vp, c_ll, c_vp]
     L.stts_conv1d_fwd_tx.restype = c_int
+    L.stts_conv1d_bwd_tx.argtypes = [c_int, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_ll, c_vp]
+    L.stts_conv1d_bwd_tx.restype = c_int
+    L.stts_conv1d_wgrad_tx.argtypes = [c_int, c_vp, c_vp] + [c_int] * 9 + [c_vp, c_vp, c_vp, c_ll, c_vp]
+    L.stts_conv1d_wgrad_tx.restype = c_int
     L.stts_conv1d_fwd_res.argtypes = [c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_float] + [c_int] * 9 + [c_vp, c_vp,
                                                                                                    c_ll, c_vp]
     L.stts_pool_workspace_bytes.argtypes = [c_int, c_int, c_int]
@@ -179,11 +183,12 @@ OPT_MSDFOLD = 17
 OPT_RCPP = 18
 OPT_RESSPLIT = 19
 OPT_BF16F = 20
+OPT_YF32 = 21
 # the production defaults of every STTS_OPT_* (include/stts2.h)
 OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
                 OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1, OPT_SKEW: 0, OPT_FRONT: 1, OPT_PW: 1, OPT_SPLITK: 1,
                 OPT_EXP: 0, OPT_UPS: 1, OPT_WGRAD: 1, OPT_PLAINRC: 1, OPT_MSDFOLD: 1,
-                OPT_RCPP: 1, OPT_RESSPLIT: 1, OPT_BF16F: 0}
+                OPT_RCPP: 1, OPT_RESSPLIT: 1, OPT_BF16F: 0, OPT_YF32: 1}
 # STTS_OPTS="KEY=VALUE,..." (A/B runs of whole suites): option values that replace the defaults for the process,
 # applied when the library loads and by reset_options()
 for _kv in filter(None, os.environ.get("STTS_OPTS", "").split(",")):

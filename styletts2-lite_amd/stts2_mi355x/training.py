@@ -874,13 +874,16 @@ class _TimeExpandFn(torch.autograd.Function):
 # the MSD's (3, kw) Conv2d over C = 32 channels as one launch that time-expands in its window loads
 # (stts_conv1d_fwd_tx); False = the materialised x3 + conv1d_frames (tests compare both)
 FUSE_TX = True
+# (K, stride) of the MSD layers whose bf16 weight gradient reads the image directly (stts_conv1d_wgrad_tx)
+_WGRAD_TX = {(3, 1), (9, 2)}
 
 
 class _ConvTxFn(torch.autograd.Function):
     """SpecDiscriminator's Conv2d(C, Cout, (3, kw), stride (1, s), padding (1, pad)) + optional leaky ReLU on the
     image h [S, H, W, C] -> frames [S H, Lq, Cout], with the time expansion inside the conv (stts_conv1d_fwd_tx,
-    weight permuted to dh-major).  The backward materialises x3 (c-major, the weight as it lies) for
-    stts_conv1d_bwd and folds dx3 back with stts_time_expand3_bwd."""
+    weight permuted to dh-major).  Backward: d h by stts_conv1d_bwd_tx (Cout = 32: dy expanded by the engine's
+    loads, weight rows reversed) or, for the Cout = 1 out layer, stts_conv1d_bwd on x3 + stts_time_expand3_bwd;
+    d w / d b by stts_conv1d_bwd over the materialised x3 (c-major, the weight as it lies)."""
 
     @staticmethod
     def forward(ctx, h, w, bias, stride, pad, dtype, act):
@@ -921,22 +924,49 @@ class _ConvTxFn(torch.autograd.Function):
             dyf = dpre
         dev = dyf.device
         B, Cin = S * H, 3 * C
-        x3 = torch.empty(S, H, W, Cin, dtype=torch.float32, device=dev)
-        check(_tl().stts_time_expand3(_ptr(hf), S, H, W, C, _ptr(x3), _stream()), "stts_time_expand3")
-        nb = lib().stts_conv1d_bwd_workspace_bytes(dt, B, W, Cin, co, kw, stride, 1, pad, Lq)
-        check(int(nb) if nb < 0 else 0, "stts_conv1d_bwd_workspace_bytes")
-        ws = _ws(nb, dev)
-        dx3 = torch.empty(B, W, Cin, dtype=torch.float32, device=dev) if need_x else None
-        dw = torch.empty(co, Cin, kw, dtype=torch.float32, device=dev) if need_w else None
-        db = torch.empty(co, dtype=torch.float32, device=dev) if (need_b and has_bias) else None
-        check(lib().stts_conv1d_bwd(dt, _ptr(x3), _ptr(wc), _ptr(dyf), B, W, Cin, co, kw, stride, 1, pad, Lq,
-                                    _ptr(dx3), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()), "stts_conv1d_bwd")
-        _count("bwd", 2.0 * B * Lq * co * Cin * kw * ((dx3 is not None) + (dw is not None)))
         dh = None
+        if need_x and co == 32:  # d h straight from dy (no dx3 image, no fold)
+            wd = wc.flip(2).permute(2, 0, 1, 3).contiguous()  # [3][Cout][C][kw]: chunk j = row dh = 2 - j
+            nb = lib().stts_conv1d_bwd_tx_workspace_bytes(dt, S, H, W, C, co, kw, stride, pad, Lq)
+            check(int(nb) if nb < 0 else 0, "stts_conv1d_bwd_tx_workspace_bytes")
+            ws = _ws(nb, dev)
+            dh = torch.empty(S, H, W, C, dtype=torch.float32, device=dev)
+            check(lib().stts_conv1d_bwd_tx(dt, _ptr(dyf), _ptr(wd), S, H, W, C, co, kw, stride, pad, Lq, _ptr(dh),
+                                           _ptr(ws), int(nb), _stream()), "stts_conv1d_bwd_tx")
+            _count("bwd", 2.0 * B * Lq * co * Cin * kw)
+            need_x = False
+        need_b = need_b and has_bias
+        dx3 = dw = db = None
+        if not need_x and (need_w or need_b) and dt == 1 and (kw, stride) in _WGRAD_TX:  # bf16: no x3 either
+            nb = lib().stts_conv1d_bwd_workspace_bytes(dt, B, W, Cin, co, kw, stride, 1, pad, Lq)
+            check(int(nb) if nb < 0 else 0, "stts_conv1d_bwd_workspace_bytes")
+            ws = _ws(nb, dev)
+            dwt = torch.empty(co, 3, C, kw, dtype=torch.float32, device=dev)
+            db = torch.empty(co, dtype=torch.float32, device=dev) if need_b else None
+            check(lib().stts_conv1d_wgrad_tx(dt, _ptr(hf), _ptr(dyf), S, H, W, C, co, kw, stride, pad, Lq, _ptr(dwt),
+                                             _ptr(db), _ptr(ws), int(nb), _stream()), "stts_conv1d_wgrad_tx")
+            _count("bwd", 2.0 * B * Lq * co * Cin * kw)
+            dw = dwt.permute(0, 2, 1, 3) if need_w else None  # -> [Cout][C][3][kw]
+            need_w = need_b = False
+        if need_x or need_w or need_b:  # (the G step's frozen discriminators skip this: d h only)
+            x3 = torch.empty(S, H, W, Cin, dtype=torch.float32, device=dev)
+            check(_tl().stts_time_expand3(_ptr(hf), S, H, W, C, _ptr(x3), _stream()), "stts_time_expand3")
+            nb = lib().stts_conv1d_bwd_workspace_bytes(dt, B, W, Cin, co, kw, stride, 1, pad, Lq)
+            check(int(nb) if nb < 0 else 0, "stts_conv1d_bwd_workspace_bytes")
+            ws = _ws(nb, dev)
+            dx3 = torch.empty(B, W, Cin, dtype=torch.float32, device=dev) if need_x else None
+            dw = torch.empty(co, Cin, kw, dtype=torch.float32, device=dev) if need_w else None
+            db = torch.empty(co, dtype=torch.float32, device=dev) if need_b else None
+            check(lib().stts_conv1d_bwd(dt, _ptr(x3), _ptr(wc), _ptr(dyf), B, W, Cin, co, kw, stride, 1, pad, Lq,
+                                        _ptr(dx3), _ptr(dw), _ptr(db), _ptr(ws), int(nb), _stream()),
+                  "stts_conv1d_bwd")
+            _count("bwd", 2.0 * B * Lq * co * Cin * kw * ((dx3 is not None) + (dw is not None)))
         if dx3 is not None:
             dh = torch.empty(S, H, W, C, dtype=torch.float32, device=dev)
             check(_tl().stts_time_expand3_bwd(_ptr(dx3), S, H, W, C, _ptr(dh), _stream()), "stts_time_expand3_bwd")
-        return dh, (dw.reshape(co, C, 3, kw) if dw is not None else None), db, None, None, None, None
+        if dw is not None and dw.dim() == 3:
+            dw = dw.reshape(co, C, 3, kw)
+        return dh, dw, db, None, None, None, None
 
 
 class _StftMagFn(torch.autograd.Function):

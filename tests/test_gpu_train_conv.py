@@ -269,3 +269,36 @@ def test_folded_strided_conv_matches_engine_stride(case, dtype):
     for name, a, r in zip(("y", "dx", "dw", "db"), res[0], res[1]):
         err = float((a - r).abs().max() / max(r.abs().max().item(), 1e-30))
         assert err < tol, f"{name}: folded vs strided differ by {err:.2e} of max"
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[2] % 16 == 0],
+                         ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_d{}_p{}_L{}".format(*c))
+def test_bf16_fp32_output_frames(case):
+    """STTS_OPT_YF32 (default on): bf16 convs on the general engine store fp32 output frames straight from the
+    accumulators.  Against the bf16-output path (option off, + the conversion pass) on the same inputs: y and dx
+    differ by at most the one bf16 rounding the option removes (2^-8 of the max), dw / db not at all (fp32
+    weight gradients from the same x and dy); and the option's y is at least as close to fp64 as the rounded one."""
+    from stts2_mi355x import engine as E
+    from stts2_mi355x.training import conv1d_frames, out_length
+    B, Cin, Cout, K, stride, dil, pad, Lin = case
+    g = torch.Generator().manual_seed(hash(case) % 2**31 + 11)
+    x = torch.randn(B, Lin, Cin, generator=g)
+    w = torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)
+    b = torch.randn(Cout, generator=g)
+    gy = torch.randn(B, out_length(Lin, K, stride, pad, dil), Cout, generator=g)
+    out = {}
+    try:
+        for yf in (0, 1):
+            E.set_option(E.OPT_YF32, yf)
+            xc, wc, bc = (t.cuda().requires_grad_(True) for t in (x, w, b))
+            y = conv1d_frames(xc, wc, bc, stride, pad, dil, dtype="bf16")
+            y.backward(gy.cuda())
+            out[yf] = (y.detach(), xc.grad, wc.grad, bc.grad)
+    finally:
+        E.reset_options()
+    yr = torch.nn.functional.conv1d(x.double().transpose(1, 2), w.double(), b.double(), stride=stride, padding=pad,
+                                    dilation=dil).transpose(1, 2)
+    errs = {k: _rel(a, r) for k, a, r in zip(("y", "dx", "dw", "db"), out[1], out[0])}
+    print(case, {k: f"{v:.2e}" for k, v in errs.items()}, f"vs fp64 on {_rel(out[1][0], yr):.2e} off {_rel(out[0][0], yr):.2e}")
+    assert errs["y"] <= 2 ** -8 and errs["dx"] <= 2 ** -8 and errs["dw"] == 0 and errs["db"] == 0
+    assert _rel(out[1][0], yr) <= _rel(out[0][0], yr) * 1.01

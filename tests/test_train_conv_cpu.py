@@ -28,6 +28,14 @@ def test_workspace_queries_validate_geometry():
     assert tx(1, 2, 37, 257, 16, 32, 9, 2, 4, Lq) == -1
     assert tx(1, 2, 37, 257, 32, 32, 9, 2, 4, Lq + 1) == -1
     assert tx(3, 2, 37, 257, 32, 32, 9, 2, 4, Lq) == -2
+    # its input gradient (stts_conv1d_bwd_tx): the dx of the conv 32 -> 96 over S H rows; Cout = 32 only
+    txb = L.stts_conv1d_bwd_tx_workspace_bytes
+    assert txb(1, 2, 37, 257, 32, 32, 9, 2, 4, Lq) == L.stts_conv1d_bwd_workspace_bytes(1, 74, 257, 32, 96, 9, 2, 1, 4, Lq)
+    assert txb(1, 2, 37, 257, 32, 1, 9, 2, 4, Lq) == -1
+    # the weight gradient from the image (stts_conv1d_wgrad_tx): bf16 only, arguments checked before any launch
+    wg = L.stts_conv1d_wgrad_tx
+    assert wg(0, None, None, 2, 37, 257, 32, 32, 9, 2, 4, Lq, None, None, None, 0, None) == -2
+    assert wg(1, None, None, 2, 37, 257, 32, 32, 9, 2, 4, Lq, None, None, None, 0, None) == -1
 
 
 def test_module_refuses_groups_and_padding_modes():
