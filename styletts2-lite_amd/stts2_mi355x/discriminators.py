@@ -11,6 +11,8 @@ Two paths behind one forward(y, y_hat):
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 from torch import nn
 from torch.nn import Conv2d, Conv2d as _C2
@@ -88,28 +90,57 @@ def _needs_graph(module, y, y_hat):
         any(p.requires_grad for p in module.parameters())
 
 
+# the sub-discriminators (periods / resolutions) of one training forward run on their own HIP streams: their
+# launches at config-5 sizes fill a fraction of the 256 CUs each (e.g. 192 tiles for an MPD 1024-channel conv), so
+# they overlap; autograd runs each backward op on its forward's stream.  False = one stream (A/B, tests)
+CONCURRENT = True
+_STREAMS = {}
+
+
+def _side_streams(n, dev):
+    key = (dev.index, n)
+    if key not in _STREAMS:
+        _STREAMS[key] = [torch.cuda.Stream(device=dev) for _ in range(n)]
+    return _STREAMS[key]
+
+
 def _train_forward(run, discs, y, y_hat):
     """The reference's per-discriminator loop (discriminators.py:143-156 / :80-94) on the autograd path.  y and
     y_hat go through one batched call when they need the same graph (the D step: neither requires grad);
-    otherwise separately, the side without a gradient under no_grad when no parameter needs one."""
+    otherwise separately, the side without a gradient under no_grad when no parameter needs one.  With
+    CONCURRENT, sub-discriminator i runs on side stream i (ordered after the caller's stream, which waits for
+    all of them before it uses the outputs)."""
     dev = torch.device("cuda", torch.cuda.current_device())
     y, y_hat = y.to(device=dev, dtype=torch.float32), y_hat.to(device=dev, dtype=torch.float32)
     B = y.shape[0]
     params_grad = any(p.requires_grad for d in discs for p in d.parameters())
     y_d_rs, y_d_gs, fmap_rs, fmap_gs = [], [], [], []
-    for d in discs:
-        if y.requires_grad == y_hat.requires_grad:
-            score, fmaps = run(d, torch.cat([y, y_hat], 0))
-            r, fr = score[:B], [f[:B] for f in fmaps]
-            g, fg = score[B:], [f[B:] for f in fmaps]
-        else:
-            with torch.set_grad_enabled(params_grad or y.requires_grad):
-                r, fr = run(d, y)
-            g, fg = run(d, y_hat)
+    main = torch.cuda.current_stream(dev)
+    streams = _side_streams(len(discs), dev) if CONCURRENT and len(discs) > 1 else None
+    for i, d in enumerate(discs):
+        if streams is not None:
+            st = streams[i]
+            st.wait_stream(main)
+            y.record_stream(st)
+            y_hat.record_stream(st)
+        with torch.cuda.stream(streams[i]) if streams is not None else contextlib.nullcontext():
+            if y.requires_grad == y_hat.requires_grad:
+                score, fmaps = run(d, torch.cat([y, y_hat], 0))
+                r, fr = score[:B], [f[:B] for f in fmaps]
+                g, fg = score[B:], [f[B:] for f in fmaps]
+            else:
+                with torch.set_grad_enabled(params_grad or y.requires_grad):
+                    r, fr = run(d, y)
+                g, fg = run(d, y_hat)
         y_d_rs.append(r)
         y_d_gs.append(g)
         fmap_rs.append(fr)
         fmap_gs.append(fg)
+    if streams is not None:
+        for st in streams:
+            main.wait_stream(st)
+        for t in [*y_d_rs, *y_d_gs, *(f for fs in fmap_rs + fmap_gs for f in fs)]:
+            t.record_stream(main)  # made on a side stream, read on the caller's
     return y_d_rs, y_d_gs, fmap_rs, fmap_gs
 
 

@@ -1010,6 +1010,38 @@ def _wn_w(layer):
     return weight_norm(layer.weight_g, layer.weight_v)
 
 
+# independent branches of the generator (the noise branch beside snake -> ups, the num_kernels resblocks of a
+# stage) run on their own HIP streams, as discriminators.CONCURRENT does for the sub-discriminators; autograd runs
+# each backward op on its forward's stream.  False = one stream (A/B, tests)
+CONCURRENT_BRANCHES = True
+_BRANCH_STREAMS = {}
+
+
+def _branches(fns, inputs=()):
+    """[f() for f in fns], f i on side stream i, ordered after the caller's stream, which waits for all of them;
+    `inputs` (tensors of the caller's stream the branches read or save for backward) are recorded on each side
+    stream so the allocator does not hand their memory out before those reads finish."""
+    if not CONCURRENT_BRANCHES or len(fns) < 2:
+        return [f() for f in fns]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    key = (dev.index, len(fns))
+    if key not in _BRANCH_STREAMS:
+        _BRANCH_STREAMS[key] = [torch.cuda.Stream(device=dev) for _ in fns]
+    main = torch.cuda.current_stream(dev)
+    outs = []
+    for f, st in zip(fns, _BRANCH_STREAMS[key]):
+        st.wait_stream(main)
+        for t in inputs:
+            t.record_stream(st)
+        with torch.cuda.stream(st):
+            outs.append(f())
+    for st in _BRANCH_STREAMS[key]:
+        main.wait_stream(st)
+    for o in outs:
+        o.record_stream(main)
+    return outs
+
+
 def generator_forward(g, x, s, f0_curve, noise=None, seed=0, utt_offset=0, dtype="fp32"):
     """Generator.forward (hifigan.py:321-347) on frames x [B, 2T, 512] for a module with the reference's
     parameter layout (stts2_mi355x.hifigan.Generator) -> waveform frames [B, L, 1]."""
@@ -1020,22 +1052,29 @@ def generator_forward(g, x, s, f0_curve, noise=None, seed=0, utt_offset=0, dtype
                           scale).unsqueeze(-1)  # frames [B, L, 1]
     B = har.shape[0]
     for i, (u, k) in enumerate(zip(rates, kernels)):
-        x = snake(x, g.alphas[i])
         nc = g.noise_convs[i]
-        S, P = int(nc.stride), int(nc.padding)
-        if S > 1 and nc.weight.shape[-1] == 2 * S and 2 * P == S:
-            # Conv1d(1, C, 2S, stride S, padding S/2) (hifigan.py:296-299) as a 2-tap stride-1 conv over
-            # S-sample frames: frame r = samples [r S - P, r S - P + S), w'[c][j][t] = w[c][0][t S + j]
-            fr = torch.nn.functional.pad(har[..., 0], (P, S - P)).reshape(B, -1, S)
-            w2 = nc.weight.reshape(nc.weight.shape[0], 2, S).transpose(1, 2)
-            x_src = conv1d_frames(fr, w2, nc.bias, 1, 0, 1, dtype)
-        else:
-            x_src = conv1d_frames(har, nc.weight, nc.bias, nc.stride, nc.padding, 1, dtype)
-        x_src = resblock1_frames(g.noise_res[i], x_src, s, dtype)
-        up = g.ups[i]
-        x = conv_transpose1d_frames(x, _wn_w(up), up.bias, up.stride, up.padding, up.output_padding, dtype)
+
+        def noise_branch(i=i, nc=nc):
+            S, P = int(nc.stride), int(nc.padding)
+            if S > 1 and nc.weight.shape[-1] == 2 * S and 2 * P == S:
+                # Conv1d(1, C, 2S, stride S, padding S/2) (hifigan.py:296-299) as a 2-tap stride-1 conv over
+                # S-sample frames: frame r = samples [r S - P, r S - P + S), w'[c][j][t] = w[c][0][t S + j]
+                fr = torch.nn.functional.pad(har[..., 0], (P, S - P)).reshape(B, -1, S)
+                w2 = nc.weight.reshape(nc.weight.shape[0], 2, S).transpose(1, 2)
+                x_src = conv1d_frames(fr, w2, nc.bias, 1, 0, 1, dtype)
+            else:
+                x_src = conv1d_frames(har, nc.weight, nc.bias, nc.stride, nc.padding, 1, dtype)
+            return resblock1_frames(g.noise_res[i], x_src, s, dtype)
+
+        def up_branch(i=i, x=x):
+            x = snake(x, g.alphas[i])
+            up = g.ups[i]
+            return conv_transpose1d_frames(x, _wn_w(up), up.bias, up.stride, up.padding, up.output_padding, dtype)
+
+        x, x_src = _branches([up_branch, noise_branch], (x, har, s))
         x = sum_div([x, x_src])
-        rs = [resblock1_frames(g.resblocks[i * nk + j], x, s, dtype) for j in range(nk)]
+        rs = _branches([lambda j=j, x=x: resblock1_frames(g.resblocks[i * nk + j], x, s, dtype) for j in range(nk)],
+                       (x, s))
         x = sum_div(rs, nk)
     x = snake(x, g.alphas[len(rates)])
     cp = g.conv_post

@@ -304,6 +304,36 @@ def test_decoder_grads_vs_oracle():
     _check3({i: t.grad for i, t in enumerate(ins)}, refs[torch.float32][2], refs[torch.float64][2], "decoder inputs")
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_decoder_concurrent_branches_match_serial(dtype):
+    """training.CONCURRENT_BRANCHES (the generator's noise branch beside snake -> ups, and a stage's three
+    resblocks, each on its own HIP stream) against one stream: output, every parameter gradient and the four
+    input gradients bit-identical (the same launches, only their overlap differs)."""
+    from stts2_mi355x import training as TR
+    B, T = 2, 40
+    dec, _ = make_decoder("hifigan")
+    dec = dec.cuda().eval()
+    asr, f0, n, s, _, noise = _train_inputs(B, T)
+    r = torch.from_numpy(synth.normal("dec_probe_conc", (B, 1, 600 * T))).float().cuda()
+    out = {}
+    try:
+        for conc in (False, True):
+            TR.CONCURRENT_BRANCHES = conc
+            dec.zero_grad(set_to_none=True)
+            ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
+            y = dec(*ins, noise=noise.cuda(), dtype=dtype)
+            (y * r).sum().backward()
+            torch.cuda.synchronize()
+            out[conc] = (y.detach().clone(), {k: p.grad.clone() for k, p in dec.named_parameters()},
+                         [t.grad.clone() for t in ins])
+    finally:
+        TR.CONCURRENT_BRANCHES = True
+    a, b = out[False], out[True]
+    assert torch.equal(a[0], b[0])
+    assert all(torch.equal(a[1][k], b[1][k]) for k in a[1])
+    assert all(torch.equal(u, v) for u, v in zip(a[2], b[2]))
+
+
 def test_decoder_train_mode_smoothing():
     """.train() applies hifigan.py:447-455 with Python's random: replay the same draws into the oracle."""
     B, T = 1, 8
@@ -348,6 +378,44 @@ def test_discriminator_grads_vs_oracle():
     assert abs(float(loss) - float(lr)) < 1e-4 * abs(float(lr))
     _check_grads({k: p.grad for k, p in mpd.named_parameters()}, {k: v.grad for k, v in lp.items()}, what="mpd")
     _check_grads({k: p.grad for k, p in msd.named_parameters()}, {k: v.grad for k, v in ls.items()}, what="msd")
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_discriminators_concurrent_streams_match_serial(dtype):
+    """discriminators.CONCURRENT (each period / resolution on its own HIP stream, autograd backward on the same
+    streams) against the serial loop: the D-step loss with its parameter gradients and the G-step loss with its
+    input gradient, bit-identical (the same launches, only their overlap differs)."""
+    from stts2_mi355x import discriminators as D
+    from stts2_mi355x.losses import DiscriminatorLoss, GeneratorLoss
+    mpd, msd = (m.cuda() for m in _discs())
+    mpd.dtype_compute = msd.dtype_compute = dtype
+    y = _waves(2, 4800, 0).cuda()
+    yh = _waves(2, 4800, 1).cuda()
+    out = {}
+    try:
+        for conc in (False, True):
+            D.CONCURRENT = conc
+            for p in list(mpd.parameters()) + list(msd.parameters()):
+                p.grad = None
+                p.requires_grad_(True)
+            ld = DiscriminatorLoss(mpd, msd)(y, yh)
+            ld.backward()
+            gd = {k: p.grad.clone() for k, p in list(mpd.named_parameters()) + list(msd.named_parameters())}
+            for p in list(mpd.parameters()) + list(msd.parameters()):
+                p.requires_grad_(False)
+            yhd = yh.clone().requires_grad_(True)
+            lg = GeneratorLoss(mpd, msd)(y, yhd)
+            lg.backward()
+            torch.cuda.synchronize()
+            out[conc] = (float(ld), gd, float(lg), yhd.grad.clone())
+    finally:
+        D.CONCURRENT = True
+        for p in list(mpd.parameters()) + list(msd.parameters()):
+            p.requires_grad_(True)
+    a, b = out[False], out[True]
+    assert a[0] == b[0] and a[2] == b[2]
+    assert all(torch.equal(a[1][k], b[1][k]) for k in a[1])
+    assert torch.equal(a[3], b[3])
 
 
 def test_generator_loss_input_grad_vs_oracle():

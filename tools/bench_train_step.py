@@ -135,12 +135,17 @@ def main():
     ap.add_argument("--cpu-baseline", action="store_true")
     ap.add_argument("--no-fold", action="store_true", help="strided convs on the engines' strided path")
     ap.add_argument("--no-fuse-tx", action="store_true", help="MSD convs on the materialised time expansion (A/B)")
+    ap.add_argument("--serial-discs", action="store_true", help="sub-discriminators and generator branches on one stream (A/B)")
     ap.add_argument("--opt", action="append", default=[], help="STTS_OPT_* KEY=VALUE held for the run (A/B)")
     ap.add_argument("--no-grad-check", action="store_true")
     a = ap.parse_args()
     if a.no_fold:
         from stts2_mi355x import training
         training.FOLD_STRIDED = False
+    if a.serial_discs:
+        from stts2_mi355x import discriminators, training
+        discriminators.CONCURRENT = False
+        training.CONCURRENT_BRANCHES = False
     if a.no_fuse_tx:
         from stts2_mi355x import training
         training.FUSE_TX = False
