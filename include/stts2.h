@@ -456,6 +456,10 @@ const char* stts_error_string(int code);
 /*   STTS_OPT_YF32     1 (default) = bf16 training-step convs on the general engine store the caller's fp32 output frames
  *                     from the accumulators (no bf16 rounding of y, no conversion pass); 0 = bf16 output + conversion. */
 #define STTS_OPT_YF32 21
+/*   STTS_OPT_COUT1    1 (default) = training-step conv forwards with one output channel (conv_post, MPD conv_post, the
+ *                     F0 / N convs) run as a GEMV (one wave per output frame, fp32 FMAs over the dtype's operands);
+ *                     0 = the MFMA engine's 16-column tile (A/B). */
+#define STTS_OPT_COUT1 22
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

@@ -6,6 +6,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 typedef __bf16 bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -18,6 +22,21 @@ constexpr int ST_NDTYPES = 3;
 // internal (not a C-ABI dtype): bf16 MFMA operands staged from fp32 frames, fp32 outputs (the training
 // step's convs on the general engine: no frames conversion passes around them)
 constexpr int ST_BF16F = 3;
+
+// hipOccupancyMaxActiveBlocksPerMultiprocessor per (kernel, block size, dynamic LDS), queried once per process
+// (a host-side query on every launch otherwise: the training step makes ~5,000 launches a step); 0 on error
+inline int occupancy_cached(const void* kern, int nt, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, size_t>, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_tuple(kern, nt, lds);
+  const auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, nt, lds) != hipSuccess) return 0;
+  cache[key] = per_cu;
+  return per_cu;
+}
 
 // domain error codes (negative; positive values are hipError_t)
 enum StStatus {

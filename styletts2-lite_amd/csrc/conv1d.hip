@@ -825,8 +825,7 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
     ST_CHECK_HIP(hipGetDevice(&dev));
     ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  int per_cu = 0;
-  ST_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, C::NT, lds));
+  int per_cu = occupancy_cached((const void*)kern, C::NT, lds);
   if (per_cu < 1) per_cu = 1;
   const long long ntn = (p.N + C::BN - 1) / C::BN, ntm = (p.Lq + C::BM - 1) / C::BM;
   const long long tiles = ntn * ntm * p.B;

@@ -23,8 +23,9 @@
 #include "common.h"
 #include "kernels.h"
 
-int g_opt_bf16f = 0;
-int g_opt_yf32 = 1;  // STTS_OPT_BF16F: bf16 training convs on the general engine read / write fp32 frames
+int g_opt_bf16f = 0;  // STTS_OPT_BF16F: bf16 training convs on the general engine read / write fp32 frames
+int g_opt_yf32 = 1;   // STTS_OPT_YF32: ... store fp32 output frames from the accumulators
+int g_opt_cout1 = 1;  // STTS_OPT_COUT1: one-output-channel forwards as a GEMV (k_conv_cout1)
 int g_opt_wgw = 1;  // k_wgrad_bf16w for the stride-1 convs (STTS_OPT_WGRAD); 0 = the per-tap kernel everywhere
 
 namespace {
@@ -480,6 +481,37 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ dy, lo
   }
 }
 
+// Cout = 1 forwards (MPD conv_post 1024 -> 1 (3, 1), the generator's conv_post, the F0 / N stride-2
+// one-channel convs): a GEMV per output frame, which the MFMA engines run as a 16-column tile on a few dozen
+// workgroups (~90 us a launch at config-5 sizes).  One wave per frame, lanes over the input channels, fp32 FMAs
+// over the operands as the dtype rounds them (RB: bf16, as the bf16 MFMA sees them), a fixed-order wave reduction.
+template <bool RB>
+__global__ __launch_bounds__(256) void k_conv_cout1(const float* __restrict__ x, const float* __restrict__ w,
+                                                    const float* __restrict__ bias, int B, int Lin, int Cin, int K,
+                                                    int stride, int dil, int pad, int Lq, int lrelu, float slope,
+                                                    float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long long)B * Lq) return;  // (wave-uniform)
+  const int b = (int)(row / Lq), q = (int)(row - (long long)b * Lq);
+  const float* xb = x + (size_t)b * Lin * Cin;
+  auto rd = [](float v) __attribute__((always_inline)) { return RB ? (float)(bf16_t)v : v; };
+  float acc = 0.f;
+  for (int t = 0; t < K; ++t) {
+    const int r = q * stride - pad + t * dil;
+    if (r < 0 || r >= Lin) continue;  // (wave-uniform)
+    const float* xr = xb + (size_t)r * Cin;
+    for (int c = lane; c < Cin; c += 64) acc = fmaf(rd(w[(size_t)c * K + t]), rd(xr[c]), acc);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) {
+    float v = acc + (bias ? bias[0] : 0.f);
+    if (lrelu) v = v > 0.f ? v : v * slope;
+    y[row] = v;
+  }
+}
+
 // w [Cout][Cin][K] -> wt [Cin][Cout][K] with the taps reversed (the stride-1 dgrad weight)
 __global__ void k_flip_transpose(const float* __restrict__ w, int Cout, int Cin, int K, float* __restrict__ wt) {
   const size_t n = (size_t)Cout * Cin * K;
@@ -617,6 +649,16 @@ int bias_grad(const Geo& g, const float* dy, float* db, double* part2, hipStream
 int run_engine(int dtype, const Geo& g, bool fwd, const float* xf, const float* w, const float* bias, float* y,
                char* ws, hipStream_t s, const float* res = nullptr, float scale = 1.f, bool lrelu = false,
                float slope = 0.f, int tx_H = 0) {
+  if (fwd && g.Cout == 1 && !tx_H && !res && g_opt_cout1) {  // the GEMV kernel (no workspace)
+    const long long rows = (long long)g.B * g.Lq;
+    if (dtype == ST_BF16)
+      hipLaunchKernelGGL(k_conv_cout1<true>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, xf, w, bias, g.B, g.Lin,
+                         g.Cin, g.K, g.stride, g.dil, g.pad, g.Lq, (int)lrelu, slope, y);
+    else
+      hipLaunchKernelGGL(k_conv_cout1<false>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, xf, w, bias, g.B,
+                         g.Lin, g.Cin, g.K, g.stride, g.dil, g.pad, g.Lq, (int)lrelu, slope, y);
+    return (int)hipGetLastError();
+  }
   const EngineGeo e = engine_geo(g, fwd);
   const WsLayout L = ws_layout(g, dtype, fwd);
   const int K = g.K, B = g.B;

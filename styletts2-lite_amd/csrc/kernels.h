@@ -112,6 +112,7 @@ extern int g_opt_ups;
 extern int g_opt_wgw;
 extern int g_opt_bf16f;
 extern int g_opt_yf32;  // STTS_OPT_YF32 (convbwd.hip)
+extern int g_opt_cout1;  // STTS_OPT_COUT1 (convbwd.hip)
 extern int g_opt_plainrc;  // resconv.hip: prologue-free C = 32 / 64 convs (training step) on resconv (STTS_OPT_PLAINRC)  // convbwd.hip: bf16 weight gradient of stride-1 convs on k_wgrad_bf16w (STTS_OPT_WGRAD)
 bool st_ups_eligible(const ConvParams& p, int dtype);
 int st_bigconv2_ups(const ConvParams& p, hipStream_t stream);

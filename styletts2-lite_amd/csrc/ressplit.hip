@@ -330,8 +330,7 @@ int launch_rs(const ConvParams& p, hipStream_t stream) {
     ST_CHECK_HIP(hipGetDevice(&dev));
     ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_rs, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  int per_cu = 0;
-  ST_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, G::NT, G::LDS));
+  int per_cu = occupancy_cached((const void*)kern, G::NT, G::LDS);
   if (per_cu < 1) per_cu = 1;
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   long long grid = (long long)g_num_cu_rs * per_cu;

@@ -302,3 +302,33 @@ def test_bf16_fp32_output_frames(case):
     print(case, {k: f"{v:.2e}" for k, v in errs.items()}, f"vs fp64 on {_rel(out[1][0], yr):.2e} off {_rel(out[0][0], yr):.2e}")
     assert errs["y"] <= 2 ** -8 and errs["dx"] <= 2 ** -8 and errs["dw"] == 0 and errs["db"] == 0
     assert _rel(out[1][0], yr) <= _rel(out[0][0], yr) * 1.01
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
+@pytest.mark.parametrize("case", [c for c in CASES if c[2] == 1] + [(8, 1024, 1, 3, 1, 1, 1, 575)],
+                         ids=lambda c: "B{}_Ci{}_Co{}_K{}_s{}_d{}_p{}_L{}".format(*c))
+def test_cout1_gemv_forward(case, dtype):
+    """STTS_OPT_COUT1 (default on): one-output-channel forwards (conv_post, MPD conv_post 1024 -> 1, the F0 / N
+    stride-2 convs) as a GEMV, against torch fp64 (fp32 / bf16x3: 1e-5 of the max; bf16: its rounded operands,
+    2e-2) and against the MFMA engine (option off) in the same dtype (1e-5; bf16: one bf16 output rounding)."""
+    from stts2_mi355x import engine as E
+    from stts2_mi355x.training import conv1d_frames
+    B, Cin, Cout, K, stride, dil, pad, Lin = case
+    g = torch.Generator().manual_seed(hash(case) % 2**31 + 13)
+    x = torch.randn(B, Lin, Cin, generator=g)
+    w = torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)
+    b = torch.randn(Cout, generator=g)
+    yr = torch.nn.functional.conv1d(x.double().transpose(1, 2), w.double(), b.double(), stride=stride, padding=pad,
+                                    dilation=dil).transpose(1, 2)
+    ys = {}
+    try:
+        for on in (0, 1):
+            E.set_option(E.OPT_COUT1, on)
+            with torch.no_grad():
+                ys[on] = conv1d_frames(x.cuda(), w.cuda(), b.cuda(), stride, pad, dil, dtype=dtype).cpu()
+    finally:
+        E.reset_options()
+    e_ref, e_ab = _rel(ys[1], yr), _rel(ys[1], ys[0])
+    print(case, dtype, f"vs fp64 {e_ref:.2e}, vs engine {e_ab:.2e}")
+    assert e_ref < (2e-2 if dtype == "bf16" else 1e-5)
+    assert e_ab < (2 ** -7 if dtype == "bf16" else 1e-5)
