@@ -61,10 +61,13 @@ def run_gpu(dtype, B, T, steps, warmup):
     ev = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host = []
     for i in range(steps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
+        h0 = time.perf_counter()
         out = step(*ins, wav, seed=1000 + i)
+        host.append((time.perf_counter() - h0) * 1e3)
         b.record()
         ev.append((a, b))
     torch.cuda.synchronize()
@@ -72,6 +75,8 @@ def run_gpu(dtype, B, T, steps, warmup):
     ms = statistics.median(x.elapsed_time(y) for x, y in ev)
     return {"metric": "config5 train step", "dtype": dtype, "B": B, "T_frames": T, "samples_per_utt": 600 * T,
             "ms_per_step_median": round(ms, 2), "ms_per_step_wall": round(wall, 2), "steps": steps,
+            # the host's time to issue one step (Python autograd + C-ABI calls, no sync): ~ms_per_step = host-bound
+            "host_ms_per_step": round(statistics.median(host), 2),
             "conv_gflop_per_step": round(flops / 1e9, 1), "conv_tflops": round(flops / ms / 1e9, 2),
             "frac_of_dense_mfma_peak": round(flops / (ms * 1e-3) / PEAK[dtype], 4),
             "losses": {k: float(out[k]) for k in ("d_loss", "loss_mel", "loss_gen_all")},
