@@ -233,12 +233,27 @@ def forward_only(module, what):
             "torch.no_grad() as inference.py does, or freeze its parameters (requires_grad_(False))")
 
 
+_DEVICE_OK = False
+
+
 def _require_device():
+    global _DEVICE_OK
+    if _DEVICE_OK:
+        return
     if not torch.cuda.is_available():
         raise RuntimeError("stts2_mi355x needs a HIP device (MI355X / gfx950); no CPU fallback exists")
+    _DEVICE_OK = True
+
+
+# the raw query of the current stream: torch.cuda.current_stream() costs ~9 us of host time a call (device index,
+# availability and environment checks), and a training step makes ~2,500 of these calls
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_GET_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
 
 
 def _stream():
+    if _RAW_STREAM is not None and _GET_DEVICE is not None:
+        return ctypes.c_void_p(_RAW_STREAM(_GET_DEVICE()))
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 

@@ -10,6 +10,7 @@ per 32 tensors (stts_adamw_step, include/stts2_train.h).
 from __future__ import annotations
 
 import ctypes
+import weakref
 from functools import reduce
 
 import torch
@@ -31,6 +32,7 @@ class AdamW(torch.optim.Optimizer):
         if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
             raise ValueError(f"invalid AdamW hyper-parameters lr={lr} betas={betas} eps={eps}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False))
+        self._step_views = weakref.WeakKeyDictionary()  # step tensor -> numpy view of its memory
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -55,10 +57,18 @@ class AdamW(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
+                # the step count stays torch.optim's 0-d CPU tensor (state_dict compatibility), advanced through a
+                # cached numpy view of its memory: a torch op + .item() per parameter was ~5 us of host time each
+                t = st["step"]
+                if not t.is_cpu:  # (a checkpoint may carry the step on the device)
+                    t = st["step"] = t.detach().to("cpu", torch.float32)
+                sn = self._step_views.get(t)
+                if sn is None:
+                    sn = self._step_views[t] = t.numpy()
+                sn += 1
                 g = p.grad if p.grad.is_contiguous() and p.grad.dtype == torch.float32 else \
                     p.grad.float().contiguous()
-                batches.setdefault(int(st["step"].item()), []).append((p, g, st["exp_avg"], st["exp_avg_sq"]))
+                batches.setdefault(int(sn), []).append((p, g, st["exp_avg"], st["exp_avg_sq"]))
             for step, items in batches.items():
                 arr = (_AdamWTensor * len(items))()
                 for i, (p, g, m, v) in enumerate(items):
@@ -69,8 +79,7 @@ class AdamW(torch.optim.Optimizer):
                       "stts_adamw_step")
                 # the kernel writes through raw pointers: bump each parameter's version counter as torch's
                 # in-place update would, so cached packed weights (engine._Engine.stale) see the new values
-                for p, _, _, _ in items:
-                    increment_version(p)
+                increment_version([p for p, _, _, _ in items])
         return loss
 
 

@@ -14,6 +14,7 @@ Tolerances: fp32 gradients within 1e-4 of the tensor's max |g| (floored at 1e-3 
 the module: parameters whose true gradient is ~0, e.g. a conv bias feeding an InstanceNorm, carry only
 rounding noise); the mel loss is parity-unpinned upstream (torchaudio is absent: DESIGN §6e).
 """
+import copy
 import random
 
 import numpy as np
@@ -276,6 +277,17 @@ def test_adamw_matches_torch():
         assert ((a - b).abs() <= ulp.clamp_min(1e-11)).all(), (a - b).abs().max().item()
     sd = od.state_dict()
     assert sd["state"][0]["step"].item() == 3 and set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+    # a reloaded optimizer continues from the saved step counts (new step tensors, new host views of them)
+    pd2 = [p.detach().clone().requires_grad_(True) for p in pd]
+    od2 = AdamW(pd2, lr=1e-4, betas=(0.0, 0.99), eps=1e-9, weight_decay=1e-4)
+    od2.load_state_dict(copy.deepcopy(sd))  # (torch shares same-device state tensors with the source otherwise)
+    g = [torch.randn(s).cuda() for s in shapes]
+    for a, b, gg in zip(pd, pd2, g):
+        a.grad, b.grad = gg.clone(), gg.clone()
+    od.step()
+    od2.step()
+    assert all(torch.equal(a, b) for a, b in zip(pd, pd2))
+    assert od.state_dict()["state"][0]["step"].item() == 4 == od2.state_dict()["state"][0]["step"].item()
 
 
 # ------------------------------------------------------------------ whole modules vs the oracle's autograd
