@@ -4,6 +4,8 @@
 //   SourceModuleHnNSF), the depthwise x2 ConvTranspose "pool", the AdaIN style
 //   projections, the iSTFTNet CustomSTFT transform / inverse, and weight-norm
 //   folding + MFMA weight packing.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -834,6 +836,44 @@ int st_mpd_losses(const float* out, const MpdLossSegs& sg, double* part, double*
   hipLaunchKernelGGL(k_mpd_loss_sums, dim3(kMpdLossBlocks, sg.n), dim3(256), 0, s, out, sg, part);
   ST_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_mpd_loss_final, dim3(1), dim3(1), 0, s, sg, part, loss);
+  return (int)hipGetLastError();
+}
+
+namespace {
+// the resblock average of the concurrent branches (decoder_forward at small batches): acc = ((acc + r0) + r1 ...)
+// / div in the running-sum epilogues' order; bf16 storage rounds each partial sum and divides by a reciprocal
+// multiply, as the bf16 epilogues do (fp32: bit-identical to the running sum)
+struct BranchRs {
+  const void* r[4];
+};
+template <typename T>
+__global__ void __launch_bounds__(256) k_branch_avg(T* __restrict__ acc, BranchRs rs, int nr, float div, long long n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float a = to_f32(acc[i]);
+  for (int j = 0; j < nr; ++j) {
+    const float v = to_f32(reinterpret_cast<const T*>(rs.r[j])[i]);
+    if (j + 1 < nr)
+      a = to_f32(from_f32<T>(a + v));
+    else if (std::is_same<T, float>::value)
+      a = (a + v) / div;
+    else
+      a = (a + v) * (1.0f / div);
+  }
+  acc[i] = from_f32<T>(a);
+}
+}  // namespace
+
+int g_opt_branches = 4;  // STTS_OPT_BRANCHES (plan.cpp decoder_forward): concurrent resblocks up to this batch
+
+int st_branch_avg(void* acc, const void* const* rs, int nr, float div, long long n, int dtype, hipStream_t s) {
+  if (nr < 1 || nr > 4 || n < 0) return ST_EINVAL;
+  BranchRs r = {};
+  for (int j = 0; j < nr; ++j) r.r[j] = rs[j];
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  if (!grid) return 0;
+  DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_branch_avg<T>, dim3(grid), dim3(256), 0, s, reinterpret_cast<T*>(acc), r,
+                                              nr, div, n));
   return (int)hipGetLastError();
 }
 

@@ -112,6 +112,19 @@ struct Small {  // weight-norm conv folded to fp32 for a VALU kernel
 struct stts_model {
   int kind = 0;
   Params P;
+  // small-batch decoder: the stage's resblocks 1.. on side streams (decoder_forward), created on first use
+  hipStream_t side[4] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[4] = {};
+  stts_model() = default;
+  stts_model(const stts_model&) = delete;
+  stts_model& operator=(const stts_model&) = delete;
+  ~stts_model() {
+    for (auto& s : side)
+      if (s) (void)hipStreamDestroy(s);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    for (auto& e : ev_join)
+      if (e) (void)hipEventDestroy(e);
+  }
   // -------- decoder config
   int dim_in = 512, style_dim = 128, init_ch = 512, n_fft = 0, hop = 0;
   std::vector<int> rates, kernels, rbk;
@@ -1046,6 +1059,17 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     G[i].p = c.alloc((size_t)B * smax * esz);
     G[i].bs = smax;
   }
+  // small batches (STTS_OPT_BRANCHES): a stage's resblocks 1 .. nrb-1 run beside resblock 0 on side streams, each
+  // with its own temporaries and output, averaged afterwards (st_branch_avg) instead of through the running sum:
+  // at B = 1 one resblock conv fills 64-512 workgroups, so three side by side fill the chip better.  Not in the
+  // split accuracy mode (its two-pass C = 64 convs share the one fp32 partial buffer)
+  const bool br = g_opt_branches > 0 && B <= g_opt_branches && nrb > 1 && nrb <= 5 && c.cdtype != ST_SPLIT;
+  Buf GB[8];
+  if (br)
+    for (int i = 0; i < 2 * (nrb - 1); ++i) {
+      GB[i].p = c.alloc((size_t)B * smax * esz);
+      GB[i].bs = smax;
+    }
   Buf HFR;  // S-sample frames of the source for the MFMA noise_convs (largest such stage)
   {
     int rows = 0;
@@ -1154,9 +1178,41 @@ int decoder_forward(Ctx& c, const DecIO& io) {
       p.stats_ld = C;
       RUN(conv_run(c, p));
     }
-    for (int j = 0; j < nrb; ++j) {
-      const int ro = nrb == 1 ? RO_ACC_FIRST : (j == 0 ? RO_ACC_FIRST : (j == nrb - 1 ? RO_ACC_LAST : RO_ACC_MID));
-      ST_CHECK(resblock1(c, m.resblocks[(size_t)s * nrb + j], X, S_x, R, XT, ro, &ACC, nrb));
+    if (br) {
+      // fork: side stream j - 1 runs resblock j after everything queued so far on the caller's stream
+      if (!c.dry) {
+        for (int j = 0; j + 1 < nrb; ++j) {
+          if (!m.side[j]) ST_CHECK_HIP(hipStreamCreateWithFlags(&m.side[j], hipStreamNonBlocking));
+          if (!m.ev_join[j]) ST_CHECK_HIP(hipEventCreateWithFlags(&m.ev_join[j], hipEventDisableTiming));
+        }
+        if (!m.ev_fork) ST_CHECK_HIP(hipEventCreateWithFlags(&m.ev_fork, hipEventDisableTiming));
+        ST_CHECK_HIP(hipEventRecord(m.ev_fork, c.s));
+        for (int j = 0; j + 1 < nrb; ++j) ST_CHECK_HIP(hipStreamWaitEvent(m.side[j], m.ev_fork, 0));
+      }
+      ST_CHECK(resblock1(c, m.resblocks[(size_t)s * nrb], X, S_x, R, XT, RO_ACC_FIRST, &ACC, nrb));
+      const hipStream_t s0 = c.s;
+      const void* rs[4];
+      for (int j = 1; j < nrb; ++j) {
+        Buf Rj = view(GB[2 * (j - 1)]), XTj = view(GB[2 * (j - 1) + 1]);
+        if (!c.dry) c.s = m.side[j - 1];
+        const int rc = resblock1(c, m.resblocks[(size_t)s * nrb + j], X, S_x, Rj, XTj, RO_PLAIN, nullptr, 0);
+        c.s = s0;
+        ST_CHECK(rc);
+        rs[j - 1] = Rj.p;
+      }
+      // join, then ACC = ((ACC + R_1) + R_2 ...) / nrb
+      if (!c.dry) {
+        for (int j = 0; j + 1 < nrb; ++j) {
+          ST_CHECK_HIP(hipEventRecord(m.ev_join[j], m.side[j]));
+          ST_CHECK_HIP(hipStreamWaitEvent(c.s, m.ev_join[j], 0));
+        }
+      }
+      RUN(st_branch_avg(ACC.p, rs, nrb - 1, (float)nrb, (long long)B * Ls_ * C, c.dtype, c.s));
+    } else {
+      for (int j = 0; j < nrb; ++j) {
+        const int ro = nrb == 1 ? RO_ACC_FIRST : (j == 0 ? RO_ACC_FIRST : (j == nrb - 1 ? RO_ACC_LAST : RO_ACC_MID));
+        ST_CHECK(resblock1(c, m.resblocks[(size_t)s * nrb + j], X, S_x, R, XT, ro, &ACC, nrb));
+      }
     }
     xin = ACC;
     Lcur = Ls_;
@@ -1872,6 +1928,10 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_BF16F: g_opt_bf16f = value ? 1 : 0; return 0;
     case STTS_OPT_YF32: g_opt_yf32 = value ? 1 : 0; return 0;
     case STTS_OPT_COUT1: g_opt_cout1 = value ? 1 : 0; return 0;
+    case STTS_OPT_BRANCHES:
+      if (value < 0) return ST_EINVAL;
+      g_opt_branches = value;
+      return 0;
     default: return ST_EINVAL;
   }
 }
@@ -1905,6 +1965,7 @@ int stts_get_option(int key) {
     case STTS_OPT_BF16F: return g_opt_bf16f;
     case STTS_OPT_YF32: return g_opt_yf32;
     case STTS_OPT_COUT1: return g_opt_cout1;
+    case STTS_OPT_BRANCHES: return g_opt_branches;
     default: return ST_EINVAL;
   }
 }

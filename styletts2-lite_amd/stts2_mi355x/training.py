@@ -759,7 +759,14 @@ class _SumDivFn(torch.autograd.Function):
             dyc = _f32(dy)
             g = torch.empty_like(dyc)
             check(_tl().stts_div(_ptr(dyc), dyc.numel(), ctypes.c_float(ctx.div), _ptr(g), _stream()), "stts_div")
-        return (None,) + tuple(g if need else None for need in ctx.needs_input_grad[1:])
+        # every input gets its own tensor: the inputs may come from concurrent branches (CONCURRENT_BRANCHES), and
+        # autograd may accumulate a gradient in place on one stream while another branch's stream still reads a
+        # shared one
+        out, first = [], True
+        for need in ctx.needs_input_grad[1:]:
+            out.append((g if first else g.clone()) if need else None)
+            first = first and not need
+        return (None,) + tuple(out)
 
 
 def sum_div(xs, div=1.0):

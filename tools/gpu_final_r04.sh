@@ -31,4 +31,11 @@ else
   echo pmc ok
   timeout -k 10 500 python -u tools/bench_train_step.py --steps 8 --warmup 2 --dtypes bf16,bf16x3,fp32 > gpurun_out/bench_train_r04.log 2>&1 || exit $?
   tail -3 gpurun_out/bench_train_r04.log | cut -c1-300
+  timeout -k 10 300 python -u tools/train_conv_shapes.py --dtype bf16 --top 40 > gpurun_out/train_conv_shapes_r04.txt 2>&1 || exit $?
+  head -3 gpurun_out/train_conv_shapes_r04.txt
+  # B = 1 (the reference's inference.py unit): concurrent resblock branches (default) vs the running sum
+  B1="--batch 1 --steps 20 --warmup 5 --no-cpu-baseline --no-parity-mode --no-accuracy-mode --no-e2e --no-profile"
+  STTS_OPTS=23=0 timeout -k 10 300 python -u bench.py $B1 > gpurun_out/bench_b1_nobranch.log 2>&1 || exit $?
+  timeout -k 10 300 python -u bench.py $B1 > gpurun_out/bench_b1_branch.log 2>&1 || exit $?
+  tail -1 gpurun_out/bench_b1_nobranch.log | cut -c1-250; tail -1 gpurun_out/bench_b1_branch.log | cut -c1-250
 fi

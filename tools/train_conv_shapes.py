@@ -15,7 +15,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd"), os.path.join(ROO
 import torch  # noqa: E402
 
 NAMES = ["stts_conv1d_fwd", "stts_conv1d_fwd_res", "stts_conv1d_fwd_act", "stts_conv1d_bwd",
-         "stts_conv_transpose1d_fwd", "stts_conv_transpose1d_bwd"]
+         "stts_conv_transpose1d_fwd", "stts_conv_transpose1d_bwd",
+         # the MSD's time-expanded convs: (S, H, W, C, Cout, K, stride, pad, Lq)
+         "stts_conv1d_fwd_tx", "stts_conv1d_bwd_tx", "stts_conv1d_wgrad_tx"]
 
 
 def main():
@@ -24,8 +26,12 @@ def main():
     ap.add_argument("--top", type=int, default=30)
     a = ap.parse_args()
     from bench_train_step import build
+    from stts2_mi355x import discriminators, training
     from stts2_mi355x import engine as E
     from stts2_mi355x.trainstep import TrainStep
+    # one stream, so that each call's events bracket its own work only
+    discriminators.CONCURRENT = False
+    training.CONCURRENT_BRANCHES = False
     torch.cuda.set_device(0)
     dec, mpd, msd, (asr, f0, n, s, wav) = build(2, 155)
     dec, mpd, msd = dec.cuda().eval(), mpd.cuda().train(), msd.cuda().train()
