@@ -114,7 +114,7 @@ struct stts_model {
   Params P;
   // small-batch decoder: the stage's resblocks 1.. on side streams (decoder_forward), created on first use
   hipStream_t side[4] = {};
-  hipEvent_t ev_fork = nullptr, ev_join[4] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[4] = {}, ev_fork2 = nullptr, ev_noise[8] = {};
   stts_model() = default;
   stts_model(const stts_model&) = delete;
   stts_model& operator=(const stts_model&) = delete;
@@ -122,7 +122,10 @@ struct stts_model {
     for (auto& s : side)
       if (s) (void)hipStreamDestroy(s);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_fork2) (void)hipEventDestroy(ev_fork2);
     for (auto& e : ev_join)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : ev_noise)
       if (e) (void)hipEventDestroy(e);
   }
   // -------- decoder config
@@ -612,6 +615,7 @@ struct Ctx {
     splitk = reinterpret_cast<float*>(alloc((size_t)splitk_elems * 4));
   }
   float* H = nullptr;
+  bool h_ready = false;  // H (every AdaIN layer's style projection) already computed this forward
   const char* packed;
   char* aux;
   int cdtype = 0;  // conv engines / packed weights: the run's dtype (ST_SPLIT in the accuracy mode)
@@ -982,7 +986,7 @@ int run_front(Ctx& c, const DecIO& io, FrontBufs& f) {
   const int B = c.B, T = io.T, n = 2 * T;
   const int ld_enc = rup8(m.dim_in + 2), ld_cat = rup8(1024 + 2 + 64);
   Buf &ENC = f.ENC, *CAT = f.CAT, &H1 = f.H1, &SC = f.SC, &POOL = f.POOL, &X0 = f.X0;
-  RUN(st_linear(io.s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
+  if (!c.h_ready) RUN(st_linear(io.s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
   double* S_enc = c.stat(ld_enc);
   RUN(st_ncl_to_frames(io.asr, B, m.dim_in, T, ENC.p, ld_enc, 0, ENC.bs, S_enc, ld_enc, c.dtype, c.s));
   double* S_cat[4];
@@ -1085,30 +1089,31 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     HARF = c.frames(F, ld_h);
     POST = c.frames(F, ld_h);
   }
+  // small batches (with the resblock branches): every stage's noise branch (noise_convs -> noise_res, which reads
+  // only the harmonic source) runs on a third side stream from the start, beside the front-end and the stages;
+  // stage s's ups conv waits for its output (per-stage buffers NSO)
+  const bool nbr = br && nup <= 8;
+  Buf NSO[8], NB[2];
+  float* splitk_nb = nullptr;  // the side stream's own split-K scratch (the front-end's short convs use c.splitk)
+  if (nbr) {
+    for (int s = 0; s < nup; ++s) NSO[s] = c.frames(Ls[s], Cs[s]);
+    for (int i = 0; i < 2; ++i) {
+      NB[i].p = c.alloc((size_t)B * smax * esz);
+      NB[i].bs = smax;
+    }
+    if (c.splitk_elems) splitk_nb = reinterpret_cast<float*>(c.alloc((size_t)c.splitk_elems * 4));
+  }
   c.stats_begin = c.stats_off = c.off;  // stats region follows; its size is known after the dry run
-  // ---------------- style projections + front-end (hifigan.py:458-472)
-  ST_CHECK(run_front(c, io, fb));
   // ---------------- harmonic source (hifigan.py:323-326 / istftnet.py:544-550)
   RUN(st_sine_phase(io.f0, B, n, scale, PH, c.s));
   RUN(st_sine_source(io.f0, PH, B, n, scale, c.P(m.l_lin_w), c.P(m.l_lin_b), io.noise, io.seed, io.utt, HAR, c.s));
   if (ist) {
     RUN(st_stft(HAR, B, L, m.n_fft, m.hop, c.P(m.stft_fr), c.P(m.stft_fi), HARF.p, ld_h, c.dtype, c.s));
   }
-  // ---------------- generator stages
-  Buf xin = X0;
-  int Lcur = 2 * T, Ccur = 512;
-  int accsel = 4;
-  for (int s = 0; s < nup; ++s) {
-    const int u = m.rates[s], C = Cs[s], Ls_ = Ls[s];
+  // noise branch of stage s (hifigan.py:330-331): noise_convs -> NS -> noise_res -> R
+  auto noise_branch = [&](int s, Buf NS, Buf R, Buf XT) -> int {
+    const int C = Cs[s], Ls_ = Ls[s];
     const bool last = s + 1 == nup;
-    auto view = [&](Buf g) {
-      g.ld = C;
-      g.L = Ls_;
-      g.bs = (long long)Ls_ * C;
-      return g;
-    };
-    Buf NS = view(G[0]), R = view(G[1]), XT = view(G[2]), X = view(G[3]), ACC = view(G[accsel]);
-    // noise branch: noise_convs -> noise_res (hifigan.py:330-331)
     double* S_ns = c.stat(C);
     int sf = 1;
     for (int j = s + 1; j < nup; ++j) sf *= m.rates[j];
@@ -1146,6 +1151,65 @@ int decoder_forward(Ctx& c, const DecIO& io) {
       RUN(conv_run(c, p));
     }
     ST_CHECK(resblock1(c, m.noise_res[s], NS, S_ns, R, XT, RO_PLAIN, nullptr, 0));
+    return 0;
+  };
+  auto sview = [&](Buf g, int s) {
+    g.ld = Cs[s];
+    g.L = Ls[s];
+    g.bs = (long long)Ls[s] * Cs[s];
+    return g;
+  };
+  if (nbr) {
+    // the noise branches' AdaIN layers read H (the style projections): computed before the fork
+    RUN(st_linear(io.s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
+    c.h_ready = true;
+    if (!c.dry) {
+      if (!m.side[2]) ST_CHECK_HIP(hipStreamCreateWithFlags(&m.side[2], hipStreamNonBlocking));
+      for (int s = 0; s < nup; ++s)
+        if (!m.ev_noise[s]) ST_CHECK_HIP(hipEventCreateWithFlags(&m.ev_noise[s], hipEventDisableTiming));
+      if (!m.ev_fork2) ST_CHECK_HIP(hipEventCreateWithFlags(&m.ev_fork2, hipEventDisableTiming));
+      ST_CHECK_HIP(hipEventRecord(m.ev_fork2, c.s));
+      ST_CHECK_HIP(hipStreamWaitEvent(m.side[2], m.ev_fork2, 0));
+    }
+    const hipStream_t s0 = c.s;
+    float* const splitk0 = c.splitk;
+    for (int s = 0; s < nup; ++s) {
+      if (!c.dry) c.s = m.side[2];
+      c.splitk = splitk_nb;
+      const int rc = noise_branch(s, sview(NB[0], s), NSO[s], sview(NB[1], s));
+      c.splitk = splitk0;
+      if (rc == 0 && !c.dry) {
+        const int e = (int)hipEventRecord(m.ev_noise[s], c.s);
+        c.s = s0;
+        ST_CHECK(e);
+      }
+      c.s = s0;
+      ST_CHECK(rc);
+    }
+  }
+  // ---------------- style projections + front-end (hifigan.py:458-472)
+  ST_CHECK(run_front(c, io, fb));
+  // ---------------- generator stages
+  Buf xin = X0;
+  int Lcur = 2 * T, Ccur = 512;
+  int accsel = 4;
+  for (int s = 0; s < nup; ++s) {
+    const int u = m.rates[s], C = Cs[s], Ls_ = Ls[s];
+    const bool last = s + 1 == nup;
+    auto view = [&](Buf g) {
+      g.ld = C;
+      g.L = Ls_;
+      g.bs = (long long)Ls_ * C;
+      return g;
+    };
+    Buf R = view(G[1]), XT = view(G[2]), X = view(G[3]), ACC = view(G[accsel]);
+    Buf XS = R;  // x_source: the noise branch's output
+    if (nbr) {   // this stage's noise branch ran on the side stream
+      XS = NSO[s];
+      if (!c.dry) ST_CHECK_HIP(hipStreamWaitEvent(c.s, m.ev_noise[s], 0));
+    } else {
+      ST_CHECK(noise_branch(s, view(G[0]), R, XT));
+    }
     // ups (+ x_source): Snake(alpha_s) / LReLU(0.1) prologue, polyphase ConvTranspose1d
     double* S_x = c.stat(C);
     {
@@ -1171,9 +1235,9 @@ int decoder_forward(Ctx& c, const DecIO& io) {
         p.y_row_off = 1;
         p.reflect_front = 1;
       }
-      p.res = R.p;
-      p.res_bs = R.bs;
-      p.res_ld = R.ld;
+      p.res = XS.p;
+      p.res_bs = XS.bs;
+      p.res_ld = XS.ld;
       p.stats = S_x;
       p.stats_ld = C;
       RUN(conv_run(c, p));
