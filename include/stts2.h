@@ -460,9 +460,11 @@ const char* stts_error_string(int code);
  *                     F0 / N convs) run as a GEMV (one wave per output frame, fp32 FMAs over the dtype's operands);
  *                     0 = the MFMA engine's 16-column tile (A/B). */
 #define STTS_OPT_COUT1 22
-/*   STTS_OPT_BRANCHES 4 (default) = decoder forwards of at most this many utterances run a generator stage's resblocks
- *                     1 .. n-1 beside resblock 0 on side streams (fork / join events on the caller's stream, so they
- *                     capture into a hipGraph) and average them after, instead of the running sum; 0 = off. */
+/*   STTS_OPT_BRANCHES 8 (default) = decoder forwards of at most this many utterances run a generator stage's resblocks
+ *                     1 .. n-1 beside resblock 0 on side streams, and every stage's noise branch on a third, from the
+ *                     start (fork / join events on the caller's stream, so they capture into a hipGraph); the
+ *                     resblocks are averaged after instead of through the running sum; 0 = off.  (Measured: B = 1
+ *                     -29 %, B = 4 -19 %, B = 8 -6 %, B = 16 even, B = 32 +5 % time.) */
 #define STTS_OPT_BRANCHES 23
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */

@@ -1063,7 +1063,7 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     G[i].p = c.alloc((size_t)B * smax * esz);
     G[i].bs = smax;
   }
-  // small batches (STTS_OPT_BRANCHES): a stage's resblocks 1 .. nrb-1 run beside resblock 0 on side streams, each
+  // small batches (STTS_OPT_BRANCHES, default B <= 8): a stage's resblocks 1 .. nrb-1 run beside resblock 0 on side streams, each
   // with its own temporaries and output, averaged afterwards (st_branch_avg) instead of through the running sum:
   // at B = 1 one resblock conv fills 64-512 workgroups, so three side by side fill the chip better.  Not in the
   // split accuracy mode (its two-pass C = 64 convs share the one fp32 partial buffer)
