@@ -227,6 +227,7 @@ int st_frames_to_f32(const void* src, int B, int L, int C, int ld, float* dst, i
 // acc = ((acc + rs[0]) + rs[1] ...) / div over n contiguous elements (the concurrent resblock branches' average)
 int st_branch_avg(void* acc, const void* const* rs, int nr, float div, long long n, int dtype, hipStream_t s);
 extern int g_opt_branches;  // STTS_OPT_BRANCHES (plan.cpp)
+extern int g_opt_nbranch;   // STTS_OPT_NBRANCH (plan.cpp)
 // GAN losses over the MPD engine's outputs (misc.hip): per (period, layer) block, its offset, the
 // size of its real half, and whether it is a score block (conv_post)
 constexpr int kMpdMaxSegs = 64;

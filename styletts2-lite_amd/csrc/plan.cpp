@@ -1092,7 +1092,7 @@ int decoder_forward(Ctx& c, const DecIO& io) {
   // small batches (with the resblock branches): every stage's noise branch (noise_convs -> noise_res, which reads
   // only the harmonic source) runs on a third side stream from the start, beside the front-end and the stages;
   // stage s's ups conv waits for its output (per-stage buffers NSO)
-  const bool nbr = br && nup <= 8;
+  const bool nbr = (br || (g_opt_nbranch > 0 && B <= g_opt_nbranch && c.cdtype != ST_SPLIT)) && nup <= 8;
   Buf NSO[8], NB[2];
   float* splitk_nb = nullptr;  // the side stream's own split-K scratch (the front-end's short convs use c.splitk)
   if (nbr) {
@@ -1996,6 +1996,10 @@ int stts_set_option(int key, int value) {
       if (value < 0) return ST_EINVAL;
       g_opt_branches = value;
       return 0;
+    case STTS_OPT_NBRANCH:
+      if (value < 0) return ST_EINVAL;
+      g_opt_nbranch = value;
+      return 0;
     default: return ST_EINVAL;
   }
 }
@@ -2030,6 +2034,7 @@ int stts_get_option(int key) {
     case STTS_OPT_YF32: return g_opt_yf32;
     case STTS_OPT_COUT1: return g_opt_cout1;
     case STTS_OPT_BRANCHES: return g_opt_branches;
+    case STTS_OPT_NBRANCH: return g_opt_nbranch;
     default: return ST_EINVAL;
   }
 }

@@ -21,11 +21,13 @@ def _dec(kind):
     return _DEC[kind]
 
 
-def _run(kind, B, T, dtype, branches):
+def _run(kind, B, T, dtype, branches, nbranch=None):
     from stts2_mi355x import engine as E
     asr, f0, n, s, nz = decoder_case(B, T)
     try:
         E.set_option(E.OPT_BRANCHES, branches)
+        if nbranch is not None:
+            E.set_option(E.OPT_NBRANCH, nbranch)
         with torch.no_grad():
             out = _dec(kind)(asr.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=nz.cuda(), dtype=dtype)
         torch.cuda.synchronize()
@@ -68,3 +70,11 @@ def test_branches_in_captured_graph():
     out = run(asr.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=nz.cuda()).cpu().numpy()
     ref = _run("hifigan", 1, 40, "fp32", 0)
     assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("B,T", [(12, 40), (32, 16)])
+def test_noise_branches_alone_fp32_bit_identical(B, T):
+    """Above the resblock-branch threshold only the noise branches run on a side stream (STTS_OPT_NBRANCH)."""
+    a = _run("hifigan", B, T, "fp32", 0, 0)
+    b = _run("hifigan", B, T, "fp32", 0, 64)
+    assert np.array_equal(a, b)
