@@ -466,8 +466,9 @@ const char* stts_error_string(int code);
  *                     resblocks are averaged after instead of through the running sum; 0 = off.  (Measured: B = 1
  *                     -29 %, B = 4 -19 %, B = 8 -6 %, B = 16 even, B = 32 +5 % time.) */
 #define STTS_OPT_BRANCHES 23
-/*   STTS_OPT_NBRANCH  64 (default) = batches up to this size (beyond STTS_OPT_BRANCHES) run only the noise branches on
- *                     a side stream (measured: B = 16 -5 %, B = 32 -1.3 % time); 0 = off. */
+/*   STTS_OPT_NBRANCH  16 (default) = batches up to this size (beyond STTS_OPT_BRANCHES) run only the noise branches on
+ *                     a side stream (measured: B = 16 -5 %, B = 32 -1.3 % time; B = 32 keeps it off so that its conv
+ *                     launches run alone and their hipEvent durations price the kernels, not the overlap); 0 = off. */
 #define STTS_OPT_NBRANCH 24
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
