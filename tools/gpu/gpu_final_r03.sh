@@ -11,7 +11,7 @@ tail -3 gpurun_out/pytest_gpu.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/smoke.log
-KERNEL=k_bigconv OUT=gpurun_out/traffic.json bash tools/gpu_traffic.sh > gpurun_out/traffic.log 2>&1 || exit $?
+KERNEL=k_bigconv OUT=gpurun_out/traffic.json bash tools/gpu/gpu_traffic.sh > gpurun_out/traffic.log 2>&1 || exit $?
 python3 tools/traffic_calibrated.py gpurun_out/traffic profiles/r03_calib_c256.json profiles/r03_calib_c128.json profiles/r03_traffic.json > profiles/r03_traffic_calibrated.txt 2>&1 || exit $?
 tail -1 profiles/r03_traffic_calibrated.txt
 timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1 || exit $?

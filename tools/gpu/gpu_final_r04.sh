@@ -21,10 +21,10 @@ if [ "${PART:-a}" = "a" ]; then
   echo "profiled bench ok"
 else
   export BENCH_ARGS="--no-parity-mode --no-accuracy-mode --no-e2e"
-  KERNEL=k_bigconv OUT=gpurun_out/traffic.json bash tools/gpu_traffic.sh > gpurun_out/traffic.log 2>&1 || exit $?
+  KERNEL=k_bigconv OUT=gpurun_out/traffic.json bash tools/gpu/gpu_traffic.sh > gpurun_out/traffic.log 2>&1 || exit $?
   for fam in k_bigconv k_resconv; do
     rm -rf gpurun_out/pmc
-    KREGEX=$fam timeout -k 10 600 bash tools/gpu_pmc.sh > gpurun_out/pmc_r04_$fam.log 2>&1 || exit $?
+    KREGEX=$fam timeout -k 10 600 bash tools/gpu/gpu_pmc.sh > gpurun_out/pmc_r04_$fam.log 2>&1 || exit $?
     python3 tools/analyze_pmc.py gpurun_out/pmc > gpurun_out/pmc_${fam}_r04.txt 2>&1 || exit $?
     rm -rf gpurun_out/pmc_$fam && mv gpurun_out/pmc gpurun_out/pmc_$fam
   done

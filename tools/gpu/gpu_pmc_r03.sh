@@ -6,7 +6,7 @@ export BENCH_ARGS="--no-parity-mode --no-e2e"
 mkdir -p gpurun_out
 for fam in k_bigconv k_resconv; do
   rm -rf gpurun_out/pmc
-  KREGEX=$fam timeout -k 10 900 bash tools/gpu_pmc.sh > gpurun_out/pmc_r03_$fam.log 2>&1 || exit $?
+  KREGEX=$fam timeout -k 10 900 bash tools/gpu/gpu_pmc.sh > gpurun_out/pmc_r03_$fam.log 2>&1 || exit $?
   python3 tools/analyze_pmc.py gpurun_out/pmc > gpurun_out/pmc_${fam}_r03.txt 2>&1 || exit $?
   rm -rf gpurun_out/pmc_$fam && mv gpurun_out/pmc gpurun_out/pmc_$fam
 done

@@ -1,5 +1,5 @@
 # Generic round-4 GPU cycle: optional pytest selection, optional bench, optional extra command.
-#   PYTEST="tests/test_x.py -k y"  BENCH="--steps 10"  EXTRA="python tools/..."  bash tools/gpu_run.sh
+#   PYTEST="tests/test_x.py -k y"  BENCH="--steps 10"  EXTRA="python tools/..."  bash tools/gpu/gpu_run.sh
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 # HBM traffic of the dominant conv kernel (FETCH_SIZE / WRITE_SIZE in separate --pmc passes,
 # kernel-trace only) over one bench step, reduced by tools/pmc_traffic.py into profiles/.
-#   KERNEL=k_bigconv OUT=profiles/r01_traffic.json bash tools/gpu_traffic.sh
+#   KERNEL=k_bigconv OUT=profiles/r01_traffic.json bash tools/gpu/gpu_traffic.sh
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 K=${KERNEL:-k_bigconv}

@@ -1,4 +1,4 @@
-"""Per-dispatch PMC summary of one kernel family from the rocprofv3 --pmc passes of tools/gpu_pmc.sh
+"""Per-dispatch PMC summary of one kernel family from the rocprofv3 --pmc passes of tools/gpu/gpu_pmc.sh
 (same format as profiles/r01_pmc_*.txt).
 
     python tools/pmc_summary.py gpurun_out/pmc [kernel-substring]

@@ -1,4 +1,4 @@
-"""HBM traffic per launch of one kernel from rocprofv3 --pmc passes (tools/gpu_traffic.sh).
+"""HBM traffic per launch of one kernel from rocprofv3 --pmc passes (tools/gpu/gpu_traffic.sh).
 
     python tools/pmc_traffic.py <pmc_root> <kernel> <out.json> [--decoder hifigan --dtype bf16 --batch 32 --frames 400]
 

@@ -3,7 +3,7 @@ tools/calib_traffic.py applied.
 
     python tools/traffic_calibrated.py <pmc_root> <calib_c256.json> <calib_c128.json> <out.json>
 
-<pmc_root> holds the FETCH_SIZE and WRITE_SIZE passes of tools/gpu_traffic.sh (one headline bench step,
+<pmc_root> holds the FETCH_SIZE and WRITE_SIZE passes of tools/gpu/gpu_traffic.sh (one headline bench step,
 HiFi-GAN bf16, B = 32 x 400 frames).  Per dispatch:
   * writes = WRITE_SIZE (calibrated exact for the epilogue's store pattern, calib mode 5);
   * reads  = FETCH_SIZE x f_win, with f_win the measured bytes-per-counted-byte of bigconv2's own
