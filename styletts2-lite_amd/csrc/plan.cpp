@@ -115,6 +115,9 @@ struct stts_model {
   // small-batch decoder: the stage's resblocks 1.. on side streams (decoder_forward), created on first use
   hipStream_t side[4] = {};
   hipEvent_t ev_fork = nullptr, ev_join[4] = {}, ev_fork2 = nullptr, ev_noise[8] = {};
+  // the side streams and events are per model: concurrent forwards of one model (with their own workspaces and
+  // streams) take turns through the forks and joins, so each wait sees its own forward's record
+  std::mutex branch_mu;
   stts_model() = default;
   stts_model(const stts_model&) = delete;
   stts_model& operator=(const stts_model&) = delete;
@@ -1159,6 +1162,8 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     g.bs = (long long)Ls[s] * Cs[s];
     return g;
   };
+  std::unique_lock<std::mutex> branch_lock;
+  if ((br || nbr) && !c.dry) branch_lock = std::unique_lock<std::mutex>(m.branch_mu);
   if (nbr) {
     // the noise branches' AdaIN layers read H (the style projections): computed before the fork
     RUN(st_linear(io.s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
