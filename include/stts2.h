@@ -372,6 +372,13 @@ int stts_weight_norm(const float* g, const float* v, int d0, int inner, float* w
 
 const char* stts_error_string(int code);
 
+/* ABI revision of this header and the library (STTS_ABI_VERSION).  Bumped on every incompatible change of an
+ * entry point's signature or meaning (5: round 5; 4 changed stts_adamw_step's scalars to double and added
+ * stts_mpd_losses / stts_msd_losses' scratch_bytes).  A caller binding by hand checks
+ * stts_abi_version() == STTS_ABI_VERSION before any other call; stts2_mi355x.engine.lib() does. */
+#define STTS_ABI_VERSION 5
+int stts_abi_version(void);
+
 /* Engine options (process-wide, take effect on the next launch):
  *   STTS_OPT_RESCONV  1 (default) = the specialised resblock conv engine serves the bf16
  *                     C = 32 / 64 dilated convs; 0 = the general implicit-GEMM engine serves them
@@ -466,9 +473,10 @@ const char* stts_error_string(int code);
  *                     resblocks are averaged after instead of through the running sum; 0 = off.  (Measured: B = 1
  *                     -29 %, B = 4 -19 %, B = 8 -6 %, B = 16 even, B = 32 +5 % time.) */
 #define STTS_OPT_BRANCHES 23
-/*   STTS_OPT_NBRANCH  16 (default) = batches up to this size (beyond STTS_OPT_BRANCHES) run only the noise branches on
- *                     a side stream (measured: B = 16 -5 %, B = 32 -1.3 % time; B = 32 keeps it off so that its conv
- *                     launches run alone and their hipEvent durations price the kernels, not the overlap); 0 = off. */
+/*   STTS_OPT_NBRANCH  64 (default) = batches up to this size (beyond STTS_OPT_BRANCHES) run only the noise branches on
+ *                     a side stream (measured: B = 16 -5 %, B = 32 -1.3 % time); 0 = off (bench.py's per-launch
+ *                     profiled pass sets 0, so that the conv launches run alone and their hipEvent durations price
+ *                     the kernels, not the overlap). */
 #define STTS_OPT_NBRANCH 24
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */

@@ -864,7 +864,7 @@ __global__ void __launch_bounds__(256) k_branch_avg(T* __restrict__ acc, BranchR
 }
 }  // namespace
 
-int g_opt_nbranch = 16;  // STTS_OPT_NBRANCH: the noise branches alone on a side stream up to this batch
+int g_opt_nbranch = 64;  // STTS_OPT_NBRANCH: the noise branches alone on a side stream up to this batch
 int g_opt_branches = 8;  // STTS_OPT_BRANCHES (plan.cpp decoder_forward): concurrent resblocks up to this batch
 
 int st_branch_avg(void* acc, const void* const* rs, int nr, float div, long long n, int dtype, hipStream_t s) {

@@ -1072,11 +1072,17 @@ int decoder_forward(Ctx& c, const DecIO& io) {
   // split accuracy mode (its two-pass C = 64 convs share the one fp32 partial buffer)
   const bool br = g_opt_branches > 0 && B <= g_opt_branches && nrb > 1 && nrb <= 5 && c.cdtype != ST_SPLIT;
   Buf GB[8];
-  if (br)
+  // each side-stream resblock also gets its own split-K scratch (the short-conv engine's fp32 partials,
+  // st_pw_split): branches that shared c.splitk would write and reduce their partial sums in the same memory
+  float* splitk_br[4] = {};
+  if (br) {
     for (int i = 0; i < 2 * (nrb - 1); ++i) {
       GB[i].p = c.alloc((size_t)B * smax * esz);
       GB[i].bs = smax;
     }
+    if (c.splitk_elems)
+      for (int j = 0; j + 1 < nrb; ++j) splitk_br[j] = reinterpret_cast<float*>(c.alloc((size_t)c.splitk_elems * 4));
+  }
   Buf HFR;  // S-sample frames of the source for the MFMA noise_convs (largest such stage)
   {
     int rows = 0;
@@ -1164,6 +1170,27 @@ int decoder_forward(Ctx& c, const DecIO& io) {
   };
   std::unique_lock<std::mutex> branch_lock;
   if ((br || nbr) && !c.dry) branch_lock = std::unique_lock<std::mutex>(m.branch_mu);
+  // forked side streams that are not joined back yet: an error return joins them (event on each side stream, the
+  // caller's stream waits), so that no side-stream work is left outside a hipGraph capture or still writing the
+  // workspace after the call returns
+  struct SideJoin {
+    hipStream_t main = nullptr;
+    hipStream_t s[4] = {};
+    hipEvent_t e[4] = {};
+    int n = 0;
+    void add(hipStream_t st, hipEvent_t ev) {
+      s[n] = st;
+      e[n] = ev;
+      ++n;
+    }
+    ~SideJoin() {
+      for (int i = 0; i < n; ++i) {
+        (void)hipEventRecord(e[i], s[i]);
+        (void)hipStreamWaitEvent(main, e[i], 0);
+      }
+    }
+  } join_noise, join_br;
+  join_noise.main = join_br.main = c.s;
   if (nbr) {
     // the noise branches' AdaIN layers read H (the style projections): computed before the fork
     RUN(st_linear(io.s, B, m.style_dim, c.aux_f(m.wt_off), c.aux_f(m.bcat_off), m.Htot, c.H, c.s));
@@ -1175,6 +1202,7 @@ int decoder_forward(Ctx& c, const DecIO& io) {
       if (!m.ev_fork2) ST_CHECK_HIP(hipEventCreateWithFlags(&m.ev_fork2, hipEventDisableTiming));
       ST_CHECK_HIP(hipEventRecord(m.ev_fork2, c.s));
       ST_CHECK_HIP(hipStreamWaitEvent(m.side[2], m.ev_fork2, 0));
+      join_noise.add(m.side[2], m.ev_noise[nup - 1]);
     }
     const hipStream_t s0 = c.s;
     float* const splitk0 = c.splitk;
@@ -1256,21 +1284,28 @@ int decoder_forward(Ctx& c, const DecIO& io) {
         }
         if (!m.ev_fork) ST_CHECK_HIP(hipEventCreateWithFlags(&m.ev_fork, hipEventDisableTiming));
         ST_CHECK_HIP(hipEventRecord(m.ev_fork, c.s));
-        for (int j = 0; j + 1 < nrb; ++j) ST_CHECK_HIP(hipStreamWaitEvent(m.side[j], m.ev_fork, 0));
+        for (int j = 0; j + 1 < nrb; ++j) {
+          ST_CHECK_HIP(hipStreamWaitEvent(m.side[j], m.ev_fork, 0));
+          join_br.add(m.side[j], m.ev_join[j]);
+        }
       }
       ST_CHECK(resblock1(c, m.resblocks[(size_t)s * nrb], X, S_x, R, XT, RO_ACC_FIRST, &ACC, nrb));
       const hipStream_t s0 = c.s;
+      float* const splitk0 = c.splitk;
       const void* rs[4];
       for (int j = 1; j < nrb; ++j) {
         Buf Rj = view(GB[2 * (j - 1)]), XTj = view(GB[2 * (j - 1) + 1]);
         if (!c.dry) c.s = m.side[j - 1];
+        c.splitk = splitk_br[j - 1];
         const int rc = resblock1(c, m.resblocks[(size_t)s * nrb + j], X, S_x, Rj, XTj, RO_PLAIN, nullptr, 0);
         c.s = s0;
+        c.splitk = splitk0;
         ST_CHECK(rc);
         rs[j - 1] = Rj.p;
       }
       // join, then ACC = ((ACC + R_1) + R_2 ...) / nrb
       if (!c.dry) {
+        join_br.n = 0;  // joined here
         for (int j = 0; j + 1 < nrb; ++j) {
           ST_CHECK_HIP(hipEventRecord(m.ev_join[j], m.side[j]));
           ST_CHECK_HIP(hipStreamWaitEvent(c.s, m.ev_join[j], 0));
@@ -1288,6 +1323,7 @@ int decoder_forward(Ctx& c, const DecIO& io) {
     Ccur = C;
     accsel = accsel == 4 ? 5 : 4;
   }
+  join_noise.n = 0;  // every stage waited for its noise branch: the side stream is joined
   // ---------------- output head
   if (!ist) {  // Snake(alpha_last) -> conv_post -> tanh  (hifigan.py:343-345)
     ConvParams p = conv_base(c, m.conv_post, xin, 0);
@@ -1960,6 +1996,8 @@ int stts_wave_preprocess(const float* wave, int B, long long L, long long wave_l
                          long long ws_bytes, void* stream) {
   return st_wave_preprocess(wave, B, L, wave_ld, mel, ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
+
+int stts_abi_version(void) { return STTS_ABI_VERSION; }
 
 const char* stts_error_string(int code) {
   switch (code) {

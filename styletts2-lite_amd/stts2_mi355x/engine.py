@@ -20,6 +20,7 @@ DTYPES = {"fp32": 0, "bf16": 1, "bf16x3": 2}  # bf16x3: the split-operand accura
 _LIB = None
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libstts2.so")
+ABI_VERSION = 5  # include/stts2.h STTS_ABI_VERSION: the signatures bound below
 
 c_int, c_ll, c_ull, c_vp, c_fp = ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_void_p, ctypes.c_void_p
 
@@ -33,6 +34,11 @@ def lib():
         raise RuntimeError(f"{LIB_PATH} missing: build it with `python -m stts2_mi355x.build` "
                            "(__graft_entry__.build()); there is no non-HIP fallback")
     L = ctypes.CDLL(LIB_PATH)
+    L.stts_abi_version.argtypes = []
+    L.stts_abi_version.restype = c_int
+    if L.stts_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: C-ABI revision {L.stts_abi_version()}, these bindings expect {ABI_VERSION} "
+                           "(include/stts2.h STTS_ABI_VERSION): rebuild the library")
     L.stts_model_create.argtypes = [c_int, ctypes.POINTER(c_int), c_int, ctypes.POINTER(c_vp)]
     L.stts_model_create.restype = c_int
     L.stts_model_destroy.argtypes = [c_vp]
@@ -191,7 +197,7 @@ OPT_NBRANCH = 24
 OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
                 OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1, OPT_SKEW: 0, OPT_FRONT: 1, OPT_PW: 1, OPT_SPLITK: 1,
                 OPT_EXP: 0, OPT_UPS: 1, OPT_WGRAD: 1, OPT_PLAINRC: 1, OPT_MSDFOLD: 1,
-                OPT_RCPP: 1, OPT_RESSPLIT: 1, OPT_BF16F: 0, OPT_YF32: 1, OPT_COUT1: 1, OPT_BRANCHES: 8, OPT_NBRANCH: 16}
+                OPT_RCPP: 1, OPT_RESSPLIT: 1, OPT_BF16F: 0, OPT_YF32: 1, OPT_COUT1: 1, OPT_BRANCHES: 8, OPT_NBRANCH: 64}
 # STTS_OPTS="KEY=VALUE,..." (A/B runs of whole suites): option values that replace the defaults for the process,
 # applied when the library loads and by reset_options()
 for _kv in filter(None, os.environ.get("STTS_OPTS", "").split(",")):

@@ -62,9 +62,12 @@ class AdamW(torch.optim.Optimizer):
                 t = st["step"]
                 if not t.is_cpu:  # (a checkpoint may carry the step on the device)
                     t = st["step"] = t.detach().to("cpu", torch.float32)
-                sn = self._step_views.get(t)
+                views = self.__dict__.get("_step_views")
+                if views is None:  # (not in Optimizer.__getstate__: a deep-copied / unpickled optimizer rebuilds it)
+                    views = self._step_views = weakref.WeakKeyDictionary()
+                sn = views.get(t)
                 if sn is None:
-                    sn = self._step_views[t] = t.numpy()
+                    sn = views[t] = t.numpy()
                 sn += 1
                 g = p.grad if p.grad.is_contiguous() and p.grad.dtype == torch.float32 else \
                     p.grad.float().contiguous()

@@ -577,7 +577,11 @@ def adain_resblk1d_frames(m, x, s, dtype="fp32"):
     scale in conv2's epilogue."""
     up = m.upsample if isinstance(getattr(m, "upsample", None), bool) else m.upsample_type != "none"
     # nn.Dropout(dropout_p) before each conv in train mode (models.py:335, 358-367; the predictor's blocks)
-    p_drop = float(getattr(m, "dropout_p", 0.0) or 0.0) if m.training else 0.0
+    # (the reference's AdainResBlk1d keeps only self.dropout = nn.Dropout(p), models.py:335: read its p then)
+    p_drop = getattr(m, "dropout_p", None)
+    if p_drop is None:
+        p_drop = getattr(getattr(m, "dropout", None), "p", 0.0)
+    p_drop = float(p_drop or 0.0) if m.training else 0.0
     r = adain_act(x, s, m.norm1.fc.weight, m.norm1.fc.bias, None, ACT_LRELU)
     if up:
         r = _PoolFn.apply(r, weight_norm(m.pool.weight_g, m.pool.weight_v), m.pool.bias)

@@ -29,7 +29,7 @@ def test_two_rank_launch_matches_one_rank(tmp_path):
     two, a2 = _run(2, tmp_path)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert two["config"]["global_batch"] == 6 and one["config"]["global_batch"] == 3
-    assert two["scaling"] == "weak" and "with_gather" in two
+    assert two["scaling"] == "weak" and "with_gather" in two and "with_scatter_gather" in two
     assert a2.shape == (6, 1, 2400)
     # weak scaling: rank r holds global utterances [3r, 3r + 3); the single-rank run is utterances 0-2
     assert np.array_equal(a2[:3], a1)

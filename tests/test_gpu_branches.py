@@ -78,3 +78,29 @@ def test_noise_branches_alone_fp32_bit_identical(B, T):
     a = _run("hifigan", B, T, "fp32", 0, 0)
     b = _run("hifigan", B, T, "fp32", 0, 64)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("B,T", [(1, 16), (2, 24)])
+def test_branches_bf16_general_engines_own_splitk(B, T):
+    """With the resblock engines off (STTS_OPT_RESCONV 0) the small-batch resblock convs take the general engines,
+    incl. the split-K short-conv path (st_pw_split) whose fp32 partials live in per-stream scratch: each side-stream
+    resblock has its own, so the concurrent branches equal the one-stream run within bf16 rounding of the average."""
+    from stts2_mi355x import engine as E
+
+    def run(branches):
+        asr, f0, n, s, nz = decoder_case(B, T)
+        try:
+            E.set_option(E.OPT_RESCONV, 0)
+            E.set_option(E.OPT_BRANCHES, branches)
+            E.set_option(E.OPT_NBRANCH, branches)
+            with torch.no_grad():
+                out = _dec("hifigan")(asr.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=nz.cuda(), dtype="bf16")
+            torch.cuda.synchronize()
+        finally:
+            E.reset_options()
+        return out.cpu().numpy()
+
+    a, b = run(0), run(8)
+    err = float(np.abs(a - b).max())
+    print(f"hifigan B={B} T={T} bf16 RESCONV=0 branches vs one stream: max-abs {err:.3e}")
+    assert np.isfinite(b).all() and err < 2e-2
