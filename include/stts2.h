@@ -478,6 +478,11 @@ int stts_abi_version(void);
  *                     profiled pass sets 0, so that the conv launches run alone and their hipEvent durations price
  *                     the kernels, not the overlap). */
 #define STTS_OPT_NBRANCH 24
+/*   STTS_OPT_BIGSPLIT 1 (default) = the accuracy mode's (STTS_SPLIT) C = 128 / 256 resblock convs, the front-end k3
+ *                     convs and ups[0] / ups[1] run on the bigconv2 engine's split-operand variant (16-channel
+ *                     groups, 3 MFMAs a product); 3 / 4 = the same on 4- / 8-wave blocks everywhere; 0 = the split
+ *                     implicit-GEMM engine (A/B). */
+#define STTS_OPT_BIGSPLIT 25
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

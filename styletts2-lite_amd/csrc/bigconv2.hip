@@ -23,6 +23,15 @@
 //   * Epilogue per tile from the accumulators: + residual, * out_scale, resblock average,
 //     bf16 stores, per-lane statistics reduced across the wave and added into LDS, flushed to
 //     the fp64 statistics when the workgroup leaves an utterance.
+//
+// SP (the split-operand accuracy mode, STTS_SPLIT): fp32 activations, every operand v = hi + lo
+// with hi = bf16(v), lo = bf16(v - hi), products W_hi X_hi + W_lo X_hi + W_hi X_lo on the same MFMA.  A group
+// is then 16 input channels instead of 32, and every LDS image keeps its byte layout: a window row holds
+// [X_hi 0-7 | X_hi 8-15 | X_lo 0-7 | X_lo 8-15] where the bf16 kernel holds channels 0-31 (the raw fp32 window
+// of 16 channels is the same 64 B a row, transformed in place into its hi / lo halves), and a weight slot
+// [W_hi | W_lo] of 16 input channels where the bf16 kernel holds 32 (gathered by the LDS-DMA from the packed
+// hi and lo copies).  So the fragment reads, the DMA counts and the LDS budget are the bf16 kernel's; a tap
+// issues 24 MFMAs on the same 2 weight + 16 window fragments instead of 16, and the epilogue stores fp32.
 #include "common.h"
 #include "conv_common.h"
 #include "kernels.h"
@@ -169,14 +178,16 @@ __device__ __forceinline__ uint4 f32_to_bf8v(const float* v) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false>
 __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS>;
   constexpr int NXB = G::NXB;
   constexpr int TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
   constexpr int NCF = G::NCOEF;
   // input-channel groups: C / 32 for the square resblock convs, ceil(Cin / 32) for the front-end
-  const int NG = (PRO == PK_SNAKE && CINP == C) ? C / 32 : (p.Cin + 31) / 32;
+  // (SP: 16-channel groups)
+  constexpr int GW = SP ? 16 : 32;
+  const int NG = (PRO == PK_SNAKE && CINP == C) ? C / GW : (p.Cin + GW - 1) / GW;
   constexpr int NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* coef = reinterpret_cast<float*>(smem + G::OFF_COEF);
@@ -229,33 +240,52 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 
   // ---------------- weights: step s = (group, tap) -> this wave's 2 KB slice, slot s % RS
   char* wring = smem + G::OFF_W + wu * RS * 2048;
-  const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)NG * K * C * 32 * 2));
+  // (SP: the packed hi copy, then the lo copy, each of p.nchunks 32-channel chunks)
+  const unsigned wcopy = SP ? (unsigned)((size_t)p.nchunks * K * C * 32 * 2) : 0u;
+  const Rsrc rw = make_rsrc(p.w, SP ? 2u * wcopy : (unsigned)((size_t)NG * K * C * 32 * 2));
   // (group index gi, output part ch and tap t of the step: from the group cursors below, so no
   // runtime division by the group count runs per step)
   auto issue_w = [&](int s, int gi, int ch, int t) __attribute__((always_inline)) {
     if (dbg & 8) return;
-    const unsigned base = (unsigned)((((size_t)gi * K + t) * C + ch * NCO + 32 * cb) * 64) + lane * 16;
     char* dst = wring + (s % RS) * 2048;
-    glds16(rw, dst, base);
-    glds16(rw, dst + 1024, base + 1024);
+    if constexpr (SP) {
+      // slot byte P = lane's 16 B of half hf: row n = P / 64 (output channel 32 cb + n of part ch), physical
+      // unit P / 16 % 4 = logical unit lu ^ sw (sw = (n >> 2) & 3, the packed layout's own swizzle), logical
+      // unit lu = [hi 0-7, hi 8-15, lo 0-7, lo 8-15] of the group's 16 channels: 32-channel chunk gi / 2,
+      // logical unit 2 (gi & 1) + (lu & 1) of the packed row in copy lu / 2
+      const int c32 = gi >> 1, h16 = gi & 1;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int n = hf * 16 + (lane >> 2), sw = (n >> 2) & 3, lu = (lane & 3) ^ sw;
+        const int pu = (2 * h16 + (lu & 1)) ^ sw;
+        const unsigned off = ((lu >> 1) ? wcopy : 0u) +
+                             (unsigned)((((size_t)c32 * K + t) * C + ch * NCO + 32 * cb + n) * 64 + pu * 16);
+        glds16(rw, dst + hf * 1024, off);
+      }
+    } else {
+      const unsigned base = (unsigned)((((size_t)gi * K + t) * C + ch * NCO + 32 * cb) * 64) + lane * 16;
+      glds16(rw, dst, base);
+      glds16(rw, dst + 1024, base + 1024);
+    }
   };
 
   // ---------------- window: group gg -> raw rows [gr0, gr0 + WROWS) of its 32 channels, buffer gg & 1
   // LDS unit pidx = row * 4 + u' holds logical 16-B unit u = u' ^ ((row >> 2) & 3) of that row
   auto issue_x = [&](int gg, int gi, int b, int mt) __attribute__((always_inline)) {
     if (dbg & 16) return;
-    const Rsrc rx = make_rsrc(reinterpret_cast<const bf16_t*>(p.x) + (size_t)b * p.x_bs,
-                              (unsigned)((size_t)p.Lin * p.x_ld * 2));
+    constexpr unsigned ES = SP ? 4u : 2u;  // element bytes (SP: fp32 frames, 4 channels a 16-B unit)
+    const Rsrc rx = make_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)b * p.x_bs * ES,
+                              (unsigned)((size_t)p.Lin * p.x_ld * ES));
     const int gr0 = mt * TM - G::PAD;
     char* dst = smem + G::OFF_X + (gg % NXB) * (G::WROWS * 64);
 #pragma unroll
     for (int j = 0; j < NWIN; ++j) {
       const int pidx = (j * NW + wu) * 64 + lane;
       const int r = pidx >> 2, u = (pidx & 3) ^ ((r >> 2) & 3);
-      const int e = (gr0 + r) * p.x_ld + gi * 32 + 8 * u;
+      const int e = (gr0 + r) * p.x_ld + gi * GW + (16 / (int)ES) * u;
       // rows past the window (WROWS rounds R up to whole DMA instructions) read out of range: no
       // HBM traffic for them (profiles/r02_pmc_bigconv.txt measured 1.5x the window bytes)
-      glds16(rx, dst + (j * NW + wu) * 1024, (e >= 0 && r < G::R) ? (unsigned)e * 2u : OOB);
+      glds16(rx, dst + (j * NW + wu) * 1024, (e >= 0 && r < G::R) ? (unsigned)e * ES : OOB);
     }
   };
   // AdaIN + Snake coefficients of utterance b into parity slot b & 1 (see bigconv.hip)
@@ -292,8 +322,76 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   auto transform = [&](int gg, int gi, int b, int mt) __attribute__((always_inline)) {
     if (dbg & 1) return;
     const int gr0 = mt * TM - G::PAD;
-    const float* cf = coef + (b & 1) * NCF * CINP + gi * 32 + 8 * my_u;
     char* buf = smem + G::OFF_X + (gg % NXB) * (G::WROWS * 64);
+    if constexpr (SP) {
+      // the lane's unit holds fp32 channels 4 my_u .. 4 my_u + 3 of its row; after the prologue their hi parts go
+      // to logical unit my_u / 2 and their lo parts to logical unit 2 + my_u / 2, at byte 8 (my_u & 1) of the unit
+      // (the row's other three lanes write the rest of it: each lane reads its whole unit before the row's writes,
+      // in program order of the one wave that owns the row)
+      const int sw = (lane >> 4) & 3;  // the row's swizzle, (r >> 2) & 3 for every row this lane owns
+      const unsigned o_hi = (unsigned)((((my_u >> 1) ^ sw) * 16) + (my_u & 1) * 8 - (lane & 3) * 16);
+      const unsigned o_lo = (unsigned)((((2 + (my_u >> 1)) ^ sw) * 16) + (my_u & 1) * 8 - (lane & 3) * 16);
+      const float* cf = coef + (b & 1) * NCF * CINP + gi * 16 + 4 * my_u;
+      if constexpr (PRO == PK_LRELU) {
+        f32x4v m2, a;
+        lds_coef2(lds_addr(cf), m2, a, (unsigned)(CINP * 4));
+        const float am[4] = {m2.x, m2.y, m2.z, m2.w}, aa[4] = {a.x, a.y, a.z, a.w};
+        const float slope = (p.pro.mode & PRO_LRELU) ? p.pro.slope : 1.0f;
+        const int c0 = gi * 16 + 4 * my_u;
+#pragma unroll
+        for (int j = 0; j < NWIN; ++j) {
+          const int pidx = (j * NW + wu) * 64 + lane;
+          const int r = pidx >> 2;
+          const unsigned ua = lds_addr(buf + pidx * 16);
+          const float4 raw = *reinterpret_cast<const float4*>(buf + pidx * 16);
+          float v[4] = {raw.x, raw.y, raw.z, raw.w};
+          const bool pad = (unsigned)(gr0 + r) >= (unsigned)p.Lin;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x2 = __builtin_fmaf(v[e], aa[e], am[e]);
+            // channels >= Cin (the last group's padding, whose memory may hold anything) are forced to 0
+            v[e] = (c0 + e < p.Cin && !pad) ? (x2 > 0.f ? x2 : x2 * slope) : 0.f;
+          }
+          float h[4], l[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            h[e] = (float)(bf16_t)v[e];
+            l[e] = v[e] - h[e];
+          }
+          lds_write_b64(ua + o_hi, f32_to_bf4(h));
+          lds_write_b64(ua + o_lo, f32_to_bf4(l));
+        }
+      } else {
+        f32x4v m2, a, ar, mr, nia;
+        lds_coef5(lds_addr(cf), m2, a, ar, mr, nia, (unsigned)(CINP * 4));
+        const float am[4] = {m2.x, m2.y, m2.z, m2.w}, aa[4] = {a.x, a.y, a.z, a.w};
+        const float aar[4] = {ar.x, ar.y, ar.z, ar.w}, amr[4] = {mr.x, mr.y, mr.z, mr.w};
+        const float ani[4] = {nia.x, nia.y, nia.z, nia.w};
+#pragma unroll
+        for (int j = 0; j < NWIN; ++j) {
+          const int pidx = (j * NW + wu) * 64 + lane;
+          const int r = pidx >> 2;
+          if (G::WROWS > G::R && r >= G::R) continue;  // padding rows: never read by a tap
+          const unsigned ua = lds_addr(buf + pidx * 16);
+          const float4 raw = *reinterpret_cast<const float4*>(buf + pidx * 16);
+          float v[4] = {raw.x, raw.y, raw.z, raw.w};
+          const bool pad = (unsigned)(gr0 + r) >= (unsigned)p.Lin;
+          float h[4], l[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x2 = __builtin_fmaf(v[e], aa[e], am[e]);
+            const float c = __builtin_amdgcn_cosf(__builtin_fmaf(v[e], aar[e], amr[e]));
+            const float y = pad ? 0.f : __builtin_fmaf(c, ani[e], x2);  // zero padding is post-prologue
+            h[e] = (float)(bf16_t)y;
+            l[e] = y - h[e];
+          }
+          lds_write_b64(ua + o_hi, f32_to_bf4(h));
+          lds_write_b64(ua + o_lo, f32_to_bf4(l));
+        }
+      }
+      return;
+    }
+    const float* cf = coef + (b & 1) * NCF * CINP + gi * 32 + 8 * my_u;
     if constexpr (PRO == PK_LRELU) {
     // (in chunks of at most 3 units: C = 128's 5 units at once spill)
     constexpr int JC = NWIN < 3 ? NWIN : 3;
@@ -381,7 +479,9 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   };
 
   f32x16 acc[8];
-  constexpr int NST = 16;  // vector-memory stores of one epilogue (8 fragments x 2)
+  constexpr int NU = SP ? 4 : 2;  // 16-B units of a lane's 16 output channels (SP: fp32)
+  constexpr unsigned OES = SP ? 4u : 2u;  // output / residual element bytes
+  constexpr int NST = 8 * NU;  // vector-memory stores of one epilogue (8 fragments x NU)
   auto epilogue = [&](int b, int mt, int ch) __attribute__((always_inline)) {
     const int q0 = mt * TM + fh * 256 + l32;
     // the lane's 16 consecutive output channels (packing permutation)
@@ -390,11 +490,11 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     const int ph = UPS ? co0 / p.Cout : 0, c0 = UPS ? co0 - ph * p.Cout : co0;
     const int Lrows = UPS ? p.Lout : p.Lq;
     auto orow = [&](int q) __attribute__((always_inline)) { return UPS ? q * p.up + ph - p.opad : q; };
-    const Rsrc ry = make_rsrc(reinterpret_cast<bf16_t*>(p.y) + (size_t)b * p.y_bs, (unsigned)((size_t)Lrows * p.y_ld * 2));
-    const Rsrc rr = make_rsrc(RES ? reinterpret_cast<const bf16_t*>(p.res) + (size_t)b * p.res_bs : nullptr,
-                              RES ? (unsigned)((size_t)Lrows * p.res_ld * 2) : 0u);
-    const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const bf16_t*>(p.accb) + (size_t)b * p.acc_bs : nullptr,
-                              ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * 2) : 0u);
+    const Rsrc ry = make_rsrc(reinterpret_cast<char*>(p.y) + (size_t)b * p.y_bs * OES, (unsigned)((size_t)Lrows * p.y_ld * OES));
+    const Rsrc rr = make_rsrc(RES ? reinterpret_cast<const char*>(p.res) + (size_t)b * p.res_bs * OES : nullptr,
+                              RES ? (unsigned)((size_t)Lrows * p.res_ld * OES) : 0u);
+    const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const char*>(p.accb) + (size_t)b * p.acc_bs * OES : nullptr,
+                              ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * OES) : 0u);
     const float osc = p.out_scale;
     const float adiv = (ACC && p.acc_div != 0.f) ? 1.0f / p.acc_div : 1.0f;
     float ts[16], tq[16];
@@ -409,24 +509,42 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     lap(7);
     // (EPI1: a residual-only epilogue loads all 8 fragments in one batch, into the registers the dead
     // tap fragments held: one load latency per tile instead of two; STTS_OPT_EXP bit 2)
-    constexpr int NB = (RES && !(EPI1 && !ACC)) ? 2 : 1, FB = 8 / NB;
-    uint4 rl[FB][2], al[FB][2];
-    auto finish = [&](int f, const uint4 (&r2)[2], const uint4 (&a2)[2]) __attribute__((always_inline)) {
+    // (SP: fp32 residual / running-sum rows, 64 B per fragment: 4 fragments a batch with a residual only, 2 with a
+    // residual and a running sum)
+    constexpr int NB = SP ? (RES ? (ACC ? 4 : 2) : 1) : ((RES && !(EPI1 && !ACC)) ? 2 : 1), FB = 8 / NB;
+    uint4 rl[FB][NU], al[FB][NU];
+    auto unpack16 = [&](const uint4 (&u)[NU], float (&o)[16]) __attribute__((always_inline)) {
+      if constexpr (SP) {
+        __builtin_memcpy(o, u, 64);
+      } else {
+        bf8_to_f32v(u[0], o);
+        bf8_to_f32v(u[1], o + 8);
+      }
+    };
+    auto finish = [&](int f, const uint4 (&r2)[NU], const uint4 (&a2)[NU]) __attribute__((always_inline)) {
       f32x16& v = acc[f];  // in place: the accumulators of a finished tile are the output
       const int q = q0 + 32 * f;
       if constexpr (RES) {
         float r0[16];
-        bf8_to_f32v(r2[0], r0);
-        bf8_to_f32v(r2[1], r0 + 8);
+        unpack16(r2, r0);
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = (v[r] + r0[r]) * osc;
       }
       if constexpr (ACC) {
         float a0[16];
-        bf8_to_f32v(a2[0], a0);
-        bf8_to_f32v(a2[1], a0 + 8);
+        unpack16(a2, a0);
+        if constexpr (SP) {  // the reference divides (xs / num_kernels, hifigan.py:342), as the fp32 engines
+          if (p.acc_div != 0.f) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = (a0[r] + v[r]) * adiv;
+            for (int r = 0; r < 16; ++r) v[r] = (a0[r] + v[r]) / p.acc_div;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = a0[r] + v[r];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = (a0[r] + v[r]) * adiv;
+        }
       }
       float o[16];
 #pragma unroll
@@ -435,9 +553,18 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
         // (an LDS-transposed variant writing 16 rows x 64 contiguous bytes per store measured the
         // same in the decoder: the stores are bound by the chip-wide write burst, not by requests)
         // rows past the output (and UPS rows before frame 0: negative offsets) fall outside the descriptor
-        const unsigned ey = (unsigned)(orow(q) * p.y_ld + c0) * 2u;
-        bstore16(ry, ey, f32_to_bf8v(o));
-        bstore16(ry, ey + 16u, f32_to_bf8v(o + 8));
+        const unsigned ey = (unsigned)(orow(q) * p.y_ld + c0) * OES;
+        if constexpr (SP) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            uint4 w;
+            __builtin_memcpy(&w, o + 4 * i, 16);
+            bstore16(ry, ey + 16u * i, w);
+          }
+        } else {
+          bstore16(ry, ey, f32_to_bf8v(o));
+          bstore16(ry, ey + 16u, f32_to_bf8v(o + 8));
+        }
       }
       if (!ACC) {
         const float m = (unsigned)orow(q) < (unsigned)Lrows ? 1.f : 0.f;
@@ -455,14 +582,14 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       for (int k = 0; k < FB; ++k) {
         const int q = q0 + 32 * (nb * FB + k);
         if constexpr (RES) {
-          const unsigned er = (unsigned)((UPS ? orow(q) : (q >> p.res_shift)) * p.res_ld + c0) * 2u;
-          rl[k][0] = bload16(rr, er);
-          rl[k][1] = bload16(rr, er + 16u);
+          const unsigned er = (unsigned)((UPS ? orow(q) : (q >> p.res_shift)) * p.res_ld + c0) * OES;
+#pragma unroll
+          for (int i = 0; i < NU; ++i) rl[k][i] = bload16(rr, er + 16u * i);
         }
         if constexpr (ACC) {
-          const unsigned ea = (unsigned)(q * p.acc_ld + co0) * 2u;
-          al[k][0] = bload16(ra, ea);
-          al[k][1] = bload16(ra, ea + 16u);
+          const unsigned ea = (unsigned)(q * p.acc_ld + co0) * OES;
+#pragma unroll
+          for (int i = 0; i < NU; ++i) al[k][i] = bload16(ra, ea + 16u * i);
         }
       }
       asm volatile("" ::: "memory");
@@ -647,7 +774,22 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       {
         const bf16x8(&a)[2] = fa[t & 1];
         // half 0 of tap t; reads of half 1
-        {
+        // (SP: fb0 = X_hi, fb1 = X_lo, a[0] = W_hi, a[1] = W_lo: W_hi X_hi + W_lo X_hi here, W_hi X_lo in half 1)
+        if constexpr (SP) {
+          int u;
+          const char* row = brow(gw, t, 1, u);
+#pragma unroll
+          for (int f = 0; f < 8; ++f) {
+            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], fb0[f], acc[f], 0, 0, 0);
+            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb0[f], acc[f], 0, 0, 0);
+            fb1[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+        } else {
           int u;
           const char* row = brow(gw, t, 1, u);
 #pragma unroll
@@ -657,13 +799,14 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           }
           interleave(8);
         }
+        const bf16x8& a1 = SP ? a[0] : a[1];  // the second half's weight fragment
         // half 1 of tap t; reads of half 0 of tap t+1 and, once its DMA is in, of its weights
         if (t + 1 < K) {
           int u;
           const char* row = brow(gw, t + 1, 0, u);
 #pragma unroll
           for (int f = 0; f < 4; ++f) {
-            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb1[f], acc[f], 0, 0, 0);
+            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fb1[f], acc[f], 0, 0, 0);
             fb0[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
           }
           interleave(4);
@@ -680,13 +823,13 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           rd_a(s + 1, fa[(t + 1) & 1]);
 #pragma unroll
           for (int f = 4; f < 8; ++f) {
-            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb1[f], acc[f], 0, 0, 0);
+            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fb1[f], acc[f], 0, 0, 0);
             fb0[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
           }
           interleave(4);
         } else {
 #pragma unroll
-          for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb1[f], acc[f], 0, 0, 0);
+          for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fb1[f], acc[f], 0, 0, 0);
         }
       }
       // the next window: this wave's DMAs of it are older than the weight DMAs of taps 0..t.  With two
@@ -723,10 +866,10 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
   using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -749,30 +892,30 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-template <int C, int NW, int K, bool OFS = false>
+template <int C, int NW, int K, bool OFS = false, bool SP = false>
 int launch_b2_k(const ConvParams& p, hipStream_t s) {
   if (!p.res) {  // conv1 of an iteration: dilation 1 / 3 / 5, no residual
     if (p.accb) return ST_EINVAL;
     switch (p.dil) {
-      case 1: return launch_b2<C, NW, K, 1, false, false, PK_SNAKE, C, false, false, C, OFS>(p, s);
-      case 3: return launch_b2<C, NW, K, 3, false, false, PK_SNAKE, C, false, false, C, OFS>(p, s);
-      case 5: return launch_b2<C, NW, K, 5, false, false, PK_SNAKE, C, false, false, C, OFS>(p, s);
+      case 1: return launch_b2<C, NW, K, 1, false, false, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
+      case 3: return launch_b2<C, NW, K, 3, false, false, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
+      case 5: return launch_b2<C, NW, K, 5, false, false, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
       default: return ST_EINVAL;
     }
   }
   if (p.dil != 1) return ST_EINVAL;  // conv2: dilation 1, residual, optionally the resblock sum
-  if (p.accb) return launch_b2<C, NW, K, 1, true, true, PK_SNAKE, C, false, false, C, OFS>(p, s);
-  if constexpr (!OFS)
+  if (p.accb) return launch_b2<C, NW, K, 1, true, true, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
+  if constexpr (!OFS && !SP)
     if (g_opt_exp & 2) return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, true>(p, s);
-  return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, false, false, C, OFS>(p, s);
+  return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
 }
 
-template <int C, int NW, bool OFS = false>
+template <int C, int NW, bool OFS = false, bool SP = false>
 int launch_b2_c(const ConvParams& p, hipStream_t s) {
   switch (p.KS) {
-    case 3: return launch_b2_k<C, NW, 3, OFS>(p, s);
-    case 7: return launch_b2_k<C, NW, 7, OFS>(p, s);
-    case 11: return launch_b2_k<C, NW, 11, OFS>(p, s);
+    case 3: return launch_b2_k<C, NW, 3, OFS, SP>(p, s);
+    case 7: return launch_b2_k<C, NW, 7, OFS, SP>(p, s);
+    case 11: return launch_b2_k<C, NW, 11, OFS, SP>(p, s);
     default: return ST_EINVAL;
   }
 }
@@ -873,5 +1016,43 @@ bool st_ups_eligible(const ConvParams& p, int dtype) {
 int st_bigconv2_ups(const ConvParams& p, hipStream_t s) {
   if (p.N == 2560 && p.Cout == 256) return launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256>(p, s);
   if (p.N == 640 && p.Cout == 128) return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128>(p, s);
+  return ST_EINVAL;
+}
+
+// ---- the split-operand accuracy mode (STTS_SPLIT, dtype ST_SPLIT: fp32 frames, bf16 hi + lo operands) on this
+// engine (SP): the C = 128 / 256 resblock convs, the front-end k3 convs and ups[0] / ups[1], which ran on the split
+// conv1d_igemm (STTS_OPT_BIGSPLIT, default on; 0 = the split igemm, A/B)
+int g_opt_bigsplit = 1;
+
+bool st_bigsplit_eligible(const ConvParams& p, int dtype) {
+  if (!g_opt_bigsplit || dtype != ST_SPLIT) return false;
+  // the bf16 engines' shape rules (frames ld multiples of 8 elements: 32-B aligned fp32 rows)
+  return st_bigconv_eligible(p, ST_BF16) || st_front_eligible(p, ST_BF16) || st_ups_eligible(p, ST_BF16);
+}
+
+int st_bigsplit(const ConvParams& p, hipStream_t s) {
+  if (st_ups_eligible(p, ST_BF16)) {
+    if (p.N == 2560 && p.Cout == 256)
+      return launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256, false, true>(p, s);
+    if (p.N == 640 && p.Cout == 128)
+      return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128, false, true>(p, s);
+    return ST_EINVAL;
+  }
+  if (st_front_eligible(p, ST_BF16)) {
+    if (p.Cout == 1024)
+      return p.res ? launch_b2<1024, 8, 3, 1, true, false, PK_LRELU, FE_CINP, false, false, 1024, false, true>(p, s)
+                   : launch_b2<1024, 8, 3, 1, false, false, PK_LRELU, FE_CINP, false, false, 1024, false, true>(p, s);
+    if (p.Cout == 512)
+      return p.res ? launch_b2<512, 8, 3, 1, true, false, PK_LRELU, FE_CINP, false, false, 512, false, true>(p, s)
+                   : launch_b2<512, 8, 3, 1, false, false, PK_LRELU, FE_CINP, false, false, 512, false, true>(p, s);
+    return ST_EINVAL;
+  }
+  // resblock convs: 4-wave blocks (two per CU) where the bf16 engine takes them (few tiles, C = 128 k7 / k11)
+  const int tm8 = p.Cout == 128 ? 512 : 256;
+  const long long tiles8 = (long long)((p.Lq + tm8 - 1) / tm8) * p.B;
+  // (STTS_OPT_BIGSPLIT 3 = 4-wave blocks everywhere, 4 = 8-wave blocks everywhere: tests)
+  const bool two = g_opt_bigsplit != 4 && (tiles8 < b2_num_cu() || (p.Cout == 128 && p.KS >= 7) || g_opt_bigsplit == 3);
+  if (p.Cout == 128) return two ? launch_b2_c<128, 4, false, true>(p, s) : launch_b2_c<128, 8, false, true>(p, s);
+  if (p.Cout == 256) return two ? launch_b2_c<256, 4, false, true>(p, s) : launch_b2_c<256, 8, false, true>(p, s);
   return ST_EINVAL;
 }

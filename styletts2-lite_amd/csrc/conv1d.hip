@@ -898,6 +898,7 @@ int st_conv1d_engine(const ConvParams& p, int dtype) {
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
   if (st_pw_split_eligible(q, dtype) || st_pw_eligible(q, dtype)) return ST_ENGINE_PW;
   if (st_ressplit_eligible(q, dtype)) return ST_ENGINE_RESSPLIT;
+  if (st_bigsplit_eligible(q, dtype)) return ST_ENGINE_BIGSPLIT;
   return ST_ENGINE_IGEMM;
 }
 
@@ -926,6 +927,7 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (st_pw_split_eligible(q, dtype)) return st_pw_split(q, stream);
   if (st_pw_eligible(q, dtype)) return st_pw(q, stream);
   if (st_ressplit_eligible(q, dtype)) return st_ressplit(q, stream);
+  if (st_bigsplit_eligible(q, dtype)) return st_bigsplit(q, stream);
   if (dtype == ST_FP32) return launch_typed<float, float>(q, stream);
   if (dtype == ST_BF16) {
     return launch_typed<bf16_t, bf16_t>(q, stream);

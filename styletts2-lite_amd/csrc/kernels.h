@@ -76,11 +76,16 @@ __device__ __forceinline__ double* stats_slot(const ConvParams& p, int g) {
 int st_stats_fold(double* stats, int B, int ld, int C, int slots, long long slot_bs, hipStream_t s);
 // which engine st_conv1d routes p to (profiling records; bench.py names the dominant kernel)
 enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2, ST_ENGINE_RESFUSED = 3, ST_ENGINE_HEAD = 4,
-       ST_ENGINE_PW = 5, ST_ENGINE_RESSPLIT = 6 };
+       ST_ENGINE_PW = 5, ST_ENGINE_RESSPLIT = 6, ST_ENGINE_BIGSPLIT = 7 };
 // split-operand (ST_SPLIT) resblock convs, C = 32 / 64 (ressplit.hip; C = 64 needs p.splitk_ws >= B Lq 64 floats)
 bool st_ressplit_eligible(const ConvParams& p, int dtype);
 int st_ressplit(const ConvParams& p, hipStream_t stream);
 extern int g_opt_ressplit;
+// split-operand (ST_SPLIT) C = 128 / 256 resblock convs, front-end k3 convs, ups[0] / ups[1] on the bigconv2
+// engine (bigconv2.hip, SP)
+bool st_bigsplit_eligible(const ConvParams& p, int dtype);
+int st_bigsplit(const ConvParams& p, hipStream_t stream);
+extern int g_opt_bigsplit;  // STTS_OPT_BIGSPLIT
 int st_conv1d_engine(const ConvParams& p, int dtype);
 // resblock conv engine (resconv.hip): bf16, C = 32 / 64, 1-D 'same' dilated conv with the
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.

@@ -120,3 +120,28 @@ def test_ressplit_engine_ab(B, T):
     err = np.abs(out - ref).max()
     print(f"ressplit A/B B={B} T={T}: max-abs {err:.3e}")
     assert err < 2e-5
+
+
+@pytest.mark.parametrize("B,T,mode,front", [(2, 40, 1, 2), (1, 400, 1, 1), (3, 64, 4, 2), (2, 48, 3, 2)])
+def test_bigsplit_engine_ab(B, T, mode, front):
+    """The split variant of the bigconv2 engine (bigconv2.hip SP: 16-channel groups of bf16 hi + lo windows and
+    weights, 3 MFMAs a product; the C = 128 / 256 resblock convs, the front-end k3 convs, ups[0] / ups[1]) against
+    the split igemm engine on the same decode (STTS_OPT_BIGSPLIT 0): the same split arithmetic in a different
+    summation order.  Modes: production routing, 8-wave blocks everywhere (4), 4-wave blocks everywhere (3);
+    STTS_OPT_FRONT 2 forces the front-end engine at these small sizes."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_FRONT, front)
+        E.set_option(E.OPT_BIGSPLIT, 0)
+        ref = _run("hifigan", B, T, "bf16x3")
+        E.set_option(E.OPT_BIGSPLIT, mode)
+        out = _run("hifigan", B, T, "bf16x3")
+    finally:
+        E.reset_options()
+    err = np.abs(out - ref).max()
+    g = golden(f"hifigan_T{T}_B1")["out"][0] if T in (16, 40, 400) and B == 1 else None
+    print(f"bigsplit A/B B={B} T={T} mode {mode}: max-abs {err:.3e}"
+          + (f", vs reference golden {np.abs(out[0] - g).max():.3e}" if g is not None else ""))
+    assert np.isfinite(out).all() and err < 2e-5
+    if g is not None:
+        assert np.abs(out[0] - g).max() < 1e-3
