@@ -319,7 +319,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   // The lane's NWIN units are read first (one LDS latency), transformed per 4-channel half with
   // that half's coefficients, and written back with one 16-B store each.  Padding rows past R
   // are transformed too (their DMA read zeros; no tap reads them): no per-unit branch.
-  auto transform = [&](int gg, int gi, int b, int mt) __attribute__((always_inline)) {
+  auto transform = [&](int gg, int gi, int b, int mt, int ja = 0, int jb = G::NWIN) __attribute__((always_inline)) {
     if (dbg & 1) return;
     const int gr0 = mt * TM - G::PAD;
     char* buf = smem + G::OFF_X + (gg % NXB) * (G::WROWS * 64);
@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
         const float slope = (p.pro.mode & PRO_LRELU) ? p.pro.slope : 1.0f;
         const int c0 = gi * 16 + 4 * my_u;
 #pragma unroll
-        for (int j = 0; j < NWIN; ++j) {
+        for (int j = ja; j < jb; ++j) {
           const int pidx = (j * NW + wu) * 64 + lane;
           const int r = pidx >> 2;
           const unsigned ua = lds_addr(buf + pidx * 16);
@@ -368,7 +368,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
         const float aar[4] = {ar.x, ar.y, ar.z, ar.w}, amr[4] = {mr.x, mr.y, mr.z, mr.w};
         const float ani[4] = {nia.x, nia.y, nia.z, nia.w};
 #pragma unroll
-        for (int j = 0; j < NWIN; ++j) {
+        for (int j = ja; j < jb; ++j) {
           const int pidx = (j * NW + wu) * 64 + lane;
           const int r = pidx >> 2;
           if (G::WROWS > G::R && r >= G::R) continue;  // padding rows: never read by a tap
@@ -448,7 +448,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       const float aar[4] = {ar.x, ar.y, ar.z, ar.w}, amr[4] = {mr.x, mr.y, mr.z, mr.w};
       const float ani[4] = {nia.x, nia.y, nia.z, nia.w};
 #pragma unroll
-      for (int j = 0; j < NWIN; ++j) {
+      for (int j = ja; j < jb; ++j) {
         const int pidx = (j * NW + wu) * 64 + lane;
         const int r = pidx >> 2;
         if (G::WROWS > G::R && r >= G::R) continue;  // padding rows: never read by a tap

@@ -56,6 +56,10 @@ def main():
             step_ms[v].append(ev0.elapsed_time(ev1))
             if r == 0:
                 outs[v] = out.cpu().clone()
+            # per-launch events price each kernel alone: the noise branches stay on the caller's stream in this pass
+            # (unless the option under test is STTS_OPT_NBRANCH itself)
+            if a.opt != E.OPT_NBRANCH:
+                E.set_option(E.OPT_NBRANCH, 0)
             E.profile_enable(True)
             eng.forward(asr, f0, n, s, seed=5, out=out)
             torch.cuda.synchronize()
