@@ -141,20 +141,54 @@ int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, double lr, 
 
 /* ---- ProsodyPredictor.F0Ntrain under train.py's G step (train.py:265, 318, 323; models.py:448-461) */
 
-/* Training forward of ProsodyPredictor.shared (nn.LSTM(d_hid + style_dim, d_hid / 2, bidirectional, batch_first),
- * models.py:449) on full-length sequences: stts_bilstm_fwd's output y [B][T][2H] (same params, same workspace
- * size) plus every step's cell state c_seq [2][B][T][H] for the backward. */
+/* Training forward of the bidirectional nn.LSTM(batch_first) layers under train.py's G step: ProsodyPredictor.shared
+ * (models.py:449, full-length rows) and, with `lengths` (device int32 [B], NULL = every row has length T; ABI 5), the
+ * packed-sequence LSTMs of TextEncoder (models.py:267-279), DurationEncoder (:510-518) and ProsodyPredictor.lstm
+ * (:421-430): stts_bilstm_fwd's output y [B][T][2H] (rows t >= len zero; same params, same workspace size) plus
+ * every step's cell state c_seq [2][B][T][H] for the backward. */
 int stts_bilstm_fwd_train(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int Cin,
-                          const float* const* params, int H, float* y, float* c_seq, void* workspace,
-                          long long ws_bytes, void* stream);
-/* Its backward (what autograd computes for nn.LSTM): x frames [B][T][Cin] contiguous, y and c_seq from the training
- * forward, dy [B][T][2H] -> dx [B][T][Cin] (NULL: not computed) and grads[8] in torch's parameter order
- * (weight_ih_l0, weight_hh_l0, bias_ih_l0, bias_hh_l0, then the _reverse four; NULL entries skipped).  Deterministic
- * (no atomics; the bias gradients summed over utterances in order). */
+                          const int* lengths, const float* const* params, int H, float* y, float* c_seq,
+                          void* workspace, long long ws_bytes, void* stream);
+/* Its backward (what autograd computes for nn.LSTM over a packed sequence): x frames [B][T][Cin] contiguous, the same
+ * lengths, y and c_seq from the training forward, dy [B][T][2H] -> dx [B][T][Cin] (NULL: not computed; rows t >= len
+ * zero) and grads[8] in torch's parameter order (weight_ih_l0, weight_hh_l0, bias_ih_l0, bias_hh_l0, then the
+ * _reverse four; NULL entries skipped).  Deterministic (no atomics; the bias gradients summed over utterances in
+ * order). */
 long long stts_bilstm_bwd_workspace_bytes(int B, int T, int Cin, int H);
-int stts_bilstm_bwd(const float* x, int B, int T, int Cin, const float* const* params, int H, const float* y,
-                    const float* c_seq, const float* dy, float* dx, float* const* grads, void* workspace,
-                    long long ws_bytes, void* stream);
+int stts_bilstm_bwd(const float* x, int B, int T, int Cin, const int* lengths, const float* const* params, int H,
+                    const float* y, const float* c_seq, const float* dy, float* dx, float* const* grads,
+                    void* workspace, long long ws_bytes, void* stream);
+
+/* ---- The text / duration path under train.py's G step (train.py:217, 230-233, 286-299, 318, 323, 327; round 5) */
+
+/* Backward of stts_row_norm (include/stts2.h: mode 0 LayerNorm(gamma, beta) + optional LeakyReLU(slope) <- models.py
+ * :229-240, 246-249; mode 1 AdaLayerNorm with gb [b][2C] rows gb_sb apart <- :372-392, 503-507; mode 2 the copy of
+ * the DurationEncoder's input concat <- :497-501), each with the row mask t >= lengths[b] and E concatenated style
+ * columns: x, gamma, beta, gb_sb, eps, lrelu, slope, lengths as the forward; dy [b][t][C + E] (rows dys_b / dys_t
+ * apart).  Writes (each nullable) dx [B][T][C] contiguous (masked rows 0), dgamma / dbeta [C] (mode 0),
+ * dgb [B][2C] (mode 1: the gradient of the style projection fc(s), gamma half then beta half) and
+ * dextra [B][E] = sum_{t < len} dy[b][t][C + e].  Parameter sums are fp64 in row order (deterministic); they need a
+ * workspace >= stts_row_norm_bwd_workspace_bytes(B, T, C). */
+long long stts_row_norm_bwd_workspace_bytes(int B, int T, int C);
+int stts_row_norm_bwd(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T, int C, int mode,
+                      const float* gamma, const float* beta, long long gb_sb, float eps, int lrelu, float slope,
+                      const int* lengths, const float* dy, long long dys_b, long long dys_t, int E, float* dx,
+                      float* dgamma, float* dbeta, float* dgb, float* dextra, void* workspace, long long ws_bytes,
+                      void* stream);
+/* nn.Embedding backward with the masked_fill_ of TextEncoder.forward (models.py:257-260): dW [n_symbols][C] (C <=
+ * 1024) = the sum of dy rows (b, t < len) per token id, in row order (deterministic); ids outside range add nothing. */
+int stts_embedding_bwd(const long long* tokens, int B, int T, const int* lengths, const float* dy, long long dys_b,
+                       long long dys_t, int n_symbols, int C, float* dW, void* stream);
+/* The duration losses of train.py:286-299 over the predictor's logits d [B][T][K] (rows ls_b / ls_t apart), the
+ * text lengths and d_gt [B][T] (s2s_attn_mono.sum(-1), integer-valued, rows dg_b apart): loss[0] = loss_dur =
+ * mean_b l1(sum_k sigmoid(d[b][p]), d_gt[b][p]) over 1 <= p < len - 1, loss[1] = loss_ce = mean_b BCEWithLogits(d[b][:len],
+ * trg) with trg[p][k] = k < d_gt[b][p] (fp64, utterance order).  With dlogits [B][T][K] (nullable) also the gradient of
+ * g_dur loss_dur + g_ce loss_ce, the two upstream scalars read from DEVICE floats (nullable: 0), so the call needs no
+ * host sync.  Workspace >= stts_dur_losses_workspace_bytes(B); T <= 4096. */
+long long stts_dur_losses_workspace_bytes(int B);
+int stts_dur_losses(const float* logits, long long ls_b, long long ls_t, int B, int T, int K, const int* lengths,
+                    const float* d_gt, long long dg_b, double* loss, float* dlogits, const float* g_dur,
+                    const float* g_ce, void* workspace, long long ws_bytes, void* stream);
 
 /* nn.Dropout(p) in train mode (the predictor's AdainResBlk1d dropout, models.py:335, 358-367): y = x / (1 - p) where
  * a counter draw u(seed, i) >= p, else 0.  The backward is the same call on dy with the same seed (the mask is

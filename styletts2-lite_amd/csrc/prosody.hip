@@ -849,22 +849,28 @@ __global__ void __launch_bounds__(256) k_lstm_hprev(const float* __restrict__ y,
 // hidden unit j; then every lane sums a quarter of k for W_hh^T dZ (coalesced rows of W_hh, dZ broadcast from
 // LDS), reduced in fixed order.  Lane j also sums gate row j of dZ over the steps (the bias gradient, per
 // utterance; summed over utterances in order by k_lstm_db).
+// lengths (may be null): pack_padded_sequence semantics, the direction runs over the first lengths[b] steps only (the
+// reverse one from step lengths[b] - 1 with a zero state); dZ rows t >= lengths[b] are zero (no gradient reaches the
+// padded positions, as with the reference's packed sequences)
 __global__ void __launch_bounds__(1024) k_bilstm_bwd_rec(const float* __restrict__ G, const float* __restrict__ HW,
                                                          const float* __restrict__ cs, const float* __restrict__ dy,
                                                          const float* __restrict__ W0, const float* __restrict__ W1,
-                                                         int B, int T, int H, float* __restrict__ dZ,
-                                                         float* __restrict__ dbpart) {
+                                                         const int* __restrict__ lengths, int B, int T, int H,
+                                                         float* __restrict__ dZ, float* __restrict__ dbpart) {
   __shared__ float dz[1024];
   __shared__ float red[4][256];
   __shared__ float dhs[256];
   const int b = blockIdx.x, d = blockIdx.y, j = threadIdx.x, H4 = 4 * H;
   const float* __restrict__ W = d ? W1 : W0;  // [4H][H]
   const int part = j / H, jj = j - part * H;
+  int len = lengths ? lengths[b] : T;
+  len = len < 0 ? 0 : (len > T ? T : len);
+  for (int t = len; t < T; ++t) dZ[(((size_t)b * T + t) * 2 + d) * H4 + j] = 0.f;
   float dc = 0.f, dbacc = 0.f;
   if (j < H) dhs[j] = 0.f;
   __syncthreads();
-  for (int s = 0; s < T; ++s) {
-    const int t = d == 0 ? T - 1 - s : s;
+  for (int s = 0; s < len; ++s) {
+    const int t = d == 0 ? len - 1 - s : s;
     if (j < H) {
       const size_t zb = (((size_t)d * B + b) * T + t) * H4;
       const float zi = G[zb + j] + HW[zb + j], zf = G[zb + H + j] + HW[zb + H + j];
@@ -873,7 +879,7 @@ __global__ void __launch_bounds__(1024) k_bilstm_bwd_rec(const float* __restrict
       const size_t cb = ((size_t)d * B + b) * T;
       const float ct = cs[(cb + t) * H + j];
       const int tp = d == 0 ? t - 1 : t + 1;
-      const float cp = (tp >= 0 && tp < T) ? cs[(cb + tp) * H + j] : 0.f;
+      const float cp = (tp >= 0 && tp < len) ? cs[(cb + tp) * H + j] : 0.f;
       const float dh = dy[((size_t)b * T + t) * 2 * H + (size_t)d * H + j] + dhs[j];
       const float tc = tanhf(ct);
       const float dct = dc + dh * og * (1.f - tc * tc);
@@ -946,8 +952,8 @@ LstmBwdWs lstm_bwd_ws(void* base, int B, int T, int Cin, int H) {
 }  // namespace
 
 extern "C" int stts_bilstm_fwd_train(const float* x, long long xs_b, long long xs_t, long long xs_c, int B, int T,
-                                     int Cin, const float* const* params, int H, float* y, float* c_seq,
-                                     void* workspace, long long ws_bytes, void* stream) {
+                                     int Cin, const int* lengths, const float* const* params, int H, float* y,
+                                     float* c_seq, void* workspace, long long ws_bytes, void* stream) {
   if (B < 0 || T < 0 || Cin <= 0 || !params || !y || !c_seq) return ST_EINVAL;
   if (H <= 0 || H > 256 || (H & 31)) return ST_EINVAL;
   for (int i = 0; i < 8; ++i)
@@ -969,7 +975,7 @@ extern "C" int stts_bilstm_fwd_train(const float* x, long long xs_b, long long x
                G + (size_t)d * B * T * H4, (long long)T * H4, H4, 1, T, 1, 0, nullptr};
     ST_CHECK(launch_gemm(a, B, s));
   }
-  hipLaunchKernelGGL(k_bilstm_rec<1>, dim3(B, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), nullptr, B,
+  hipLaunchKernelGGL(k_bilstm_rec<1>, dim3(B, 2), dim3(H4), 0, s, G, reinterpret_cast<const float4*>(WT), lengths, B,
                      T, H, y, nullptr, nullptr, c_seq);
   return (int)hipGetLastError();
 }
@@ -979,9 +985,9 @@ extern "C" long long stts_bilstm_bwd_workspace_bytes(int B, int T, int Cin, int 
   return lstm_bwd_ws(nullptr, B, T, Cin, H).bytes;
 }
 
-extern "C" int stts_bilstm_bwd(const float* x, int B, int T, int Cin, const float* const* params, int H,
-                               const float* y, const float* c_seq, const float* dy, float* dx, float* const* grads,
-                               void* workspace, long long ws_bytes, void* stream) {
+extern "C" int stts_bilstm_bwd(const float* x, int B, int T, int Cin, const int* lengths, const float* const* params,
+                               int H, const float* y, const float* c_seq, const float* dy, float* dx,
+                               float* const* grads, void* workspace, long long ws_bytes, void* stream) {
   if (B < 0 || T < 0 || Cin <= 0 || !params || !x || !y || !c_seq || !dy || !grads) return ST_EINVAL;
   if (H <= 0 || H > 256 || (H & 31)) return ST_EINVAL;
   for (int i = 0; i < 8; ++i)
@@ -1007,8 +1013,8 @@ extern "C" int stts_bilstm_bwd(const float* x, int B, int T, int Cin, const floa
                w.HW + (size_t)d * bt * H4, (long long)T * H4, H4, 1, T, 1, 0, nullptr};
     ST_CHECK(launch_gemm(h, B, s));
   }
-  hipLaunchKernelGGL(k_bilstm_bwd_rec, dim3(B, 2), dim3(H4), 0, s, w.G, w.HW, c_seq, dy, params[1], params[5], B, T,
-                     H, w.dZ, w.dbp);
+  hipLaunchKernelGGL(k_bilstm_bwd_rec, dim3(B, 2), dim3(H4), 0, s, w.G, w.HW, c_seq, dy, params[1], params[5], lengths,
+                     B, T, H, w.dZ, w.dbp);
   ST_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_lstm_db, dim3((2 * H4 + 255) / 256), dim3(256), 0, s, w.dbp, B, H, grads[2], grads[3], grads[6],
                      grads[7]);

@@ -67,7 +67,15 @@ class ProsodyPredictor(nn.Module):
 
     def forward(self, texts, style, text_lengths, alignment, m=None):
         """reference models.py:417-446: texts = TextEncoder output [B, d_hid, T], style [B, style_dim],
-        alignment [B, T, F] -> (duration logits [B, T, max_dur], en [B, d_hid + style_dim, F])."""
+        alignment [B, T, F] -> (duration logits [B, T, max_dur], en [B, d_hid + style_dim, F]).
+
+        Under autograd (train.py:230-233 differentiates it through loss_dur / loss_ce and en) the trainable path runs:
+        texttrain.predictor_forward (packed BiLSTMs, AdaLayerNorms, the style concats, duration_proj and en = d^T aln,
+        each with its HIP backward; dropout in train mode)."""
+        from .texttrain import needs_grad
+        if needs_grad(self, texts, style, alignment):
+            from .texttrain import predictor_forward
+            return predictor_forward(self, texts, style, text_lengths, alignment)
         from .engine import forward_only
         forward_only(self, "ProsodyPredictor")
         dev = self.F0_proj.weight.device

@@ -124,7 +124,11 @@ def frames_gemm(x, xs, B, Tin, Cin, w, wst, N, K, pad, bias, bias2, y, ys, Tout)
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """Batched a @ b for 3-D float32 device tensors of any strides ([B,M,K] @ [B,K,N] -> [B,M,N])."""
+    """Batched a @ b for 3-D float32 device tensors of any strides ([B,M,K] @ [B,K,N] -> [B,M,N]); under autograd
+    (an operand requires grad) with both operand gradients (texttrain.matmul)."""
+    if torch.is_grad_enabled() and (a.requires_grad or b.requires_grad):
+        from . import texttrain
+        return texttrain.matmul(a, b)
     _on_device(a, "matmul"), _on_device(b, "matmul")
     if a.dim() != 3 or b.dim() != 3 or a.shape[0] != b.shape[0] or a.shape[2] != b.shape[1]:
         raise ValueError(f"matmul shapes {tuple(a.shape)} @ {tuple(b.shape)}")
@@ -213,6 +217,19 @@ class LSTM(nn.LSTM):
     """
 
     def forward(self, x, hx=None, lengths=None):
+        from .texttrain import needs_grad
+        if needs_grad(self, x.data if isinstance(x, PackedSequence) else x):
+            # train.py's G step: the packed-sequence BiLSTM with its backward (texttrain.bilstm); (h_n, c_n) are not
+            # formed on this path (every reference caller discards them: x, _ = lstm(x))
+            from . import texttrain
+            if hx is not None:
+                raise NotImplementedError("HIP LSTM: only the zero initial state the reference uses (hx=None)")
+            if isinstance(x, PackedSequence):
+                padded, lens = pad_packed_sequence(x, batch_first=True)
+                out, _ = self.forward(padded, lengths=lens)
+                return pack_padded_sequence(out, lens, batch_first=True, enforce_sorted=False), None
+            _on_device(x, "LSTM")
+            return texttrain.bilstm(self, x, _lengths(lengths, x.shape[0], x.shape[1], x.device)), None
         from .engine import forward_only
         forward_only(self, "LSTM")
         if hx is not None:
@@ -302,6 +319,12 @@ class TextEncoder(nn.Module):
         return cache[1]
 
     def forward(self, x, input_lengths, m=None):
+        from .texttrain import needs_grad
+        if needs_grad(self):  # train.py:217 (the text encoder in train mode, optimizer.step('text_encoder'))
+            from . import texttrain
+            if m is not None and m.shape[-1] != x.shape[-1]:
+                raise ValueError(f"mask length {m.shape[-1]} != token length {x.shape[-1]}")
+            return texttrain.text_encoder(self, x, input_lengths)
         from .engine import forward_only
         forward_only(self, "TextEncoder")
         if x.dim() != 2:
@@ -347,6 +370,13 @@ class AdaLayerNorm(nn.Module):
 
     def forward(self, x, s, lengths=None, extra=None):
         """x [B,T,C] (any strides), s [B,style_dim] -> [B,T,C(+E)]; rows t >= lengths are zero."""
+        from .texttrain import needs_grad
+        if needs_grad(self, x, s, extra):
+            from . import texttrain
+            from .training import linear
+            gb = linear(s, self.fc.weight, self.fc.bias)
+            ln = _lengths(lengths, x.shape[0], x.shape[1], x.device)
+            return texttrain.ada_layer_norm(x, gb, self.eps, ln, extra=extra)
         from .engine import forward_only
         forward_only(self, "AdaLayerNorm")
         gb = linear_frames(s.unsqueeze(0), self.fc.weight.detach(), self.fc.bias.detach())[0]
@@ -370,6 +400,11 @@ class DurationEncoder(nn.Module):
         self.dropout, self.d_model, self.sty_dim = dropout, d_model, sty_dim
 
     def forward(self, x, style, text_lengths, m=None):
+        from .texttrain import needs_grad
+        if needs_grad(self, x, style):
+            from . import texttrain
+            _on_device(x, "DurationEncoder"), _on_device(style, "DurationEncoder style")
+            return texttrain.duration_encoder(self, x, style, _lengths(text_lengths, x.shape[0], x.shape[2], x.device))
         from .engine import forward_only
         forward_only(self, "DurationEncoder")
         _on_device(x, "DurationEncoder"), _on_device(style, "DurationEncoder style")

@@ -68,9 +68,9 @@ def _tl():
         "stts_gan_loss_bwd": ([vp, vp, vp, i, vp, vp, ll, vp], i),
         "stts_adamw_step": ([vp, i, d, d, d, d, d, ll, vp], i),
         "stts_bilstm_workspace_bytes": ([i, i, i], ll),
-        "stts_bilstm_fwd_train": ([vp, ll, ll, ll, i, i, i, vp, i, vp, vp, vp, ll, vp], i),
+        "stts_bilstm_fwd_train": ([vp, ll, ll, ll, i, i, i, vp, vp, i, vp, vp, vp, ll, vp], i),
         "stts_bilstm_bwd_workspace_bytes": ([i, i, i, i], ll),
-        "stts_bilstm_bwd": ([vp, i, i, i, vp, i, vp, vp, vp, vp, vp, vp, ll, vp], i),
+        "stts_bilstm_bwd": ([vp, i, i, i, vp, vp, i, vp, vp, vp, vp, vp, vp, ll, vp], i),
         "stts_dropout": ([vp, ll, f, ull, vp, vp], i),
         "stts_rowexp_fwd": ([vp, i, i, i, i, i, i, vp, vp], i),
         "stts_rowexp_bwd": ([vp, i, i, i, i, i, i, vp, vp], i),
@@ -1231,11 +1231,12 @@ def dropout(x, p):
 
 # ------------------------------------------------------------------ ProsodyPredictor.F0Ntrain (models.py:448-461)
 class _BiLSTMFn(torch.autograd.Function):
-    """ProsodyPredictor.shared (bidirectional nn.LSTM, batch_first, full-length rows) with its backward:
-    stts_bilstm_fwd_train / stts_bilstm_bwd.  x frames [B, T, Cin]; params in torch's order."""
+    """Bidirectional nn.LSTM (batch_first) with its backward: stts_bilstm_fwd_train / stts_bilstm_bwd.  x frames
+    [B, T, Cin]; ln: None (ProsodyPredictor.shared, full-length rows) or the device int32 text lengths (the packed
+    sequences of the text / duration path, texttrain.py); params in torch's order."""
 
     @staticmethod
-    def forward(ctx, x, *params):
+    def forward(ctx, x, ln, *params):
         _require_device()
         xc = _c(x)
         B, T, Cin = xc.shape
@@ -1247,36 +1248,38 @@ class _BiLSTMFn(torch.autograd.Function):
         ws = _ws(nb, x.device)
         y = torch.empty(B, T, 2 * H, dtype=torch.float32, device=x.device)
         cs = torch.empty(2, B, T, H, dtype=torch.float32, device=x.device)
-        check(L.stts_bilstm_fwd_train(_ptr(xc), T * Cin, Cin, 1, B, T, Cin, arr, H, _ptr(y), _ptr(cs), _ptr(ws), nb,
-                                      _stream()), "stts_bilstm_fwd_train")
-        ctx.save_for_backward(xc, y, cs, *ps)
+        check(L.stts_bilstm_fwd_train(_ptr(xc), T * Cin, Cin, 1, B, T, Cin, _ptr(ln), arr, H, _ptr(y), _ptr(cs),
+                                      _ptr(ws), nb, _stream()), "stts_bilstm_fwd_train")
+        ctx.save_for_backward(xc, y, cs, ln if ln is not None else torch.empty(0), *ps)
+        ctx.has_ln = ln is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xc, y, cs, *ps = ctx.saved_tensors
+        xc, y, cs, ln, *ps = ctx.saved_tensors
+        ln = ln if ctx.has_ln else None
         B, T, Cin = xc.shape
         H = ps[1].shape[1]
         dyc = _c(dy)
         need = ctx.needs_input_grad
         dx = torch.empty_like(xc) if need[0] else None
-        grads = [torch.empty_like(p) if need[i + 1] else None for i, p in enumerate(ps)]
+        grads = [torch.empty_like(p) if need[i + 2] else None for i, p in enumerate(ps)]
         arr = (ctypes.c_void_p * 8)(*[p.data_ptr() for p in ps])
         garr = (ctypes.c_void_p * 8)(*[g.data_ptr() if g is not None else None for g in grads])
         L = _tl()
         nb = int(L.stts_bilstm_bwd_workspace_bytes(B, T, Cin, H))
         check(nb if nb < 0 else 0, "stts_bilstm_bwd_workspace_bytes")
         ws = _ws(nb, dy.device)
-        check(L.stts_bilstm_bwd(_ptr(xc), B, T, Cin, arr, H, _ptr(y), _ptr(cs), _ptr(dyc), _ptr(dx), garr, _ptr(ws),
-                                nb, _stream()), "stts_bilstm_bwd")
-        return (dx, *grads)
+        check(L.stts_bilstm_bwd(_ptr(xc), B, T, Cin, _ptr(ln), arr, H, _ptr(y), _ptr(cs), _ptr(dyc), _ptr(dx), garr,
+                                _ptr(ws), nb, _stream()), "stts_bilstm_bwd")
+        return (dx, None, *grads)
 
 
 def bilstm_frames(lstm, x):
     """lstm = the reference's nn.LSTM(.., bidirectional, batch_first) layout; x frames [B, T, Cin] -> [B, T, 2H]."""
     ps = [lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0, lstm.weight_ih_l0_reverse,
           lstm.weight_hh_l0_reverse, lstm.bias_ih_l0_reverse, lstm.bias_hh_l0_reverse]
-    return _BiLSTMFn.apply(x, *ps)
+    return _BiLSTMFn.apply(x, None, *ps)
 
 
 def f0ntrain(pp, x, s, dtype="fp32"):

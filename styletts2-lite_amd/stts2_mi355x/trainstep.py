@@ -21,7 +21,20 @@ computes s = style_encoder(gt.unsqueeze(1)), (F0_fake, N_fake) = predictor.F0Ntr
 train mode: its dropout), y_rec = decoder(en, F0_fake, N_fake, s), adds lambda_F0 smooth_l1(F0_real, F0_fake) / 10
 and lambda_norm smooth_l1(N_real, N_fake) to g_loss (:269-270, 300-307; F0_real comes from the pitch extractor and
 N_real = log_norm(gt), both outside this path) and steps AdamW on the predictor and the style encoder after the
-decoder's backward (:323-324).  `freeze_d_in_g` (default) turns off requires_grad of the discriminator parameters
+decoder's backward (:323-324).  With `text_encoder=` (and the predictor) the step starts where train.py's G step starts
+(train.py:217-262), from the tokens:
+
+    losses = step(None, None, None, None, wav, gt=None, F0_real=F0_real, N_real=N_real,
+                  text=dict(texts=, input_lengths=, attn=, attn_mono=, mels=, starts=, mel_len=))
+
+t_en = text_encoder(texts, input_lengths) (:217), asr = t_en @ attn (:220-223; attn = s2s_attn or its monotonic
+version, the caller's coin), d_gt = attn_mono.sum(-1) (:225), s = style_encoder(mels) (:228), (d, p) =
+predictor(t_en, s, input_lengths, attn_mono) (:230-233), the per-utterance crops en / p_en / gt of mel_len frames at
+`starts` (:235-251; the caller draws them, as train.py's np.random.randint), then the step above with en, p_en, gt,
+plus lambda_dur loss_dur + lambda_ce loss_ce (:286-299, texttrain.duration_losses) in g_loss and AdamW on the text
+encoder after the backward (:327).  The aligner's own losses (loss_s2s, loss_mono) and its optimizer step belong to
+the text aligner, outside this path; the gradient of asr with respect to attn is left on attn when it requires grad.
+`freeze_d_in_g` (default) turns off requires_grad of the discriminator parameters
 during the G step: the reference computes those gradients and discards them (its next iteration starts
 with zero_grad before they are used), so skipping them changes no update.
 """
@@ -36,9 +49,10 @@ from .optim import AdamW
 class TrainStep:
     def __init__(self, decoder, mpd, msd, lr_dec=1e-5, lr_disc=1e-4, lambda_mel=5.0, lambda_gen=1.0, dtype="fp32",
                  freeze_d_in_g=True, capture=False, predictor=None, style_encoder=None, lr_pred=1e-4, lr_style=1e-5,
-                 lambda_F0=1.0, lambda_norm=1.0):
+                 lambda_F0=1.0, lambda_norm=1.0, text_encoder=None, lr_text=1e-4, lambda_dur=1.0, lambda_ce=1.0):
         self.decoder, self.mpd, self.msd = decoder, mpd, msd
-        self.predictor, self.style_encoder = predictor, style_encoder
+        self.predictor, self.style_encoder, self.text_encoder = predictor, style_encoder, text_encoder
+        self.lambda_dur, self.lambda_ce = float(lambda_dur), float(lambda_ce)
         self.lambda_F0, self.lambda_norm = float(lambda_F0), float(lambda_norm)
         self.capture = capture  # keep copies of the gradients each optimizer step consumed (tests)
         self.captured = {}
@@ -52,6 +66,8 @@ class TrainStep:
             self.opt["predictor"] = mk(predictor, lr_pred)
         if style_encoder is not None:
             self.opt["style_encoder"] = mk(style_encoder, lr_style)
+        if text_encoder is not None:  # train.py:137-157: the text encoder at the general lr
+            self.opt["text_encoder"] = mk(text_encoder, lr_text)
         self.lambda_mel, self.lambda_gen = float(lambda_mel), float(lambda_gen)
         self.freeze_d_in_g = freeze_d_in_g
 
@@ -59,15 +75,41 @@ class TrainStep:
         for o in self.opt.values():
             o.zero_grad()
 
-    def __call__(self, en, F0, N, s, wav, noise=None, seed=None, p_en=None, gt=None, F0_real=None, N_real=None):
+    def __call__(self, en, F0, N, s, wav, noise=None, seed=None, p_en=None, gt=None, F0_real=None, N_real=None,
+                 text=None):
         saved = (self.mpd.dtype_compute, self.msd.dtype_compute)
         self.mpd.dtype_compute = self.msd.dtype_compute = self.dtype
         try:
-            return self._step(en, F0, N, s, wav, noise, seed, p_en, gt, F0_real, N_real)
+            return self._step(en, F0, N, s, wav, noise, seed, p_en, gt, F0_real, N_real, text)
         finally:  # other users of the same discriminators keep their own compute dtype
             self.mpd.dtype_compute, self.msd.dtype_compute = saved
 
-    def _step(self, en, F0, N, s, wav, noise, seed, p_en, gt, F0_real, N_real):
+    def _text_front(self, text):
+        """train.py:217-251: the text encoder, asr, the predictor's forward and the crops."""
+        from .prosody import matmul
+        from .texttrain import duration_losses
+        if self.text_encoder is None or self.predictor is None:
+            raise ValueError("TrainStep(text=...) needs text_encoder= and predictor=")
+        texts, lens = text["texts"], text["input_lengths"]
+        attn, mono = text["attn"], text["attn_mono"]
+        t_en = self.text_encoder(texts, lens)  # train.py:217
+        asr = matmul(t_en, attn)  # :220-223
+        d_gt = mono.sum(axis=-1).detach()  # :225
+        mels = text["mels"]
+        s_full = self.style_encoder(mels.unsqueeze(1)) if self.style_encoder is not None else text["s"]  # :228
+        d, p = self.predictor(t_en, s_full, lens, mono)  # :230-233
+        ml, starts = int(text["mel_len"]), [int(v) for v in text["starts"]]
+        en = torch.stack([asr[b, :, st:st + ml] for b, st in enumerate(starts)])  # :235-251
+        p_en = torch.stack([p[b, :, st:st + ml] for b, st in enumerate(starts)])
+        gt = torch.stack([mels[b, :, 2 * st:2 * (st + ml)] for b, st in enumerate(starts)]).detach()
+        loss_dur, loss_ce = duration_losses(d, d_gt, lens)  # :286-299
+        return en, p_en, gt, loss_dur, loss_ce
+
+    def _step(self, en, F0, N, s, wav, noise, seed, p_en, gt, F0_real, N_real, text=None):
+        text_losses = None
+        if text is not None:
+            en, p_en, gt, loss_dur, loss_ce = self._text_front(text)
+            text_losses = (loss_dur, loss_ce)
         if self.style_encoder is not None and gt is not None:
             s = self.style_encoder(gt.unsqueeze(1))  # train.py:258
         if self.predictor is not None and p_en is not None:
@@ -100,6 +142,9 @@ class TrainStep:
             if N_real is not None:
                 extra["loss_norm_rec"] = smooth_l1_loss(N_real, N)  # train.py:270
                 g_loss = g_loss + self.lambda_norm * extra["loss_norm_rec"]
+            if text_losses is not None:  # train.py:300-307: lambda_ce loss_ce + lambda_dur loss_dur
+                extra["loss_dur"], extra["loss_ce"] = text_losses
+                g_loss = g_loss + self.lambda_ce * text_losses[1] + self.lambda_dur * text_losses[0]
             g_loss.backward()
         finally:
             for p in frozen:
@@ -107,11 +152,12 @@ class TrainStep:
         if self.capture:
             self.captured["dec"] = {k: p.grad.detach().clone() for k, p in self.decoder.named_parameters()
                                     if p.grad is not None}
-            for tag, m in (("predictor", self.predictor), ("style_encoder", self.style_encoder)):
+            for tag, m in (("predictor", self.predictor), ("style_encoder", self.style_encoder),
+                           ("text_encoder", self.text_encoder)):
                 if m is not None:
                     self.captured[tag] = {k: p.grad.detach().clone() for k, p in m.named_parameters()
                                           if p.grad is not None}
-        for key in ("predictor", "style_encoder", "decoder"):  # train.py:323-325
+        for key in ("predictor", "style_encoder", "decoder", "text_encoder"):  # train.py:323-327
             if key in self.opt:
                 self.opt[key].step()
         out = {"y_rec": y_rec.detach(), "d_loss": d_loss.detach(), "loss_mel": loss_mel.detach(),
