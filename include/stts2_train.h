@@ -51,6 +51,11 @@ long long stts_source_workspace_bytes(int B, int n);
 int stts_source_fwd(const float* f0_curve, const float* lw, const float* lb, const float* noise,
                     unsigned long long seed, long long utt_offset, int B, int n, int scale, float* sw, float* har,
                     void* ws, long long ws_bytes, void* stream);
+/* The same with the seed read from DEVICE memory (seed_dev, or noise given): a hipGraph capture of the training step
+ * replays with the seed the caller writes there before each replay (round 5). */
+int stts_source_fwd_seed_dev(const float* f0_curve, const float* lw, const float* lb, const float* noise,
+                             const unsigned long long* seed_dev, long long utt_offset, int B, int n, int scale,
+                             float* sw, float* har, void* ws, long long ws_bytes, void* stream);
 int stts_source_bwd(const float* sw, const float* har, const float* dhar, int B, long long L, float* dW, float* db,
                     void* ws, long long ws_bytes, void* stream);
 
@@ -138,6 +143,12 @@ typedef struct {
 } stts_adamw_tensor;
 int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, double lr, double beta1, double beta2,
                     double eps, double weight_decay, long long step, void* stream);
+/* Capturable form (round 5; torch's `capturable=True`): the step count lives in DEVICE memory, state[0] (fp64,
+ * >= 8 doubles of state), advanced and turned into the step's scalars by a one-thread launch on the stream, so a
+ * hipGraph replay of the call takes the next step's bias corrections without the host.  The scalars are formed in
+ * device fp64 (pow: the device library's), so an update may differ from the host form in the last fp32 bit. */
+int stts_adamw_step_dev(const stts_adamw_tensor* tensors, int n_tensors, double lr, double beta1, double beta2,
+                        double eps, double weight_decay, double* state, void* stream);
 
 /* ---- ProsodyPredictor.F0Ntrain under train.py's G step (train.py:265, 318, 323; models.py:448-461) */
 

@@ -168,8 +168,10 @@ __device__ __forceinline__ float rng_normal(unsigned long long seed, long long u
 __global__ void __launch_bounds__(256) k_source_train(const float* __restrict__ f0, const float* __restrict__ ph,
                                                       int n, int scale, const float* __restrict__ lw,
                                                       const float* __restrict__ lb, const float* __restrict__ noise,
-                                                      unsigned long long seed, long long utt_offset,
-                                                      float* __restrict__ sw, float* __restrict__ har) {
+                                                      unsigned long long seed, const unsigned long long* seed_dev,
+                                                      long long utt_offset, float* __restrict__ sw,
+                                                      float* __restrict__ har) {
+  if (seed_dev) seed = *seed_dev;  // (the capturable form: the step's seed read from the device)
   const int b = blockIdx.y;
   const int L = n * scale;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -507,7 +509,7 @@ struct AdamScalars {
   float neg_step;   // -lr / (1 - beta1^step)
 };
 
-__global__ __launch_bounds__(256) void k_adamw(AdamTable tb, AdamScalars s) {
+__device__ __forceinline__ void adamw_body(const AdamTable& tb, const AdamScalars& s) {
   const int blk = blockIdx.x;
   int t = 0;
   while (t + 1 < tb.cnt && tb.start[t + 1] <= blk) ++t;
@@ -534,6 +536,31 @@ __global__ __launch_bounds__(256) void k_adamw(AdamTable tb, AdamScalars s) {
     m[i] = mi;
     v[i] = vi;
   }
+}
+
+__global__ __launch_bounds__(256) void k_adamw(AdamTable tb, AdamScalars s) { adamw_body(tb, s); }
+
+// capturable form (stts_adamw_step_dev): the scalars come from device memory, formed by k_adamw_prep from the step
+// count it advances there, so a hipGraph replay of the launch takes the next step's bias corrections
+__global__ __launch_bounds__(256) void k_adamw_dev(AdamTable tb, const AdamScalars* __restrict__ sp) {
+  const AdamScalars s = *sp;
+  adamw_body(tb, s);
+}
+
+__global__ void k_adamw_prep(double* __restrict__ st, double lr, double beta1, double beta2, double eps, double wd,
+                             AdamScalars* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double step = st[0] + 1.0;
+  st[0] = step;
+  AdamScalars sc;
+  sc.decay = (float)(1.0 - lr * wd);
+  sc.w1 = (float)(1.0 - beta1);
+  sc.beta2 = (float)beta2;
+  sc.omb2 = (float)(1.0 - beta2);
+  sc.bc2_sqrt = (float)sqrt(1.0 - pow(beta2, step));
+  sc.eps = (float)eps;
+  sc.neg_step = (float)(-(lr / (1.0 - pow(beta1, step))));
+  *out = sc;
 }
 
 // ------------------------------------------------------------------ Dropout (train mode)
@@ -666,9 +693,9 @@ extern "C" long long stts_source_workspace_bytes(int B, int n) {
   return (long long)std::max(al((size_t)B * 9 * n * sizeof(float)), al((size_t)kSrcBlocks * 10 * sizeof(double)));
 }
 
-extern "C" int stts_source_fwd(const float* f0_curve, const float* lw, const float* lb, const float* noise,
-                               unsigned long long seed, long long utt_offset, int B, int n, int scale, float* sw,
-                               float* har, void* ws, long long ws_bytes, void* stream) {
+static int source_fwd(const float* f0_curve, const float* lw, const float* lb, const float* noise,
+                      unsigned long long seed, const unsigned long long* seed_dev, long long utt_offset, int B, int n,
+                      int scale, float* sw, float* har, void* ws, long long ws_bytes, void* stream) {
   const long long need = stts_source_workspace_bytes(B, n);
   if (need < 0) return (int)need;
   if (!f0_curve || !lw || !lb || !sw || !har || scale <= 0 || (long long)n * scale > (1LL << 31) - 1)
@@ -679,8 +706,22 @@ extern "C" int stts_source_fwd(const float* f0_curve, const float* lw, const flo
   ST_CHECK(st_sine_phase(f0_curve, B, n, scale, ph, s));
   const int L = n * scale;
   hipLaunchKernelGGL(k_source_train, dim3((L + 255) / 256, B), dim3(256), 0, s, f0_curve, ph, n, scale, lw, lb, noise,
-                     seed, utt_offset, sw, har);
+                     seed, seed_dev, utt_offset, sw, har);
   return (int)hipGetLastError();
+}
+
+extern "C" int stts_source_fwd(const float* f0_curve, const float* lw, const float* lb, const float* noise,
+                               unsigned long long seed, long long utt_offset, int B, int n, int scale, float* sw,
+                               float* har, void* ws, long long ws_bytes, void* stream) {
+  return source_fwd(f0_curve, lw, lb, noise, seed, nullptr, utt_offset, B, n, scale, sw, har, ws, ws_bytes, stream);
+}
+
+extern "C" int stts_source_fwd_seed_dev(const float* f0_curve, const float* lw, const float* lb, const float* noise,
+                                        const unsigned long long* seed_dev, long long utt_offset, int B, int n,
+                                        int scale, float* sw, float* har, void* ws, long long ws_bytes,
+                                        void* stream) {
+  if (!seed_dev && !noise) return ST_EINVAL;
+  return source_fwd(f0_curve, lw, lb, noise, 0ull, seed_dev, utt_offset, B, n, scale, sw, har, ws, ws_bytes, stream);
 }
 
 extern "C" int stts_source_bwd(const float* sw, const float* har, const float* dhar, int B, long long L, float* dW,
@@ -831,6 +872,43 @@ extern "C" int stts_adamw_step(const stts_adamw_tensor* tensors, int n_tensors, 
     tb.start[tb.cnt] = blocks;
     if (blocks == 0) continue;
     hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(NT), 0, s, tb, sc);
+    ST_CHECK_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+// the capturable AdamW step (include/stts2_train.h): state[0] = the step count (fp64, advanced on the device), the
+// scalars of the step formed on the device in state[1..]
+extern "C" int stts_adamw_step_dev(const stts_adamw_tensor* tensors, int n_tensors, double lr, double beta1,
+                                   double beta2, double eps, double weight_decay, double* state, void* stream) {
+  if (!tensors || n_tensors < 0 || !state || !(beta1 >= 0.0 && beta1 < 1.0) || !(beta2 >= 0.0 && beta2 < 1.0))
+    return ST_EINVAL;
+  static_assert(sizeof(AdamScalars) <= 7 * sizeof(double), "scalars fit state[1..8)");
+  hipStream_t s = (hipStream_t)stream;
+  AdamScalars* sc = reinterpret_cast<AdamScalars*>(state + 1);
+  hipLaunchKernelGGL(k_adamw_prep, dim3(1), dim3(64), 0, s, state, lr, beta1, beta2, eps, weight_decay, sc);
+  ST_CHECK_HIP(hipGetLastError());
+  for (int base = 0; base < n_tensors; base += kAdamChunk) {
+    AdamTable tb;
+    memset(&tb, 0, sizeof(tb));
+    int blocks = 0;
+    for (int j = 0; j < kAdamChunk && base + j < n_tensors; ++j) {
+      const stts_adamw_tensor& t = tensors[base + j];
+      if (t.n < 0 || (t.n > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq))) return ST_EINVAL;
+      tb.p[j] = t.param;
+      tb.g[j] = t.grad;
+      tb.m[j] = t.exp_avg;
+      tb.v[j] = t.exp_avg_sq;
+      tb.n[j] = t.n;
+      tb.start[j] = blocks;
+      const long long nb = (t.n + kAdamPer - 1) / kAdamPer;
+      if (blocks + nb > (1LL << 30)) return ST_EINVAL;
+      blocks += (int)nb;
+      tb.cnt = j + 1;
+    }
+    tb.start[tb.cnt] = blocks;
+    if (blocks == 0) continue;
+    hipLaunchKernelGGL(k_adamw_dev, dim3(blocks), dim3(NT), 0, s, tb, (const AdamScalars*)sc);
     ST_CHECK_HIP(hipGetLastError());
   }
   return 0;

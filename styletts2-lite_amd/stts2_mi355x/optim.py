@@ -26,13 +26,58 @@ class _AdamWTensor(ctypes.Structure):
 
 
 class AdamW(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False):
+    """torch.optim.AdamW (single-tensor arithmetic, bitwise) on stts_adamw_step.  capturable=True (torch's flag):
+    the step count of each parameter group lives on the device (stts_adamw_step_dev), so the step can be recorded in
+    a hipGraph and replayed; state["step"] is then brought up to date by sync_steps() (one host sync)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
+                 capturable=False):
         if amsgrad:
             raise NotImplementedError("amsgrad (the reference does not use it, optimizers.py:66)")
         if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
             raise ValueError(f"invalid AdamW hyper-parameters lr={lr} betas={betas} eps={eps}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False))
         self._step_views = weakref.WeakKeyDictionary()  # step tensor -> numpy view of its memory
+        self.capturable = bool(capturable)
+        self._dev_state = {}  # capturable: group index -> device fp64 [8] (step count, then the step's scalars)
+
+    def sync_steps(self):
+        """capturable: copy each group's device step count into its parameters' state["step"] (host sync)."""
+        for gi, st in self._dev_state.items():
+            n = float(st[0].item())
+            for p in self.param_groups[gi]["params"]:
+                if p in self.state and "step" in self.state[p]:
+                    self.state[p]["step"] = torch.tensor(n)
+
+    def _step_capturable(self, gi, group):
+        beta1, beta2 = group["betas"]
+        items = []
+        for p in group["params"]:
+            if p.grad is None:
+                continue
+            if p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous() or not p.grad.is_contiguous():
+                raise RuntimeError("HIP AdamW: contiguous fp32 parameters and gradients on the device")
+            st = self.state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            items.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"]))
+        if not items:
+            return
+        dev = self._dev_state.get(gi)
+        if dev is None:  # one count per group (every parameter of the group steps together), from the host state
+            dev = torch.zeros(8, dtype=torch.float64, device=items[0][0].device)
+            dev[0] = float(self.state[items[0][0]]["step"])
+            self._dev_state[gi] = dev
+        arr = (_AdamWTensor * len(items))()
+        for i, (p, g, m, v) in enumerate(items):
+            arr[i] = _AdamWTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel())
+        check(_tl().stts_adamw_step_dev(arr, len(items), ctypes.c_double(group["lr"]), ctypes.c_double(beta1),
+                                        ctypes.c_double(beta2), ctypes.c_double(group["eps"]),
+                                        ctypes.c_double(group["weight_decay"]), ctypes.c_void_p(dev.data_ptr()),
+                                        _stream()), "stts_adamw_step_dev")
+        increment_version([p for p, _, _, _ in items])
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -41,6 +86,10 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         _require_device()
+        if self.capturable:
+            for gi, group in enumerate(self.param_groups):
+                self._step_capturable(gi, group)
+            return loss
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             # tensors of one group that share a step count go in one call (a freshly added parameter starts at 1)

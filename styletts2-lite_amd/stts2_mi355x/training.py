@@ -67,6 +67,8 @@ def _tl():
         "stts_gan_loss": ([vp, i, vp, vp, ll, vp], i),
         "stts_gan_loss_bwd": ([vp, vp, vp, i, vp, vp, ll, vp], i),
         "stts_adamw_step": ([vp, i, d, d, d, d, d, ll, vp], i),
+        "stts_adamw_step_dev": ([vp, i, d, d, d, d, d, vp, vp], i),
+        "stts_source_fwd_seed_dev": ([vp, vp, vp, vp, vp, ll, i, i, i, vp, vp, vp, ll, vp], i),
         "stts_bilstm_workspace_bytes": ([i, i, i], ll),
         "stts_bilstm_fwd_train": ([vp, ll, ll, ll, i, i, i, vp, vp, i, vp, vp, vp, ll, vp], i),
         "stts_bilstm_bwd_workspace_bytes": ([i, i, i, i], ll),
@@ -793,9 +795,16 @@ class _SourceFn(torch.autograd.Function):
         har = torch.empty(B, L, dtype=torch.float32, device=fc.device)
         nb = _tl().stts_source_workspace_bytes(B, n)
         ws = _ws(nb, fc.device)
-        check(_tl().stts_source_fwd(_ptr(fc), _ptr(wc), _ptr(bc), _ptr(nz), ctypes.c_ulonglong(int(seed) & (2**64 - 1)),
-                                    int(utt_offset), B, n, int(scale), _ptr(sw), _ptr(har), _ptr(ws), int(nb),
-                                    _stream()), "stts_source_fwd")
+        if isinstance(seed, torch.Tensor):  # a device int64 [1] (the capturable step): the kernel reads it
+            if not seed.is_cuda or seed.dtype != torch.int64:
+                raise TypeError("seed tensor: int64 on the device")
+            check(_tl().stts_source_fwd_seed_dev(_ptr(fc), _ptr(wc), _ptr(bc), _ptr(nz), _ptr(seed), int(utt_offset), B,
+                                                 n, int(scale), _ptr(sw), _ptr(har), _ptr(ws), int(nb), _stream()),
+                  "stts_source_fwd_seed_dev")
+        else:
+            check(_tl().stts_source_fwd(_ptr(fc), _ptr(wc), _ptr(bc), _ptr(nz),
+                                        ctypes.c_ulonglong(int(seed) & (2**64 - 1)), int(utt_offset), B, n, int(scale),
+                                        _ptr(sw), _ptr(har), _ptr(ws), int(nb), _stream()), "stts_source_fwd")
         ctx.save_for_backward(sw, har)
         ctx.shapes = (lw.shape, lb.shape, n)
         return har

@@ -34,6 +34,13 @@ predictor(t_en, s, input_lengths, attn_mono) (:230-233), the per-utterance crops
 plus lambda_dur loss_dur + lambda_ce loss_ce (:286-299, texttrain.duration_losses) in g_loss and AdamW on the text
 encoder after the backward (:327).  The aligner's own losses (loss_s2s, loss_mono) and its optimizer step belong to
 the text aligner, outside this path; the gradient of asr with respect to attn is left on attn when it requires grad.
+`graph=True` (the config-5 step: decoder + discriminators): the step is recorded once in a hipGraph and replayed;
+the host then issues one graph launch per step instead of ~5,000 kernel launches through Python autograd.  Every
+per-step host scalar lives on the device: the AdamW step counts (optim.AdamW(capturable=True), stts_adamw_step_dev)
+and the noise seed (stts_source_fwd_seed_dev, written before each replay).  Call 1 runs eagerly (it also warms the
+kernels' one-time setup), call 2 records the graph and replays it, later calls copy their inputs into the graph's
+static buffers and replay.  The returned losses are the graph's static outputs (overwritten by the next replay) and
+the input gradients land on `static_inputs`; optimizer state["step"] follows after AdamW.sync_steps().
 `freeze_d_in_g` (default) turns off requires_grad of the discriminator parameters
 during the G step: the reference computes those gradients and discards them (its next iteration starts
 with zero_grad before they are used), so skipping them changes no update.
@@ -49,7 +56,8 @@ from .optim import AdamW
 class TrainStep:
     def __init__(self, decoder, mpd, msd, lr_dec=1e-5, lr_disc=1e-4, lambda_mel=5.0, lambda_gen=1.0, dtype="fp32",
                  freeze_d_in_g=True, capture=False, predictor=None, style_encoder=None, lr_pred=1e-4, lr_style=1e-5,
-                 lambda_F0=1.0, lambda_norm=1.0, text_encoder=None, lr_text=1e-4, lambda_dur=1.0, lambda_ce=1.0):
+                 lambda_F0=1.0, lambda_norm=1.0, text_encoder=None, lr_text=1e-4, lambda_dur=1.0, lambda_ce=1.0,
+                 graph=False):
         self.decoder, self.mpd, self.msd = decoder, mpd, msd
         self.predictor, self.style_encoder, self.text_encoder = predictor, style_encoder, text_encoder
         self.lambda_dur, self.lambda_ce = float(lambda_dur), float(lambda_ce)
@@ -59,7 +67,10 @@ class TrainStep:
         self.dtype = dtype  # the discriminators take it for the duration of each step only (__call__)
         self.gl, self.dl = GeneratorLoss(mpd, msd), DiscriminatorLoss(mpd, msd)
         self.stft_loss = MultiResolutionSTFTLoss()
-        mk = lambda m, lr: AdamW(m.parameters(), lr=lr, weight_decay=1e-4, betas=(0.0, 0.99), eps=1e-9)  # noqa: E731
+        self.graph = bool(graph)
+        self._graph, self._calls, self.static_inputs, self._static_out = None, 0, None, None
+        mk = lambda m, lr: AdamW(m.parameters(), lr=lr, weight_decay=1e-4, betas=(0.0, 0.99), eps=1e-9,  # noqa: E731
+                                 capturable=self.graph)
         self.opt = {"decoder": mk(decoder, lr_dec), "mpd": mk(mpd, lr_disc), "msd": mk(msd, lr_disc)}
         # train.py:137-157: the predictor at the general lr, the style encoder at the acoustic ft_lr
         if predictor is not None:
@@ -80,9 +91,54 @@ class TrainStep:
         saved = (self.mpd.dtype_compute, self.msd.dtype_compute)
         self.mpd.dtype_compute = self.msd.dtype_compute = self.dtype
         try:
+            if self.graph:
+                if any(v is not None for v in (p_en, gt, F0_real, N_real, text)):
+                    raise NotImplementedError("TrainStep(graph=True) records the config-5 step (decoder + "
+                                              "discriminators); the predictor / style / text options run eagerly")
+                return self._graphed(en, F0, N, s, wav, noise, seed)
             return self._step(en, F0, N, s, wav, noise, seed, p_en, gt, F0_real, N_real, text)
         finally:  # other users of the same discriminators keep their own compute dtype
             self.mpd.dtype_compute, self.msd.dtype_compute = saved
+
+    def _graphed(self, en, F0, N, s, wav, noise, seed):
+        """The recorded step (graph=True): see the module docstring."""
+        if seed is None and noise is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # (a CPU draw: no device sync)
+        self._calls += 1
+        if self._calls == 1:  # eager: the kernels' one-time setup, the optimizers' device state
+            return self._step(en, F0, N, s, wav, noise, seed, None, None, None, None)
+        if self._graph is None:
+            dev = wav.device
+            st = {k: t.detach().clone().requires_grad_(t.requires_grad) for k, t in
+                  (("en", en), ("F0", F0), ("N", N), ("s", s))}
+            st["wav"] = wav.detach().clone()
+            st["noise"] = noise.detach().clone() if noise is not None else None
+            st["seed"] = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.static_inputs = st
+            self._fill(en, F0, N, s, wav, noise, seed)
+            g = torch.cuda.CUDAGraph()
+            # (the eager call already ran every kernel once on this stream: no side-stream warm-up needed)
+            with torch.cuda.graph(g):
+                self._static_out = self._step(st["en"], st["F0"], st["N"], st["s"], st["wav"], st["noise"],
+                                              None if st["noise"] is not None else st["seed"], None, None, None, None)
+            self._graph = g
+        else:
+            self._fill(en, F0, N, s, wav, noise, seed)
+        self._graph.replay()
+        return self._static_out
+
+    def _fill(self, en, F0, N, s, wav, noise, seed):
+        st = self.static_inputs
+        with torch.no_grad():
+            for k, t in (("en", en), ("F0", F0), ("N", N), ("s", s), ("wav", wav)):
+                if t.data_ptr() != st[k].data_ptr():
+                    st[k].copy_(t)
+            if noise is not None:
+                if st["noise"] is None:
+                    raise ValueError("TrainStep(graph=True): the graph was recorded with the device RNG (noise=None)")
+                st["noise"].copy_(noise)
+            else:
+                st["seed"].fill_(int(seed) & (2 ** 63 - 1))
 
     def _text_front(self, text):
         """train.py:217-251: the text encoder, asr, the predictor's forward and the crops."""

@@ -804,3 +804,39 @@ def test_train_step_bf16x3_vs_fp64():
     m = _metrics(gin, g64["inputs"])
     print("inputs", m)
     assert m["normwise"] < 1e-2 and m["cos"] > 0.9999, m
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_trainstep_graph_matches_eager(dtype):
+    """TrainStep(graph=True): the config-5 step recorded in a hipGraph (device-side AdamW step counts, the noise seed
+    read from the device) and replayed, against the eager step on twin modules over three steps with three seeds:
+    the losses of every step and the parameters after the last within fp32 rounding of the AdamW scalars (the
+    capturable form forms them in device fp64)."""
+    from stts2_mi355x.trainstep import TrainStep
+    B, T = 2, 16
+    asr, f0, n, s, wav, _ = _train_inputs(B, T)
+    mods = []
+    for _ in range(2):
+        dec, _ = make_decoder("hifigan")
+        mpd, msd = _discs()
+        mods.append((dec.cuda().eval(), mpd.cuda().train(), msd.cuda().train()))
+    ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
+    eager = TrainStep(*mods[0], dtype=dtype)
+    graph = TrainStep(*mods[1], dtype=dtype, graph=True)
+    for i in range(3):
+        a = eager(*ins, wav.cuda(), seed=100 + i)
+        b = graph(*ins, wav.cuda(), seed=100 + i)
+        for k in ("d_loss", "loss_mel", "loss_gen_all", "g_loss"):
+            ea, eb = float(a[k]), float(b[k])
+            assert abs(ea - eb) <= 1e-6 * abs(ea) + 1e-7, (i, k, ea, eb)
+        print(f"{dtype} step {i}: g_loss eager {float(a['g_loss']):.6f} graph {float(b['g_loss']):.6f}")
+    assert graph._graph is not None
+    worst = 0.0
+    for (k, p), (_, q) in zip(mods[0][0].named_parameters(), mods[1][0].named_parameters()):
+        d = float((p.detach() - q.detach()).abs().max())
+        worst = max(worst, d / max(float(p.detach().abs().max()), 1e-6))
+    print(f"{dtype}: decoder parameters after 3 steps, graph vs eager: worst rel {worst:.2e}")
+    assert worst < 1e-5
+    graph.opt["decoder"].sync_steps()
+    st = graph.opt["decoder"].state[next(mods[1][0].parameters())]["step"]
+    assert float(st) == 3.0

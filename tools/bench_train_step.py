@@ -43,20 +43,21 @@ def build(B, T):
     return dec, mpd, msd, (asr, f0, n, s, wav)
 
 
-def run_gpu(dtype, B, T, steps, warmup):
+def run_gpu(dtype, B, T, steps, warmup, graph=False):
     from stts2_mi355x import training
     from stts2_mi355x.trainstep import TrainStep
     dec, mpd, msd, (asr, f0, n, s, wav) = build(B, T)
     dec, mpd, msd = dec.cuda().eval(), mpd.cuda().train(), msd.cuda().train()
     ins = [t.cuda().requires_grad_(True) for t in (asr, f0, n, s)]
     wav = wav.cuda()
-    step = TrainStep(dec, mpd, msd, dtype=dtype)
-    for i in range(warmup):
+    # (the conv work of one step, counted on the host while an eager step issues its launches)
+    training.CONV_FLOPS.update(on=True, fwd=0.0, bwd=0.0)
+    TrainStep(dec, mpd, msd, dtype=dtype)(*ins, wav, seed=99)
+    training.CONV_FLOPS["on"] = False
+    step = TrainStep(dec, mpd, msd, dtype=dtype, graph=graph)
+    for i in range(max(warmup, 3 if graph else 1)):  # graph: call 1 eager, call 2 records + replays
         step(*ins, wav, seed=100 + i)
     torch.cuda.synchronize()
-    training.CONV_FLOPS.update(on=True, fwd=0.0, bwd=0.0)
-    step(*ins, wav, seed=99)
-    training.CONV_FLOPS["on"] = False
     flops = training.CONV_FLOPS["fwd"] + training.CONV_FLOPS["bwd"]
     ev = []
     torch.cuda.synchronize()
@@ -73,7 +74,8 @@ def run_gpu(dtype, B, T, steps, warmup):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps * 1e3
     ms = statistics.median(x.elapsed_time(y) for x, y in ev)
-    return {"metric": "config5 train step", "dtype": dtype, "B": B, "T_frames": T, "samples_per_utt": 600 * T,
+    return {"metric": "config5 train step", "dtype": dtype, "graph": graph, "B": B, "T_frames": T,
+            "samples_per_utt": 600 * T,
             "ms_per_step_median": round(ms, 2), "ms_per_step_wall": round(wall, 2), "steps": steps,
             # the host's time to issue one step (Python autograd + C-ABI calls, no sync): ~ms_per_step = host-bound
             "host_ms_per_step": round(statistics.median(host), 2),
@@ -143,6 +145,7 @@ def main():
     ap.add_argument("--serial-discs", action="store_true", help="sub-discriminators and generator branches on one stream (A/B)")
     ap.add_argument("--opt", action="append", default=[], help="STTS_OPT_* KEY=VALUE held for the run (A/B)")
     ap.add_argument("--no-grad-check", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="TrainStep(graph=True): the step recorded once and replayed")
     a = ap.parse_args()
     if a.no_fold:
         from stts2_mi355x import training
@@ -160,7 +163,7 @@ def main():
         E.set_option(k, v)
     ref = None if a.no_grad_check else captured_step("fp32", a.B, a.T)
     for dt in a.dtypes.split(","):
-        line = run_gpu(dt, a.B, a.T, a.steps, a.warmup)
+        line = run_gpu(dt, a.B, a.T, a.steps, a.warmup, a.graph)
         if a.opt:
             line["options"] = a.opt
         if ref is not None and dt != "fp32":
