@@ -348,6 +348,17 @@ def main():
                     "hbm_fraction": ALG[args.decoder]["bytes"]["bf16x3"] * nsm / ela / PEAK_HBM,
                     "mfma_fraction": ALG[args.decoder]["flops"] * nsm / ela / PEAK_MFMA["bf16x3"],
                     "vs_parity_mode": (nsm / ela) / parity["value"] if parity else None}
+        if not args.no_profile:  # its own dominant kernel against the bf16x3 peak (2.5 PF / 3), per-launch hipEvents
+            nb0 = E.get_option(E.OPT_NBRANCH)
+            E.set_option(E.OPT_NBRANCH, 0)
+            E.profile_enable(True)
+            for i in range(2):
+                step(200 + i, e=aeng)
+            sync()
+            arecs = E.profile_launches()
+            E.profile_enable(False)
+            E.set_option(E.OPT_NBRANCH, nb0)
+            accuracy["roofline"] = roofline(arecs, "bf16x3", 2, accuracy["ms_per_step"], B, T, args.decoder)
         dec.engine(args.dtype)
     e2e = None
     if not cpu and not args.no_e2e:

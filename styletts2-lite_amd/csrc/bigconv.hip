@@ -45,8 +45,10 @@ struct BG {
   static constexpr int WSLICE = CG * C * 32;        // bf16 elements per step
   static constexpr int WPT = WSLICE * 2 / 16 / NT;  // 16-byte units per thread per step
   static constexpr int OFF_BIAS = 2 * 5 * C * 4;    // coef [2][5][C] f32 (utterance parity)
-  static constexpr int OFF_ST = OFF_BIAS + C * 4;   // stats [C][2] f32 (per-tile reduction path)
-  static constexpr int OFF_W = OFF_ST + 2 * C * 4;
+  // stats [WAVES_M][C][2] f32 (per-tile reduction path): one copy per frame half, so every LDS word has one
+  // writer and the flush adds the copies in a fixed order (deterministic statistics, common.h ST_W)
+  static constexpr int OFF_ST = OFF_BIAS + C * 4;
+  static constexpr int OFF_W = OFF_ST + F::WAVES_M * 2 * C * 4;
   static constexpr int OFF_X = OFF_W + 4 * WSLICE * 2;  // 4-slot weight ring
   static constexpr int LDS = OFF_X + 2 * R * XP * 2;
   static_assert(F::WAVES_M * MT * 32 == BM && F::WAVES_N * NTL * 32 == C, "wave grid");
@@ -96,10 +98,8 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   if (tbeg >= tend) return;  // uniform over the block
   const int nsteps = (tend - tbeg) * NS;
 
-  for (int i = tid; i < C; i += NT) {
-    bias_s[i] = p.bias ? p.bias[i] : 0.f;
-    st_lds[2 * i] = st_lds[2 * i + 1] = 0.f;
-  }
+  for (int i = tid; i < C; i += NT) bias_s[i] = p.bias ? p.bias[i] : 0.f;
+  for (int i = tid; i < F::WAVES_M * 2 * C; i += NT) st_lds[i] = 0.f;
 
   // ---------------- weights: global step g -> (group, tap) slice, 16-byte units u = tid + k*NT
   const Rsrc rw = make_rsrc(p.w, (unsigned)((size_t)G::NCH * K * C * 32 * 2));
@@ -232,30 +232,30 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
     if constexpr (SREG) {
 #pragma unroll
       for (int ni = 0; ni < NTL; ++ni)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float a = st_s[ni][r], q = st_q[ni][r];
-#pragma unroll
-          for (int o = 16; o >= 1; o >>= 1) {
-            a += __shfl_xor(a, o);
-            q += __shfl_xor(q, o);
-          }
-          if (l32 == 0) {
-            double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + (wn * NTL + ni) * 32 + hi * 16 + r) * 2;
-            atomicAdd(d, (double)a);
-            atomicAdd(d + 1, (double)q);
-          }
-          st_s[ni][r] = st_q[ni][r] = 0.f;
+      {
+        float a, q;
+        stat_bfly16(st_s[ni], st_q[ni], l32, a, q);
+        if (l32 < 16) {
+          double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + (wn * NTL + ni) * 32 + hi * 16 + l32) * ST_W;
+          fx_add(d, a);
+          fx_add(d + 2, q);
         }
+      }
     }
   };
   // per-tile path: LDS accumulators -> global (after a barrier), when the block leaves utterance b
   auto flush_lds = [&](int b) __attribute__((always_inline)) {
     for (int ci = tid; ci < C; ci += NT) {
-      double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ci) * 2;
-      atomicAdd(d, (double)st_lds[2 * ci]);
-      atomicAdd(d + 1, (double)st_lds[2 * ci + 1]);
-      st_lds[2 * ci] = st_lds[2 * ci + 1] = 0.f;
+      double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ci) * ST_W;
+      float a = 0.f, q = 0.f;
+#pragma unroll
+      for (int m = 0; m < F::WAVES_M; ++m) {
+        a += st_lds[(m * C + ci) * 2];
+        q += st_lds[(m * C + ci) * 2 + 1];
+        st_lds[(m * C + ci) * 2] = st_lds[(m * C + ci) * 2 + 1] = 0.f;
+      }
+      fx_add(d, a);
+      fx_add(d + 2, q);
     }
   };
 
@@ -351,8 +351,8 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
               q += __shfl_xor(q, o);
             }
             if (l32 == 0) {
-              atomicAdd(st_lds + 2 * (co0 + r), a);
-              atomicAdd(st_lds + 2 * (co0 + r) + 1, q);
+              st_lds[2 * (wm * C + co0 + r)] += a;
+              st_lds[2 * (wm * C + co0 + r) + 1] += q;
             }
           }
         }

@@ -71,8 +71,10 @@ struct B2 {
   // ldsdma-fill, later from HBM under load; a tap is ~0.5 us of MFMA issue per SIMD)
   static constexpr int OFF_COEF = 0;                  // [2][NCOEF][CINP] f32 (utterance parity)
   static constexpr int OFF_BIAS = OFF_COEF + 2 * NCOEF * CINP * 4;
-  static constexpr int OFF_ST = OFF_BIAS + CO * 4;    // [CO][2] f32
-  static constexpr int OFF_W = (OFF_ST + 2 * CO * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
+  // [FH][CO][2] f32: one copy per frame half, one writer per word, added in a fixed order by the flush
+  // (deterministic statistics, common.h ST_W)
+  static constexpr int OFF_ST = OFF_BIAS + CO * 4;
+  static constexpr int OFF_W = (OFF_ST + FH * 2 * CO * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
   static constexpr int BPC = NW == 4 ? 2 : 1;                     // blocks per CU
   static constexpr int PDMAX_LDS = ((160 * 1024 / BPC - OFF_W - NXB * WROWS * 64) / (NW * 2048)) - 1;
   static constexpr int PD0 = PDMAX_LDS < K ? PDMAX_LDS : K;
@@ -80,6 +82,7 @@ struct B2 {
   static constexpr int OFF_X = OFF_W + NW * RS * 2048; // [NXB][WROWS][64 B]
   static constexpr int LDS = OFF_X + NXB * WROWS * 64;
   static_assert(FH * NCBW == NW && NCH * NCO == C, "wave grid");
+  static_assert(!UPS || NCO <= CO, "one writer per statistics word and tile");
   static_assert(LDS * BPC <= 160 * 1024, "LDS budget");
   static_assert(K >= PD && PD >= 2, "weight prefetch stays within one group");
   static_assert(OFF_W % 1024 == 0 && OFF_X % 1024 == 0, "DMA bases");
@@ -233,10 +236,8 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     const unsigned long long d = (unsigned long long)(p.skew > 0 ? p.skew : -p.skew) * 1024ull;
     while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
   }
-  for (int i = tid; i < CO; i += NT) {
-    bias_s[i] = p.bias ? p.bias[i] : 0.f;
-    st_lds[2 * i] = st_lds[2 * i + 1] = 0.f;
-  }
+  for (int i = tid; i < CO; i += NT) bias_s[i] = p.bias ? p.bias[i] : 0.f;
+  for (int i = tid; i < G::FH * 2 * CO; i += NT) st_lds[i] = 0.f;
 
   // ---------------- weights: step s = (group, tap) -> this wave's 2 KB slice, slot s % RS
   char* wring = smem + G::OFF_W + wu * RS * 2048;
@@ -471,10 +472,16 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   // ---------------- statistics: LDS per-block sums -> fp64 global when the block leaves an utterance
   auto flush = [&](int b) __attribute__((always_inline)) {
     for (int ci = tid; ci < CO; ci += NT) {
-      double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ci) * 2;
-      atomicAdd(d, (double)st_lds[2 * ci]);
-      atomicAdd(d + 1, (double)st_lds[2 * ci + 1]);
-      st_lds[2 * ci] = st_lds[2 * ci + 1] = 0.f;
+      double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ci) * ST_W;
+      float a = 0.f, q = 0.f;
+#pragma unroll
+      for (int h = 0; h < G::FH; ++h) {
+        a += st_lds[(h * CO + ci) * 2];
+        q += st_lds[(h * CO + ci) * 2 + 1];
+        st_lds[(h * CO + ci) * 2] = st_lds[(h * CO + ci) * 2 + 1] = 0.f;
+      }
+      fx_add(d, a);
+      fx_add(d + 2, q);
     }
   };
 
@@ -603,23 +610,11 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       // reduce-scatter of the lane's 16 partial sums (then squares) over the 32 lanes of its half:
       // 8 + 4 + 2 + 1 exchanges leave lane l32 with channel co0 + l32 / 2 summed over 16 lanes, one
       // more exchange with lane l32 ^ 1 completes it; the even lane adds the sum, the odd one the
-      // sum of squares (32 exchanges and one LDS atomic per lane instead of 160 and 32)
-      auto rs16 = [&](float (&v)[16]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int m = 16, n = 16; m >= 2; m >>= 1, n >>= 1) {
-          const bool up = (l32 & m) != 0;
-#pragma unroll
-          for (int i = 0; i < n / 2; ++i) {
-            const float send = up ? v[i] : v[i + n / 2];
-            const float keep = up ? v[i + n / 2] : v[i];
-            v[i] = keep + __shfl_xor(send, m);
-          }
-        }
-        return v[0] + __shfl_xor(v[0], 1);
-      };
-      const float s1 = rs16(ts);
-      const float s2 = rs16(tq);
-      atomicAdd(st_lds + 2 * (c0 + (l32 >> 1)) + (l32 & 1), (l32 & 1) ? s2 : s1);
+      // sum of squares (32 exchanges and one LDS add per lane instead of 160 and 32; the word is this frame
+      // half's, so it has one writer and the totals do not depend on wave timing)
+      const float s1 = rs16(ts, l32);
+      const float s2 = rs16(tq, l32);
+      atomicAdd(st_lds + 2 * (fh * CO + c0 + (l32 >> 1)) + (l32 & 1), (l32 & 1) ? s2 : s1);  // (ds_add: one writer)
     }
     lap(9);
   };

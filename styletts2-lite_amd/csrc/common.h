@@ -93,7 +93,7 @@ enum ProMode { PRO_AFFINE = 1, PRO_SNAKE = 2, PRO_LRELU = 4 };
 
 struct Prologue {
   int mode;              // bitmask of ProMode
-  const double* stats;   // [B][stats_ld][2] (sum, sumsq) of the input, per (utterance, channel)
+  const double* stats;   // [B][stats_ld][ST_W] fixed-point (sum, sumsq) of the input, per (utterance, channel)
   int stats_ld;
   double inv_n;          // 1 / (time length) of the normalised tensor
   const float* gamma;    // AdaIN fc output: gamma = h[b][gb_off + c], beta = h[b][gb_off + C + c]
@@ -107,13 +107,116 @@ struct Prologue {
   long long stats_slot_bs;
 };
 
+// Deterministic InstanceNorm statistics (round 5).  The producers' partial sums reach the
+// (utterance, channel) totals through device atomics from many workgroups in no fixed order; in fp64 those adds
+// round, so repeat runs differed in the last bits.  Each total is now a fixed-point integer instead: a partial v is
+// scaled by 2^48 and split into hi = floor(v 2^16) and lo = (v 2^48 - hi 2^32) in [0, 2^32), added with integer
+// atomics (exact, so any order gives the same total), and read back as hi 2^-16 + lo 2^-48 (one rounding, the same
+// every run).  Range |partial|, |sum| < 2^45, resolution 2^-48 per addend.  An entry is ST_W = 4 words: (hi, lo) of sum x, then
+// of sum x^2.  A non-finite partial adds a poison mark (2^62) to hi, read back as NaN.
+constexpr int ST_W = 4;
+__device__ __forceinline__ void fx_add(double* w, double v) {
+  unsigned long long* u = reinterpret_cast<unsigned long long*>(w);
+  if (!(v >= -0x1p45 && v <= 0x1p45)) {  // NaN, inf or out of range
+    atomicAdd(u, 0x4000000000000000ull);
+    return;
+  }
+  const double q = v * 0x1p48;
+  const double h = floor(q * 0x1p-32);
+  const long long hi = (long long)h;
+  const long long lo = (long long)floor(q - h * 0x1p32);
+  atomicAdd(u, (unsigned long long)hi);
+  atomicAdd(u + 1, (unsigned long long)lo);
+}
+// (the same for an fp32 partial, from its bits with integer shifts: no fp64 arithmetic in the MFMA engines'
+// epilogues, where registers are scarce; truncation toward zero below 2^-48)
+__device__ __forceinline__ void fx_add(double* w, float v) {
+  unsigned long long* u = reinterpret_cast<unsigned long long*>(w);
+  const unsigned bits = __float_as_uint(v);
+  const int e = (int)((bits >> 23) & 255u);
+  if (e >= 127 + 45) {  // NaN, inf or |v| >= 2^45
+    atomicAdd(u, 0x4000000000000000ull);
+    return;
+  }
+  if (e == 0) return;  // zero (or a denormal, below the resolution)
+  const unsigned long long m = (bits & 0x7fffffu) | 0x800000u;
+  const int s = e - 127 - 23 + 48;  // v 2^48 = m 2^s, s <= 69
+  unsigned long long hi, lo;
+  if (s <= 0) {
+    hi = 0;
+    lo = s > -24 ? m >> -s : 0;
+  } else if (s < 32) {
+    const unsigned long long x = m << s;  // < 2^56
+    hi = x >> 32;
+    lo = x & 0xffffffffull;
+  } else {
+    hi = m << (s - 32);
+    lo = 0;
+  }
+  if (bits >> 31) {  // -(hi 2^32 + lo) as (hi', lo') with lo' in [0, 2^32)
+    hi = 0ull - hi - (lo != 0 ? 1ull : 0ull);
+    lo = lo != 0 ? (1ull << 32) - lo : 0ull;
+  }
+  if (hi) atomicAdd(u, hi);
+  if (lo) atomicAdd(u + 1, lo);
+}
+__device__ __forceinline__ double fx_get(const double* w) {
+  const long long* u = reinterpret_cast<const long long*>(w);
+  const long long hi = u[0];
+  if (hi >= (1ll << 61) || hi <= -(1ll << 61)) return __builtin_nan("");
+  return (double)hi * 0x1p-16 + (double)u[1] * 0x1p-48;
+}
+// add the partial sums a = sum x, q = sum x^2 into the entry e (ST_W words)
+__device__ __forceinline__ void stat_add(double* e, double a, double q) {
+  fx_add(e, a);
+  fx_add(e + 2, q);
+}
+
+// Reduce-scatter of a 32-lane half-wave's 16 per-lane partials v[r] (channels r = 0..15): 8 + 4 + 2 + 1
+// exchanges leave lane l32 with channel l32 / 2 summed over 16 lanes, one exchange with lane l32 ^ 1 completes
+// it (32 exchanges instead of the 80 of 16 butterflies).  v is clobbered.
+__device__ __forceinline__ float rs16(float (&v)[16], int l32) {
+#pragma unroll
+  for (int m = 16, n = 16; m >= 2; m >>= 1, n >>= 1) {
+    const bool up = (l32 & m) != 0;
+#pragma unroll
+    for (int i = 0; i < n / 2; ++i) {
+      const float send = up ? v[i] : v[i + n / 2];
+      const float keep = up ? v[i + n / 2] : v[i];
+      v[i] = keep + __shfl_xor(send, m);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1);
+}
+// A half-wave's 16 channels' partial (sum, sumsq) -> lane r < 16 of the half holds channel r's totals in (a, q),
+// the partials are zeroed: butterflies per channel (2 live values; the reduce-scatter above needs more registers
+// than the 256-VGPR engines have left in their epilogues), the lanes then add 16 entries at once instead of lane 0
+// adding all 16 in turn.
+__device__ __forceinline__ void stat_bfly16(float (&s)[16], float (&q)[16], int l32, float& a, float& b) {
+  a = b = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float x = s[r], y = q[r];
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) {
+      x += __shfl_xor(x, o);
+      y += __shfl_xor(y, o);
+    }
+    if (l32 == r) {
+      a = x;
+      b = y;
+    }
+    s[r] = q[r] = 0.f;
+  }
+}
+
 // Per-(utterance, channel) AdaIN coefficients from raw stats: mean, a = (1+gamma)*rstd, beta.
 __device__ __forceinline__ void adain_coeffs(const Prologue& p, int b, int c, float& m, float& a, float& be) {
-  const size_t i = ((size_t)b * p.stats_ld + c) * 2;
-  double s = p.stats[i], ss = p.stats[i + 1];
-  for (int k = 1; k < p.stats_slots; ++k) {
-    s += p.stats[(size_t)k * p.stats_slot_bs + i];
-    ss += p.stats[(size_t)k * p.stats_slot_bs + i + 1];
+  const size_t i = ((size_t)b * p.stats_ld + c) * ST_W;
+  double s = fx_get(p.stats + i), ss = fx_get(p.stats + i + 2);
+  for (int k = 1; k < p.stats_slots; ++k) {  // (slot order: fixed)
+    s += fx_get(p.stats + (size_t)k * p.stats_slot_bs + i);
+    ss += fx_get(p.stats + (size_t)k * p.stats_slot_bs + i + 2);
   }
   const double mean = s * p.inv_n;
   double var = ss * p.inv_n - mean * mean;

@@ -164,8 +164,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
       if (hi == 0 && n < p.N) {
         const int co = n % p.Cout;
         double* sb = stats_slot(p, blockIdx.x);
-        atomicAdd(sb + ((size_t)b * p.stats_ld + co) * 2 + 0, (double)a);
-        atomicAdd(sb + ((size_t)b * p.stats_ld + co) * 2 + 1, (double)q);
+        fx_add(sb + ((size_t)b * p.stats_ld + co) * ST_W, a);
+        fx_add(sb + ((size_t)b * p.stats_ld + co) * ST_W + 2, q);
       }
       st_s[ni] = st_q[ni] = 0.f;
     }
@@ -664,8 +664,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
                   if (p.stats) {  // once per (utterance, channel): direct atomics
                     for (int j = 0; j < 16; ++j) {
                       const double x = to_f32(from_f32<T>(r[j]));
-                      atomicAdd(p.stats + ((size_t)b * p.stats_ld + co0 + j) * 2 + 0, x);
-                      atomicAdd(p.stats + ((size_t)b * p.stats_ld + co0 + j) * 2 + 1, x * x);
+                      stat_add(p.stats + ((size_t)b * p.stats_ld + co0 + j) * ST_W, x, x * x);
                     }
                   }
                 }

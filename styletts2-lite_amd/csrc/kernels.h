@@ -38,7 +38,7 @@ struct ConvParams {
   int epi_lrelu;      // LeakyReLU(epi_slope) on the stored output (discriminator feature maps)
   float epi_slope;
   int epi_gelu;       // exact (erf) GELU on the stored output (Vocos ConvNeXt pwconv1 -> act)
-  double* stats;  // [B][stats_ld][2] accumulated statistics of the stored output
+  double* stats;  // [B][stats_ld][ST_W] accumulated statistics of the stored output (fixed point, common.h)
   int stats_ld;
   // small-batch atomic spreading: workgroup g accumulates into slot g % stats_slots, the slot
   // buffers lying stats_slot_bs doubles apart after `stats` (slot 0 = stats itself); the caller
@@ -74,6 +74,8 @@ __device__ __forceinline__ double* stats_slot(const ConvParams& p, int g) {
 }
 // stats[b][c] += sum of slots 1..S-1, and those slots are zeroed, for b < B, c < C
 int st_stats_fold(double* stats, int B, int ld, int C, int slots, long long slot_bs, hipStream_t s);
+// n fixed-point statistics entries (ST_W words) -> n (sum, sumsq) fp64 pairs (test hooks)
+int st_stats_decode(const double* fx, long long n, double* out, hipStream_t s);
 // which engine st_conv1d routes p to (profiling records; bench.py names the dominant kernel)
 enum { ST_ENGINE_IGEMM = 0, ST_ENGINE_RESCONV = 1, ST_ENGINE_BIGCONV = 2, ST_ENGINE_RESFUSED = 3, ST_ENGINE_HEAD = 4,
        ST_ENGINE_PW = 5, ST_ENGINE_RESSPLIT = 6, ST_ENGINE_BIGSPLIT = 7 };

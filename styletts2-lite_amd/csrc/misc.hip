@@ -32,23 +32,22 @@ __global__ void __launch_bounds__(256) k_stats_fold(double* __restrict__ st, int
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= B * C) return;
   const int b = i / C, c = i % C;
-  double* d = st + ((size_t)b * ld + c) * 2;
-  double a = 0.0, q = 0.0;
+  // integer (fixed-point) words: the fold is exact and order-free like the producers' atomics (common.h ST_W)
+  long long* d = reinterpret_cast<long long*>(st + ((size_t)b * ld + c) * ST_W);
+  long long w[ST_W] = {0, 0, 0, 0};
   for (int k = 1; k < S; ++k) {
-    double* e = d + (size_t)k * slot_bs;
-    a += e[0];
-    q += e[1];
-    e[0] = 0.0;
-    e[1] = 0.0;
+    long long* e = d + (size_t)k * slot_bs;
+#pragma unroll
+    for (int j = 0; j < ST_W; ++j) {
+      w[j] += e[j];
+      e[j] = 0;
+    }
   }
-  d[0] += a;
-  d[1] += q;
+#pragma unroll
+  for (int j = 0; j < ST_W; ++j) d[j] += w[j];
 }
 
-__device__ __forceinline__ void atomic_stats(double* st, double a, double q) {
-  atomicAdd(st, a);
-  atomicAdd(st + 1, q);
-}
+__device__ __forceinline__ void atomic_stats(double* st, double a, double q) { stat_add(st, a, q); }
 
 // ------------------------------------------------------------------ NCL -> frames
 template <typename T>
@@ -79,7 +78,7 @@ __global__ void __launch_bounds__(256) k_ncl_to_frames(const float* __restrict__
           q += (double)v * v;
         }
       }
-      atomic_stats(stats + ((size_t)b * stats_ld + c0 + c) * 2, a, q);
+      atomic_stats(stats + ((size_t)b * stats_ld + c0 + c) * ST_W, a, q);
     }
   }
 }
@@ -101,7 +100,7 @@ __global__ void __launch_bounds__(256) k_frames_convert(const float* __restrict_
     a += w;
     q += (double)w * w;
   }
-  if (stats) atomic_stats(stats + ((size_t)b * stats_ld + c) * 2, a, q);
+  if (stats) atomic_stats(stats + ((size_t)b * stats_ld + c) * ST_W, a, q);
 }
 
 // fp32 frames [rows][ld_in] -> bf16 frames [rows][ld_out] (ld_out % 8 == 0), no statistics: one thread per
@@ -232,7 +231,7 @@ __global__ void __launch_bounds__(256) k_conv_cin1(const float* __restrict__ in,
       }
       for (int di = 0; di < ndst; ++di)
         if (ds[di]->stats)
-          atomic_stats(ds[di]->stats + ((size_t)b * ds[di]->stats_ld + ds[di]->c0 + cb + threadIdx.x) * 2, A, Q);
+          atomic_stats(ds[di]->stats + ((size_t)b * ds[di]->stats_ld + ds[di]->c0 + cb + threadIdx.x) * ST_W, A, Q);
     }
   }
 }
@@ -469,7 +468,7 @@ __global__ void __launch_bounds__(256) k_noise_conv(const float* __restrict__ ha
     const int c = threadIdx.x;
     const double a = (double)red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
     const double q = (double)red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-    atomic_stats(stats + ((size_t)b * C + c) * 2, a, q);
+    atomic_stats(stats + ((size_t)b * C + c) * ST_W, a, q);
   }
 }
 
@@ -517,7 +516,7 @@ __global__ void __launch_bounds__(256) k_frames_stats(const T* __restrict__ x, l
     a += v;
     q += (double)v * v;
   }
-  atomic_stats(stats + ((size_t)b * stats_ld + c0 + c) * 2, a, q);
+  atomic_stats(stats + ((size_t)b * stats_ld + c0 + c) * ST_W, a, q);
 }
 
 // ------------------------------------------------------------------ CustomSTFT
@@ -979,6 +978,19 @@ int st_istft(const void* post, int B, int F, int ld, int n_fft, int hop, const f
   dim3 grid((L + 255) / 256, B);
   DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_istft<T>, grid, dim3(256), 0, s, reinterpret_cast<const T*>(post), F,
                                               ld, n_fft, hop, br, bi, out, L));
+  return (int)hipGetLastError();
+}
+
+__global__ void k_stats_decode(const double* __restrict__ fx, long long n, double* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  out[2 * i] = fx_get(fx + i * ST_W);
+  out[2 * i + 1] = fx_get(fx + i * ST_W + 2);
+}
+
+int st_stats_decode(const double* fx, long long n, double* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_stats_decode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, fx, n, out);
   return (int)hipGetLastError();
 }
 

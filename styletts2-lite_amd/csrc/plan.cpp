@@ -638,7 +638,7 @@ struct Ctx {
   }
   double* stat(int C) {
     double* p = dry ? nullptr : reinterpret_cast<double*>(ws + stats_off);
-    stats_off += rup((size_t)slots * B * C * 2 * sizeof(double), ALIGN);
+    stats_off += rup((size_t)slots * B * C * ST_W * sizeof(double), ALIGN);
     return p;
   }
   const void* wpk(const WConv& c) const { return packed + c.off[cdtype]; }
@@ -673,7 +673,7 @@ Prologue pro_adain(Ctx& c, const WAdaIN& a, const double* stats, int stats_ld, i
   p.alpha = alpha >= 0 ? c.P(alpha) : nullptr;
   p.slope = slope;
   p.stats_slots = c.slots;  // every stats buffer of the arena has c.slots copies (unused ones zero)
-  p.stats_slot_bs = (long long)c.B * stats_ld * 2;
+  p.stats_slot_bs = (long long)c.B * stats_ld * ST_W;
   return p;
 }
 
@@ -739,7 +739,7 @@ int conv_run(Ctx& c, ConvParams& p) {
   const bool prof = g_prof.on;
   if (prof) ST_CHECK(prof_begin(c));
   p.stats_slots = p.stats ? c.slots : 1;
-  p.stats_slot_bs = (long long)c.B * p.stats_ld * 2;
+  p.stats_slot_bs = (long long)c.B * p.stats_ld * ST_W;
   int r = st_conv1d(p, c.cdtype, c.s);
   if (r) return r;
   // statistics slots are summed by the consumers' prologues (adain_coeffs): no fold launch
@@ -762,7 +762,7 @@ int resfused_run(Ctx& c, ResFusedParams& p) {
   const bool prof = g_prof.on;
   if (prof) ST_CHECK(prof_begin(c));
   p.stats_slots = p.stats ? c.slots : 1;
-  p.stats_slot_bs = (long long)c.B * p.stats_ld * 2;
+  p.stats_slot_bs = (long long)c.B * p.stats_ld * ST_W;
   ST_CHECK(st_resfused(p, c.s));
   if (prof) {
     // algorithmic work: the statistics pass = conv1 over x (x read once); the fused pass = both convs, x once
@@ -1008,18 +1008,18 @@ int run_front(Ctx& c, const DecIO& io, FrontBufs& f) {
     p.Lq = T;
     conv_out(p, c, CAT[w], 1024, T);
     if (w == 0) {
-      p.stats = S_cat[0] + 1024 * 2;
+      p.stats = S_cat[0] + 1024 * ST_W;
       p.stats_ld = ld_cat;
     }
     RUN(conv_run(c, p));
     // these statistics are copied slot 0 only into the other concat buffers' stats below: fold
     if (w == 0 && c.slots > 1)
-      RUN(st_stats_fold(p.stats, c.B, p.stats_ld, p.Cout, c.slots, (long long)c.B * p.stats_ld * 2, c.s));
+      RUN(st_stats_fold(p.stats, c.B, p.stats_ld, p.Cout, c.slots, (long long)c.B * p.stats_ld * ST_W, c.s));
   }
   if (!c.dry) {  // the constant concat channels share their statistics across the 4 blocks
     for (int k = 1; k < 4; ++k)
-      ST_CHECK_HIP(hipMemcpy2DAsync(S_cat[k] + 1024 * 2, (size_t)ld_cat * 16, S_cat[0] + 1024 * 2,
-                                    (size_t)ld_cat * 16, 66 * 16, B, hipMemcpyDeviceToDevice, c.s));
+      ST_CHECK_HIP(hipMemcpy2DAsync(S_cat[k] + 1024 * ST_W, (size_t)ld_cat * ST_W * 8, S_cat[0] + 1024 * ST_W,
+                                    (size_t)ld_cat * ST_W * 8, 66 * ST_W * 8, B, hipMemcpyDeviceToDevice, c.s));
   }
   ST_CHECK(adain_blk(c, m.encode, ENC, 0, S_enc, ld_enc, CAT[0], 0, S_cat[0], ld_cat, H1, SC, POOL));
   ST_CHECK(adain_blk(c, m.decode[0], CAT[0], 0, S_cat[0], ld_cat, CAT[1], 0, S_cat[1], ld_cat, H1, SC, POOL));
@@ -1371,7 +1371,7 @@ int vocos_forward(Ctx& c, const DecIO& io) {
   for (const auto& b : m.cnx) {
     double* S_d = c.stat(d);
     RUN(st_dwconv7(x->p, x->bs, x->ld, B, L, d, c.P(b.dw_w), c.P(b.dw_b), D.p, D.bs, D.ld, S_d, d, c.slots,
-                   (long long)B * d * 2, c.dtype, c.s));
+                   (long long)B * d * ST_W, c.dtype, c.s));
     {
       ConvParams p = conv_base(c, b.pw1, D, 0);
       p.pro = pro_adain(c, b.norm, S_d, d, L, 0, -1, 0.f);

@@ -55,20 +55,12 @@ __global__ void __launch_bounds__(NT, 2) k_pwgemm(const ConvParams p, int ntm, i
     for (int ni = 0; ni < 2; ++ni) {
       const int nb = n0 + wn * 64 + ni * 32 + 16 * hi;
       const int co = nb % p.Cout;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float a = st_s[ni][r], q = st_q[ni][r];
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) {
-          a += __shfl_xor(a, o);
-          q += __shfl_xor(q, o);
-        }
-        if (l32 == 0 && nb < p.N) {
-          double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + co + r) * 2;
-          atomicAdd(d, (double)a);
-          atomicAdd(d + 1, (double)q);
-        }
-        st_s[ni][r] = st_q[ni][r] = 0.f;
+      float a, q;
+      stat_bfly16(st_s[ni], st_q[ni], l32, a, q);
+      if (nb < p.N && l32 < 16) {
+        double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + co + l32) * ST_W;
+        fx_add(d, a);
+        fx_add(d + 2, q);
       }
     }
   };
@@ -422,9 +414,8 @@ __global__ void __launch_bounds__(256) k_pw_reduce(const ConvParams p, int S, co
   if (ty == 0 && col) {
     const double sa = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
     const double sq = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
-    double* d = stats_slot(p, blockIdx.y) + ((size_t)b * p.stats_ld + n) * 2;
-    atomicAdd(d, sa);
-    atomicAdd(d + 1, sq);
+    double* d = stats_slot(p, blockIdx.y) + ((size_t)b * p.stats_ld + n) * ST_W;
+    stat_add(d, sa, sq);
   }
 }
 

@@ -166,22 +166,16 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     if constexpr (!ACC) {
 #pragma unroll
       for (int ni = 0; ni < NTL; ++ni)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float a = st_s[ni][r], q = st_q[ni][r];
-#pragma unroll
-          for (int o = 16; o >= 1; o >>= 1) {
-            a += __shfl_xor(a, o);
-            q += __shfl_xor(q, o);
-          }
-          if (l32 == 0) {
-            const int ch = (wn * NTL + ni) * 32 + hi * 16 + r;
-            double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + (UPS ? ch % p.Cout : ch)) * 2;
-            atomicAdd(d, (double)a);
-            atomicAdd(d + 1, (double)q);
-          }
-          st_s[ni][r] = st_q[ni][r] = 0.f;
+      {
+        float a, q;
+        stat_bfly16(st_s[ni], st_q[ni], l32, a, q);
+        const int ch = (wn * NTL + ni) * 32 + hi * 16 + l32;
+        if (l32 < 16) {
+          double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + (UPS ? ch % p.Cout : ch)) * ST_W;
+          fx_add(d, a);
+          fx_add(d + 2, q);
         }
+      }
     }
   };
 
@@ -590,20 +584,12 @@ __global__ void __launch_bounds__(512, 1) k_resconv_pp(const ConvParams p) {
   int stat_b = -1;
   auto flush = [&](int b) __attribute__((always_inline)) {
     if constexpr (!ACC) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float a = st_s[r], q = st_q[r];
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) {
-          a += __shfl_xor(a, o);
-          q += __shfl_xor(q, o);
-        }
-        if (l32 == 0) {
-          double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + wn * 32 + hi * 16 + r) * 2;
-          atomicAdd(d, (double)a);
-          atomicAdd(d + 1, (double)q);
-        }
-        st_s[r] = st_q[r] = 0.f;
+      float a, q;
+      stat_bfly16(st_s, st_q, l32, a, q);
+      if (l32 < 16) {
+        double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + wn * 32 + hi * 16 + l32) * ST_W;
+        fx_add(d, a);
+        fx_add(d + 2, q);
       }
     }
   };

@@ -265,29 +265,16 @@ __global__ void __launch_bounds__(64 * NW, NW / 4) k_resfused(const ResFusedPara
   for (int nb = 0; nb < NCB; ++nb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) st_s[nb][r] = st_q[nb][r] = 0.f;
-  auto rs16 = [&](float (&v)[16]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int m = 16, n = 16; m >= 2; m >>= 1, n >>= 1) {
-      const bool up = (l32 & m) != 0;
-#pragma unroll
-      for (int i = 0; i < n / 2; ++i) {
-        const float send = up ? v[i] : v[i + n / 2];
-        const float keep = up ? v[i + n / 2] : v[i];
-        v[i] = keep + __shfl_xor(send, m);
-      }
-    }
-    return v[0] + __shfl_xor(v[0], 1);
-  };
   auto flush = [&](int b) __attribute__((always_inline)) {
     if (!want_stats) return;
     double* d = (p.stats_slots > 1 ? p.stats + (size_t)(blockIdx.x % p.stats_slots) * p.stats_slot_bs : p.stats) +
-                (size_t)b * p.stats_ld * 2;
+                (size_t)b * p.stats_ld * ST_W;
 #pragma unroll
     for (int nb = 0; nb < NCB; ++nb) {
-      const float s1 = rs16(st_s[nb]);
-      const float s2 = rs16(st_q[nb]);
+      const float s1 = rs16(st_s[nb], l32);
+      const float s2 = rs16(st_q[nb], l32);
       const int ch = 32 * nb + 16 * hi + (l32 >> 1);
-      atomicAdd(d + 2 * ch + (l32 & 1), (double)((l32 & 1) ? s2 : s1));
+      fx_add(d + ST_W * ch + 2 * (l32 & 1), (l32 & 1) ? s2 : s1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) st_s[nb][r] = st_q[nb][r] = 0.f;
     }

@@ -135,21 +135,12 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
   }
   auto flush = [&](int b) __attribute__((always_inline)) {
     if constexpr (!ACC && PASS != 1) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float a = st_s[r], q = st_q[r];
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) {
-          a += __shfl_xor(a, o);
-          q += __shfl_xor(q, o);
-        }
-        if (l32 == 0) {
-          const int ch = wn * 32 + hi * 16 + r;
-          double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ch) * 2;
-          atomicAdd(d, (double)a);
-          atomicAdd(d + 1, (double)q);
-        }
-        st_s[r] = st_q[r] = 0.f;
+      float a, q;
+      stat_bfly16(st_s, st_q, l32, a, q);
+      if (l32 < 16) {
+        double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + wn * 32 + hi * 16 + l32) * ST_W;
+        fx_add(d, a);
+        fx_add(d + 2, q);
       }
     }
   };

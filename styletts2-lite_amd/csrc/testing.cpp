@@ -25,15 +25,19 @@ extern "C" int stts_test_conv1d(int dtype, const float* x, int B, int Lin, int C
   ST_CHECK_HIP(hipMemset(xd, 0, (size_t)B * Lin * ldx * esz));
   ST_CHECK_HIP(hipMalloc(&wd, wel * esz));
   ST_CHECK_HIP(hipMalloc(&yd, (size_t)B * Lout * Cout * esz));
-  ST_CHECK_HIP(hipMalloc(&sx, (size_t)B * Cin * 2 * sizeof(double)));
-  ST_CHECK_HIP(hipMemset(sx, 0, (size_t)B * Cin * 2 * sizeof(double)));
+  double* so = nullptr;  // the engine's fixed-point statistics (common.h ST_W), decoded into stats_out below
+  ST_CHECK_HIP(hipMalloc(&sx, (size_t)B * Cin * ST_W * sizeof(double)));
+  ST_CHECK_HIP(hipMemset(sx, 0, (size_t)B * Cin * ST_W * sizeof(double)));
+  if (stats_out) {
+    ST_CHECK_HIP(hipMalloc(&so, (size_t)B * Cout * ST_W * sizeof(double)));
+    ST_CHECK_HIP(hipMemset(so, 0, (size_t)B * Cout * ST_W * sizeof(double)));
+  }
   if (res) {
     ST_CHECK_HIP(hipMalloc(&rd, (size_t)B * Lout * Cout * esz));
     ST_CHECK(st_frames_convert(res, B, Lout, Cout, Cout, rd, Cout, nullptr, 0, dtype, s));
   }
   ST_CHECK(st_frames_convert(x, B, Lin, Cin, Cin, xd, ldx, sx, Cin, dtype, s));
   ST_CHECK(st_pack_conv(w, Cin, Cout, K, transposed, u, wd, dtype, s));
-  if (stats_out) ST_CHECK_HIP(hipMemset(stats_out, 0, (size_t)B * Cout * 2 * sizeof(double)));
   ConvParams p;
   memset(&p, 0, sizeof(p));
   p.x = xd;
@@ -83,15 +87,17 @@ extern "C" int stts_test_conv1d(int dtype, const float* x, int B, int Lin, int C
   p.res_bs = (long long)Lout * Cout;
   p.res_ld = Cout;
   p.out_scale = out_scale;
-  p.stats = stats_out;
+  p.stats = so;
   p.stats_ld = Cout;
   ST_CHECK(st_conv1d(p, dtype, s));
+  if (stats_out) ST_CHECK(st_stats_decode(so, (long long)B * Cout, stats_out, s));
   ST_CHECK(st_frames_to_f32(yd, B, Lout, Cout, Cout, y, dtype, s));
   ST_CHECK_HIP(hipDeviceSynchronize());
   (void)hipFree(xd);
   (void)hipFree(wd);
   (void)hipFree(yd);
   (void)hipFree(sx);
+  if (so) (void)hipFree(so);
   if (rd) (void)hipFree(rd);
   return 0;
 }

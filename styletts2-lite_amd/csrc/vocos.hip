@@ -71,9 +71,8 @@ __global__ void __launch_bounds__(256) k_dwconv7(const T* __restrict__ x, long l
     for (int k = 0; k < 6; ++k) win[k] = win[k + 1];
   }
   if (stats) {
-    double* d = stats + (size_t)(slots > 1 ? (blockIdx.x % slots) : 0) * slot_bs + ((size_t)b * stats_ld + c) * 2;
-    atomicAdd(d, a);
-    atomicAdd(d + 1, q);
+    double* d = stats + (size_t)(slots > 1 ? (blockIdx.x % slots) : 0) * slot_bs + ((size_t)b * stats_ld + c) * ST_W;
+    stat_add(d, a, q);
   }
 }
 

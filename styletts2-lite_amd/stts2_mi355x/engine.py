@@ -19,7 +19,8 @@ DTYPES = {"fp32": 0, "bf16": 1, "bf16x3": 2}  # bf16x3: the split-operand accura
 
 _LIB = None
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstts2.so")
+# (STTS_LIB: another build of the same C-ABI revision, for build-against-build A/Bs on one box: tools/gpu/)
+LIB_PATH = os.environ.get("STTS_LIB") or os.path.join(_HERE, "libstts2.so")
 ABI_VERSION = 5  # include/stts2.h STTS_ABI_VERSION: the signatures bound below
 
 c_int, c_ll, c_ull, c_vp, c_fp = ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_void_p, ctypes.c_void_p
