@@ -483,6 +483,10 @@ int stts_abi_version(void);
  *                     groups, 3 MFMAs a product); 3 / 4 = the same on 4- / 8-wave blocks everywhere; 0 = the split
  *                     implicit-GEMM engine (A/B). */
 #define STTS_OPT_BIGSPLIT 25
+/*   STTS_OPT_BIGLA 1 = the bigconv2 engine's 3-tap (and ups[0]'s 2-tap) launches on 8-wave blocks DMA each window
+ *                     two groups ahead into a third LDS buffer, so it lands before its transform; 0 (default) = one
+ *                     group ahead (two buffers).  Bit-identical outputs; measured neutral (A/B). */
+#define STTS_OPT_BIGLA 26
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

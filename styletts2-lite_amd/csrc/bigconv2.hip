@@ -50,9 +50,14 @@ enum { PK_SNAKE = 0, PK_LRELU = 1 };
 // OFS: the second half of the waves (wu >= NW / 2) runs one group behind the first (3 window buffers), so the
 // two waves of each SIMD reach their tile epilogues one group apart and one's epilogue runs beside the other's
 // MFMAs (STTS_OPT_BIGCONV 5 / 6)
-template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C, bool UPS = false, int CO = C, bool OFS = false>
+// LA: window lookahead 2 (3 window buffers): slot sl DMAs window sl + 2 instead of sl + 1, so a window lands a whole
+// group (K taps) before its transform instead of K - 1 or K - 2 taps.  For K <= 3 those 1-2 taps (~1.5 us) are
+// about one LDS-DMA latency under load, so the transform waited on the DMA (STTS_OPT_BIGLA)
+template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C, bool UPS = false, int CO = C, bool OFS = false,
+          bool LA = false>
 struct B2 {
-  static constexpr int NXB = OFS ? 3 : 2;  // window buffers
+  static_assert(!(OFS && LA), "one use of the third window buffer");
+  static constexpr int NXB = (OFS || LA) ? 3 : 2;  // window buffers
   static constexpr int NCOEF = PRO == PK_SNAKE ? 5 : 2;  // coefficient rows per input channel
   static constexpr int NCBW = (C / 32 < NW) ? C / 32 : NW;  // 32-channel output blocks per block tile
   static constexpr int FH = NW / NCBW;   // frame halves per tile (waves per co block)
@@ -181,9 +186,9 @@ __device__ __forceinline__ uint4 f32_to_bf8v(const float* v) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false, bool SP = false>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false>
 __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
-  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA>;
   constexpr int NXB = G::NXB;
   constexpr int TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
   constexpr int NCF = G::NCOEF;
@@ -680,7 +685,13 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   issue_x(0, 0, cur.b, cur.mt);
 #pragma unroll
   for (int s = 0; s < PD; ++s) issue_w(s, 0, cur.ch, s);
-  vm_wait<2 * PD>();  // this wave's window DMA of group 0 landed
+  if constexpr (LA) {  // window 1 as well (slot 0 DMAs window 2)
+    const GCur c1 = NGG > 1 ? advance(cur) : cur;
+    issue_x(1, c1.gi, c1.b, c1.mt);
+    vm_wait<2 * PD + NWIN>();  // this wave's window DMA of group 0 landed
+  } else {
+    vm_wait<2 * PD>();
+  }
   transform(0, 0, cur.b, cur.mt);
 
   // the accumulators of tile tt start at the bias.  Set right after the previous tile's epilogue
@@ -739,7 +750,12 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     // (the extra slot re-issues a harmless window DMA, untransformed and never read, so that every slot's
     // vmcnt waits count the same younger operations)
     const bool windows = sl < NGG;
-    issue_x(sl + 1, nxt.gi, nxt.b, nxt.mt);  // buffer (sl+1) % NXB, last read NXB - 1 slots ago
+    if constexpr (LA) {  // buffer (sl+2) % 3, last read in slot sl - 1 (before this slot's barrier)
+      const GCur nn = sl + 2 < NGG ? advance(nxt) : nxt;
+      issue_x(sl + 2, nn.gi, nn.b, nn.mt);
+    } else {
+      issue_x(sl + 1, nxt.gi, nxt.b, nxt.mt);  // buffer (sl+1) % NXB, last read NXB - 1 slots ago
+    }
     if (!active) {  // the lagging half's first slot: only its share of window 1
       if (windows) {
         vm_wait<0>();
@@ -834,8 +850,24 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       constexpr int TX2 = (NW == 8) ? K - 2 : K - 1;
       if (windows && ((t == TX && (NW != 8 || wu < 4)) || (t == TX2 && NW == 8 && wu >= 4))) {
         lap(6);
-        if (t == K - 1) vm_wait<2 * K>();
-        else vm_wait<2 * (K - 1)>();
+        if constexpr (LA) {
+          // window sl + 1 was DMA'd at the start of slot sl - 1 (slot 0: in the prologue).  Younger: slot sl - 1's K
+          // weight steps (and its epilogue's NST stores when it closed a tile), window sl + 2's DMA, and this slot's
+          // weight steps of taps 0..t
+          constexpr int Y1 = NWIN + 2 * K, Y2 = NWIN + 2 * (K - 1);  // t = K - 1 / K - 2
+          if (t == K - 1) {
+            if (sl == 0) vm_wait<Y1>();
+            else if (post_epi) vm_wait<Y1 + 2 * K + NST>();
+            else vm_wait<Y1 + 2 * K>();
+          } else {
+            if (sl == 0) vm_wait<Y2>();
+            else if (post_epi) vm_wait<Y2 + 2 * K + NST>();
+            else vm_wait<Y2 + 2 * K>();
+          }
+        } else {
+          if (t == K - 1) vm_wait<2 * K>();
+          else vm_wait<2 * (K - 1)>();
+        }
         lap(1);
         transform(sl + 1, nxt.gi, nxt.b, nxt.mt);
         lap(3);
@@ -861,10 +893,10 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false, bool SP = false>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
-  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP, LA>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -887,28 +919,32 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-template <int C, int NW, int K, bool OFS = false, bool SP = false>
+template <int C, int NW, int K, bool OFS = false, bool SP = false, bool LA = false>
 int launch_b2_k(const ConvParams& p, hipStream_t s) {
   if (!p.res) {  // conv1 of an iteration: dilation 1 / 3 / 5, no residual
     if (p.accb) return ST_EINVAL;
     switch (p.dil) {
-      case 1: return launch_b2<C, NW, K, 1, false, false, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
-      case 3: return launch_b2<C, NW, K, 3, false, false, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
-      case 5: return launch_b2<C, NW, K, 5, false, false, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
+      case 1: return launch_b2<C, NW, K, 1, false, false, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
+      case 3: return launch_b2<C, NW, K, 3, false, false, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
+      case 5: return launch_b2<C, NW, K, 5, false, false, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
       default: return ST_EINVAL;
     }
   }
   if (p.dil != 1) return ST_EINVAL;  // conv2: dilation 1, residual, optionally the resblock sum
-  if (p.accb) return launch_b2<C, NW, K, 1, true, true, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
-  if constexpr (!OFS && !SP)
+  if (p.accb) return launch_b2<C, NW, K, 1, true, true, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
+  if constexpr (!OFS && !SP && !LA)
     if (g_opt_exp & 2) return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, true>(p, s);
-  return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, false, false, C, OFS, SP>(p, s);
+  return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
 }
 
 template <int C, int NW, bool OFS = false, bool SP = false>
 int launch_b2_c(const ConvParams& p, hipStream_t s) {
   switch (p.KS) {
-    case 3: return launch_b2_k<C, NW, 3, OFS, SP>(p, s);
+    case 3:
+      if constexpr (NW == 8 && !OFS && C >= 256)  // the window lookahead (B2::LA) where it fits: 8-wave blocks, 3 taps
+        // (C = 128: its 512-row windows leave no room for a third buffer)
+        if (g_opt_bigla) return launch_b2_k<C, NW, 3, OFS, SP, true>(p, s);
+      return launch_b2_k<C, NW, 3, OFS, SP>(p, s);
     case 7: return launch_b2_k<C, NW, 7, OFS, SP>(p, s);
     case 11: return launch_b2_k<C, NW, 11, OFS, SP>(p, s);
     default: return ST_EINVAL;
@@ -920,6 +956,10 @@ int launch_b2_c(const ConvParams& p, hipStream_t s) {
 // STTS_OPT_BIGCONV: 1 = bigconv.hip (v1, A/B); 2 = this engine, 8-wave blocks (one per CU);
 // 3 = this engine, 4-wave blocks (two per CU, C = 256 split into two 128-channel output parts)
 int g_opt_bigconv = 2;
+// STTS_OPT_BIGLA: the 3-tap / 2-tap 8-wave launches with the window lookahead (B2::LA).  Off: measured neutral
+// (profiles/r05_ab_bigla.txt: C = 256 k3 156 -> 161 us, the front-end and ups[0] within 2 %), so the window DMA's
+// latency is not what the 3-tap launches wait on
+int g_opt_bigla = 0;
 int g_opt_skew = 0;
 int g_opt_exp = 0;
 
@@ -964,6 +1004,16 @@ bool st_front_eligible(const ConvParams& p, int dtype) {
 }
 
 int st_bigconv2_front(const ConvParams& p, hipStream_t s) {
+  constexpr bool F = false;
+  if (g_opt_bigla) {
+    if (p.Cout == 1024)
+      return p.res ? launch_b2<1024, 8, 3, 1, true, F, PK_LRELU, FE_CINP, F, F, 1024, F, F, true>(p, s)
+                   : launch_b2<1024, 8, 3, 1, false, F, PK_LRELU, FE_CINP, F, F, 1024, F, F, true>(p, s);
+    if (p.Cout == 512)
+      return p.res ? launch_b2<512, 8, 3, 1, true, F, PK_LRELU, FE_CINP, F, F, 512, F, F, true>(p, s)
+                   : launch_b2<512, 8, 3, 1, false, F, PK_LRELU, FE_CINP, F, F, 512, F, F, true>(p, s);
+    return ST_EINVAL;
+  }
   if (p.Cout == 1024)
     return p.res ? launch_b2<1024, 8, 3, 1, true, false, PK_LRELU, FE_CINP>(p, s)
                  : launch_b2<1024, 8, 3, 1, false, false, PK_LRELU, FE_CINP>(p, s);
@@ -1009,7 +1059,9 @@ bool st_ups_eligible(const ConvParams& p, int dtype) {
 }
 
 int st_bigconv2_ups(const ConvParams& p, hipStream_t s) {
-  if (p.N == 2560 && p.Cout == 256) return launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256>(p, s);
+  if (p.N == 2560 && p.Cout == 256)
+    return g_opt_bigla ? launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256, false, false, true>(p, s)
+                       : launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256>(p, s);
   if (p.N == 640 && p.Cout == 128) return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128>(p, s);
   return ST_EINVAL;
 }

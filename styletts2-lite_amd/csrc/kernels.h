@@ -88,6 +88,7 @@ extern int g_opt_ressplit;
 bool st_bigsplit_eligible(const ConvParams& p, int dtype);
 int st_bigsplit(const ConvParams& p, hipStream_t stream);
 extern int g_opt_bigsplit;  // STTS_OPT_BIGSPLIT
+extern int g_opt_bigla;     // STTS_OPT_BIGLA
 int st_conv1d_engine(const ConvParams& p, int dtype);
 // resblock conv engine (resconv.hip): bf16, C = 32 / 64, 1-D 'same' dilated conv with the
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.

@@ -97,6 +97,21 @@ def test_decoder_deterministic_repeat(kind, B, T, dtype):
     assert np.array_equal(a, b), np.abs(a - b).max()
 
 
+@pytest.mark.parametrize("dtype,B,T", [("bf16", 4, 64), ("bf16x3", 2, 48), ("bf16", 32, 40)])
+def test_bigconv_window_lookahead_bitwise(dtype, B, T):
+    """STTS_OPT_BIGLA (the 3-tap / 2-tap bigconv2 launches DMA each window two groups ahead into a third buffer)
+    changes when a window lands, not what is computed: the decode is bit-identical to the two-buffer engine."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_BIGLA, 0)
+        ref = run("hifigan", B, T, dtype)
+        E.set_option(E.OPT_BIGLA, 1)
+        out = run("hifigan", B, T, dtype)
+    finally:
+        E.reset_options()
+    assert np.array_equal(out, ref), np.abs(out - ref).max()
+
+
 def test_resconv_engine_decoder_ab():
     """bf16 HiFi-GAN decode with the resblock engine on and off: both are the same bf16 model;
     they differ only by fp32 accumulation order (and bf16 rounding of intermediates)."""
