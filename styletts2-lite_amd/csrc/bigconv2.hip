@@ -53,9 +53,12 @@ enum { PK_SNAKE = 0, PK_LRELU = 1 };
 // LA: window lookahead 2 (3 window buffers): slot sl DMAs window sl + 2 instead of sl + 1, so a window lands a whole
 // group (K taps) before its transform instead of K - 1 or K - 2 taps.  For K <= 3 those 1-2 taps (~1.5 us) are
 // about one LDS-DMA latency under load, so the transform waited on the DMA (STTS_OPT_BIGLA)
+// NF: 32-frame accumulator fragments per wave (8: 256 frames; 4: 128 frames, for C = 64, whose two 32-channel
+// output blocks leave 4 frame slices per 8-wave tile: 512-frame windows instead of 1,024)
 template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C, bool UPS = false, int CO = C, bool OFS = false,
-          bool LA = false>
+          bool LA = false, int NF = 8>
 struct B2 {
+  static_assert(NF == 8 || NF == 4, "fragments per wave");
   static_assert(!(OFS && LA), "one use of the third window buffer");
   static constexpr int NXB = (OFS || LA) ? 3 : 2;  // window buffers
   static constexpr int NCOEF = PRO == PK_SNAKE ? 5 : 2;  // coefficient rows per input channel
@@ -63,7 +66,7 @@ struct B2 {
   static constexpr int FH = NW / NCBW;   // frame halves per tile (waves per co block)
   static constexpr int NCO = 32 * NCBW;  // output channels per tile
   static constexpr int NCH = C / NCO;    // output-channel parts per frame tile (tiles per frame range)
-  static constexpr int TM = 256 * FH;    // tile rows (frames)
+  static constexpr int TM = 32 * NF * FH;  // tile rows (frames)
   static constexpr int NG = CINP / 32;   // 32-channel input groups per tile (at most)
   static constexpr int PAD = UPS ? DIL * (K - 1) : DIL * (K - 1) / 2;
   static constexpr int R = TM + DIL * (K - 1);                    // window rows a group needs
@@ -186,9 +189,10 @@ __device__ __forceinline__ uint4 f32_to_bf8v(const float* v) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8>
 __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
-  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF>;
+  constexpr int FW = 32 * NF;  // frames per wave
   constexpr int NXB = G::NXB;
   constexpr int TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
   constexpr int NCF = G::NCOEF;
@@ -490,12 +494,12 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     }
   };
 
-  f32x16 acc[8];
+  f32x16 acc[NF];
   constexpr int NU = SP ? 4 : 2;  // 16-B units of a lane's 16 output channels (SP: fp32)
   constexpr unsigned OES = SP ? 4u : 2u;  // output / residual element bytes
-  constexpr int NST = 8 * NU;  // vector-memory stores of one epilogue (8 fragments x NU)
+  constexpr int NST = NF * NU;  // vector-memory stores of one epilogue (NF fragments x NU)
   auto epilogue = [&](int b, int mt, int ch) __attribute__((always_inline)) {
-    const int q0 = mt * TM + fh * 256 + l32;
+    const int q0 = mt * TM + fh * FW + l32;
     // the lane's 16 consecutive output channels (packing permutation)
     const int co0 = ch * NCO + 32 * cb + 16 * hi;
     // UPS: the lane's 16 columns are channels c0.. of output phase ph; row q -> frame q u + ph - opad
@@ -523,7 +527,8 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     // tap fragments held: one load latency per tile instead of two; STTS_OPT_EXP bit 2)
     // (SP: fp32 residual / running-sum rows, 64 B per fragment: 4 fragments a batch with a residual only, 2 with a
     // residual and a running sum)
-    constexpr int NB = SP ? (RES ? (ACC ? 4 : 2) : 1) : ((RES && !(EPI1 && !ACC)) ? 2 : 1), FB = 8 / NB;
+    constexpr int NB0 = SP ? (RES ? (ACC ? 4 : 2) : 1) : ((RES && !(EPI1 && !ACC)) ? 2 : 1);
+    constexpr int NB = NB0 * NF / 8 > 0 ? NB0 * NF / 8 : 1, FB = NF / NB;  // (the same batch size at NF = 4)
     uint4 rl[FB][NU], al[FB][NU];
     auto unpack16 = [&](const uint4 (&u)[NU], float (&o)[16]) __attribute__((always_inline)) {
       if constexpr (SP) {
@@ -630,7 +635,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
   // per MFMA gap, forced by sched_group_barrier), so the LDS latency is exposed once per group (its
   // first tap) instead of twice per tap.
   const int swz = (l32 >> 2) & 3;
-  bf16x8 fa[2][2], fb0[8], fb1[8];
+  bf16x8 fa[2][2], fb0[NF], fb1[NF];
   auto rd_a = [&](int s, bf16x8 (&a)[2]) __attribute__((always_inline)) {
     const char* ws = wring + (s % RS) * 2048 + l32 * 64;
     a[0] = *reinterpret_cast<const bf16x8*>(ws + ((hi) ^ swz) * 16);
@@ -641,15 +646,15 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     // hoisted out of the loop as K loop-invariant registers (which spill at K = 11)
     int l = l32;
     asm volatile("" : "+v"(l));
-    const int r0 = fh * 256 + l + t * DIL;
+    const int r0 = fh * FW + l + t * DIL;
     u = ((2 * half + hi) ^ ((r0 >> 2) & 3)) * 16;  // rows r0 + 32 f share the swizzle
     return smem + G::OFF_X + (gg % NXB) * (G::WROWS * 64) + r0 * 64;
   };
-  auto rd_b = [&](bf16x8 (&fb)[8], int gg, int t, int half) __attribute__((always_inline)) {
+  auto rd_b = [&](bf16x8 (&fb)[NF], int gg, int t, int half) __attribute__((always_inline)) {
     int u;
     const char* row = brow(gg, t, half, u);
 #pragma unroll
-    for (int f = 0; f < 8; ++f) fb[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
+    for (int f = 0; f < NF; ++f) fb[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
   };
   // [MFMA, ds_read] x n in this order
   auto interleave = [&](int n) __attribute__((always_inline)) {
@@ -702,7 +707,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     ld8_lds(bias_s + co0, *reinterpret_cast<float(*)[8]>(&bb[0]));
     ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
 #pragma unroll
-    for (int f = 0; f < 8; ++f)
+    for (int f = 0; f < NF; ++f)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[f][r] = bb[r];
   };
@@ -790,13 +795,13 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           int u;
           const char* row = brow(gw, t, 1, u);
 #pragma unroll
-          for (int f = 0; f < 8; ++f) {
+          for (int f = 0; f < NF; ++f) {
             acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], fb0[f], acc[f], 0, 0, 0);
             acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], fb0[f], acc[f], 0, 0, 0);
             fb1[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
           }
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
+          for (int i = 0; i < NF; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           }
@@ -804,11 +809,11 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           int u;
           const char* row = brow(gw, t, 1, u);
 #pragma unroll
-          for (int f = 0; f < 8; ++f) {
+          for (int f = 0; f < NF; ++f) {
             acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], fb0[f], acc[f], 0, 0, 0);
             fb1[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
           }
-          interleave(8);
+          interleave(NF);
         }
         const bf16x8& a1 = SP ? a[0] : a[1];  // the second half's weight fragment
         // half 1 of tap t; reads of half 0 of tap t+1 and, once its DMA is in, of its weights
@@ -816,11 +821,11 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           int u;
           const char* row = brow(gw, t + 1, 0, u);
 #pragma unroll
-          for (int f = 0; f < 4; ++f) {
+          for (int f = 0; f < NF / 2; ++f) {
             acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fb1[f], acc[f], 0, 0, 0);
             fb0[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
           }
-          interleave(4);
+          interleave(NF / 2);
           // weights of step s+1: younger VMEM ops are the weight DMAs of steps s+2..s+PD and, while
           // step s+1 precedes this slot's window DMAs (t + 1 < PD), those
           lap(6);
@@ -833,14 +838,14 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
           lap(0);
           rd_a(s + 1, fa[(t + 1) & 1]);
 #pragma unroll
-          for (int f = 4; f < 8; ++f) {
+          for (int f = NF / 2; f < NF; ++f) {
             acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fb1[f], acc[f], 0, 0, 0);
             fb0[f] = *reinterpret_cast<const bf16x8*>(row + f * 2048 + u);
           }
-          interleave(4);
+          interleave(NF / 2);
         } else {
 #pragma unroll
-          for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fb1[f], acc[f], 0, 0, 0);
+          for (int f = 0; f < NF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fb1[f], acc[f], 0, 0, 0);
         }
       }
       // the next window: this wave's DMAs of it are older than the weight DMAs of taps 0..t.  With two
@@ -893,10 +898,10 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
-  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP, LA>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP, LA, NF>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -919,34 +924,35 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-template <int C, int NW, int K, bool OFS = false, bool SP = false, bool LA = false>
+template <int C, int NW, int K, bool OFS = false, bool SP = false, bool LA = false, int NF = 8>
 int launch_b2_k(const ConvParams& p, hipStream_t s) {
+  constexpr bool F = false;
   if (!p.res) {  // conv1 of an iteration: dilation 1 / 3 / 5, no residual
     if (p.accb) return ST_EINVAL;
     switch (p.dil) {
-      case 1: return launch_b2<C, NW, K, 1, false, false, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
-      case 3: return launch_b2<C, NW, K, 3, false, false, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
-      case 5: return launch_b2<C, NW, K, 5, false, false, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
+      case 1: return launch_b2<C, NW, K, 1, F, F, PK_SNAKE, C, F, F, C, OFS, SP, LA, NF>(p, s);
+      case 3: return launch_b2<C, NW, K, 3, F, F, PK_SNAKE, C, F, F, C, OFS, SP, LA, NF>(p, s);
+      case 5: return launch_b2<C, NW, K, 5, F, F, PK_SNAKE, C, F, F, C, OFS, SP, LA, NF>(p, s);
       default: return ST_EINVAL;
     }
   }
   if (p.dil != 1) return ST_EINVAL;  // conv2: dilation 1, residual, optionally the resblock sum
-  if (p.accb) return launch_b2<C, NW, K, 1, true, true, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
-  if constexpr (!OFS && !SP && !LA)
+  if (p.accb) return launch_b2<C, NW, K, 1, true, true, PK_SNAKE, C, F, F, C, OFS, SP, LA, NF>(p, s);
+  if constexpr (!OFS && !SP && !LA && NF == 8)
     if (g_opt_exp & 2) return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, true>(p, s);
-  return launch_b2<C, NW, K, 1, true, false, PK_SNAKE, C, false, false, C, OFS, SP, LA>(p, s);
+  return launch_b2<C, NW, K, 1, true, F, PK_SNAKE, C, F, F, C, OFS, SP, LA, NF>(p, s);
 }
 
-template <int C, int NW, bool OFS = false, bool SP = false>
+template <int C, int NW, bool OFS = false, bool SP = false, int NF = 8>
 int launch_b2_c(const ConvParams& p, hipStream_t s) {
   switch (p.KS) {
     case 3:
       if constexpr (NW == 8 && !OFS && C >= 256)  // the window lookahead (B2::LA) where it fits: 8-wave blocks, 3 taps
         // (C = 128: its 512-row windows leave no room for a third buffer)
         if (g_opt_bigla) return launch_b2_k<C, NW, 3, OFS, SP, true>(p, s);
-      return launch_b2_k<C, NW, 3, OFS, SP>(p, s);
-    case 7: return launch_b2_k<C, NW, 7, OFS, SP>(p, s);
-    case 11: return launch_b2_k<C, NW, 11, OFS, SP>(p, s);
+      return launch_b2_k<C, NW, 3, OFS, SP, false, NF>(p, s);
+    case 7: return launch_b2_k<C, NW, 7, OFS, SP, false, NF>(p, s);
+    case 11: return launch_b2_k<C, NW, 11, OFS, SP, false, NF>(p, s);
     default: return ST_EINVAL;
   }
 }
@@ -1064,6 +1070,31 @@ int st_bigconv2_ups(const ConvParams& p, hipStream_t s) {
                        : launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256>(p, s);
   if (p.N == 640 && p.Cout == 128) return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128>(p, s);
   return ST_EINVAL;
+}
+
+// ---- C = 64 resblock convs (the generator's stage 2 and the 64-channel noise_res) on this engine with 128-frame
+// wave slices (NF = 4): 8-wave blocks of 4 frame slices x 2 output blocks, 512-frame tiles.  STTS_OPT_BIG64 bit 1:
+// the accuracy mode's (replacing the two-pass split resblock engine), bit 2: bf16 (replacing resconv)
+int g_opt_big64 = 1;
+
+bool st_big64_eligible(const ConvParams& p, int dtype) {
+  if (!(((g_opt_big64 & 1) && dtype == ST_SPLIT) || ((g_opt_big64 & 2) && dtype == ST_BF16))) return false;
+  if (p.Cout != 64 || p.Cin != 64 || p.N != 64 || p.nchunks * 32 != 64) return false;
+  if (!(p.KS == 3 || p.KS == 7 || p.KS == 11) || !(p.dil == 1 || p.dil == 3 || p.dil == 5)) return false;
+  if ((p.kw != 0 && p.kw != p.KS) || p.row_off != 0 || p.stride != 1 || p.up != 1 || p.opad != 0) return false;
+  if (p.pad != p.dil * (p.KS - 1) / 2 || p.Lq != p.Lout || p.Lq != p.Lin) return false;
+  if (p.y_row_off || p.y_f32 || p.epi_tanh || p.epi_lrelu || p.epi_gelu || p.reflect_front || p.zc_period || p.res_shift) return false;
+  if (p.pro.mode != (PRO_AFFINE | PRO_SNAKE) || !p.pro.alpha || !p.pro.stats || !p.pro.gamma) return false;
+  if (p.accb && p.stats) return false;
+  if (p.res ? p.dil != 1 : (p.accb != nullptr)) return false;
+  if (!p.y || p.x_ld % 8 || p.y_ld % 8 || (p.res && p.res_ld % 8) || (p.accb && p.acc_ld % 8)) return false;
+  return true;
+}
+
+int st_big64(const ConvParams& p, int dtype, hipStream_t s) {
+  if (dtype == ST_SPLIT) return launch_b2_c<64, 8, false, true, 4>(p, s);
+  if (dtype == ST_BF16) return launch_b2_c<64, 8, false, false, 4>(p, s);
+  return ST_EDTYPE;
 }
 
 // ---- the split-operand accuracy mode (STTS_SPLIT, dtype ST_SPLIT: fp32 frames, bf16 hi + lo operands) on this

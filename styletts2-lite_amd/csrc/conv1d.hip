@@ -893,6 +893,7 @@ int st_conv1d_engine(const ConvParams& p, int dtype) {
   if (g_opt_head && st_head_eligible(q)) return ST_ENGINE_HEAD;
   if (st_front_eligible(q, dtype) || st_ups_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
   if (st_resconv_ups_eligible(q, dtype)) return ST_ENGINE_RESCONV;
+  if (st_big64_eligible(q, dtype)) return dtype == ST_SPLIT ? ST_ENGINE_BIGSPLIT : ST_ENGINE_BIGCONV;
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return ST_ENGINE_RESCONV;
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return ST_ENGINE_BIGCONV;
   if (st_pw_split_eligible(q, dtype) || st_pw_eligible(q, dtype)) return ST_ENGINE_PW;
@@ -921,6 +922,7 @@ int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream) {
   if (st_front_eligible(q, dtype)) return st_bigconv2_front(q, stream);
   if (st_ups_eligible(q, dtype)) return st_bigconv2_ups(q, stream);
   if (st_resconv_ups_eligible(q, dtype)) return st_resconv_ups(q, stream);
+  if (st_big64_eligible(q, dtype)) return st_big64(q, dtype, stream);
   if (g_opt_resconv && st_resconv_eligible(q, dtype)) return st_resconv(q, stream);
   if (g_opt_resconv && st_bigconv_eligible(q, dtype)) return st_bigconv(q, stream);
   if (st_pw_split_eligible(q, dtype)) return st_pw_split(q, stream);

@@ -89,6 +89,10 @@ bool st_bigsplit_eligible(const ConvParams& p, int dtype);
 int st_bigsplit(const ConvParams& p, hipStream_t stream);
 extern int g_opt_bigsplit;  // STTS_OPT_BIGSPLIT
 extern int g_opt_bigla;     // STTS_OPT_BIGLA
+// C = 64 resblock convs on the bigconv2 engine with 128-frame wave slices (bf16 and / or ST_SPLIT, STTS_OPT_BIG64)
+bool st_big64_eligible(const ConvParams& p, int dtype);
+int st_big64(const ConvParams& p, int dtype, hipStream_t stream);
+extern int g_opt_big64;
 int st_conv1d_engine(const ConvParams& p, int dtype);
 // resblock conv engine (resconv.hip): bf16, C = 32 / 64, 1-D 'same' dilated conv with the
 // AdaIN + Snake prologue.  st_conv1d routes eligible launches to it while g_opt_resconv != 0.

@@ -112,6 +112,24 @@ def test_bigconv_window_lookahead_bitwise(dtype, B, T):
     assert np.array_equal(out, ref), np.abs(out - ref).max()
 
 
+@pytest.mark.parametrize("B,T", [(2, 40), (4, 64)])
+def test_big64_bf16_decoder_ab(B, T):
+    """bf16 C = 64 resblock convs on the bigconv2 engine with 128-frame wave slices (STTS_OPT_BIG64 bit 2) against
+    resconv: the same bf16 model, different fp32 accumulation order (and bf16 rounding of intermediates)."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_BIG64, 0)
+        ref = run("hifigan", B, T, "bf16")
+        E.set_option(E.OPT_BIG64, 2)
+        out = run("hifigan", B, T, "bf16")
+    finally:
+        E.reset_options()
+    corr = np.corrcoef(out.ravel(), ref.ravel())[0, 1]
+    err = np.abs(out - ref).max()
+    print(f"big64 bf16 A/B B={B} T={T}: max-abs {err:.3e} corr {corr:.7f}")
+    assert corr > 0.9995 and err < 5e-2
+
+
 def test_resconv_engine_decoder_ab():
     """bf16 HiFi-GAN decode with the resblock engine on and off: both are the same bf16 model;
     they differ only by fp32 accumulation order (and bf16 rounding of intermediates)."""
