@@ -1129,7 +1129,8 @@ int st_bigsplit(const ConvParams& p, hipStream_t s) {
   const int tm8 = p.Cout == 128 ? 512 : 256;
   const long long tiles8 = (long long)((p.Lq + tm8 - 1) / tm8) * p.B;
   // (STTS_OPT_BIGSPLIT 3 = 4-wave blocks everywhere, 4 = 8-wave blocks everywhere: tests)
-  const bool two = g_opt_bigsplit != 4 && (tiles8 < b2_num_cu() || (p.Cout == 128 && p.KS >= 7) || g_opt_bigsplit == 3);
+  // (C = 128 takes them at every K: k3 548 vs 784 us on 8-wave blocks, profiles/r05_ab_bigsplit_modes.txt)
+  const bool two = g_opt_bigsplit != 4 && (tiles8 < b2_num_cu() || p.Cout == 128 || g_opt_bigsplit == 3);
   if (p.Cout == 128) return two ? launch_b2_c<128, 4, false, true>(p, s) : launch_b2_c<128, 8, false, true>(p, s);
   if (p.Cout == 256) return two ? launch_b2_c<256, 4, false, true>(p, s) : launch_b2_c<256, 8, false, true>(p, s);
   return ST_EINVAL;

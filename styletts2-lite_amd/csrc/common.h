@@ -113,12 +113,14 @@ struct Prologue {
 // scaled by 2^48 and split into hi = floor(v 2^16) and lo = (v 2^48 - hi 2^32) in [0, 2^32), added with integer
 // atomics (exact, so any order gives the same total), and read back as hi 2^-16 + lo 2^-48 (one rounding, the same
 // every run).  Range |partial|, |sum| < 2^45, resolution 2^-48 per addend.  An entry is ST_W = 4 words: (hi, lo) of sum x, then
-// of sum x^2.  A non-finite partial adds a poison mark (2^62) to hi, read back as NaN.
+// of sum x^2.  A non-finite or out-of-range partial sets bit 63 of the lo word (ST_POISON, an atomic OR: idempotent,
+// and the lo sums, < 2^32 per addend, never carry into it), read back as NaN.
 constexpr int ST_W = 4;
+constexpr unsigned long long ST_POISON = 0x8000000000000000ull;
 __device__ __forceinline__ void fx_add(double* w, double v) {
   unsigned long long* u = reinterpret_cast<unsigned long long*>(w);
   if (!(v >= -0x1p45 && v <= 0x1p45)) {  // NaN, inf or out of range
-    atomicAdd(u, 0x4000000000000000ull);
+    atomicOr(u + 1, ST_POISON);
     return;
   }
   const double q = v * 0x1p48;
@@ -135,7 +137,7 @@ __device__ __forceinline__ void fx_add(double* w, float v) {
   const unsigned bits = __float_as_uint(v);
   const int e = (int)((bits >> 23) & 255u);
   if (e >= 127 + 45) {  // NaN, inf or |v| >= 2^45
-    atomicAdd(u, 0x4000000000000000ull);
+    atomicOr(u + 1, ST_POISON);
     return;
   }
   if (e == 0) return;  // zero (or a denormal, below the resolution)
@@ -163,8 +165,9 @@ __device__ __forceinline__ void fx_add(double* w, float v) {
 __device__ __forceinline__ double fx_get(const double* w) {
   const long long* u = reinterpret_cast<const long long*>(w);
   const long long hi = u[0];
-  if (hi >= (1ll << 61) || hi <= -(1ll << 61)) return __builtin_nan("");
-  return (double)hi * 0x1p-16 + (double)u[1] * 0x1p-48;
+  const long long lo = u[1];
+  if (lo < 0) return __builtin_nan("");  // poisoned (ST_POISON)
+  return (double)hi * 0x1p-16 + (double)lo * 0x1p-48;
 }
 // add the partial sums a = sum x, q = sum x^2 into the entry e (ST_W words)
 __device__ __forceinline__ void stat_add(double* e, double a, double q) {

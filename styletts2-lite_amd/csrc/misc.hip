@@ -34,17 +34,28 @@ __global__ void __launch_bounds__(256) k_stats_fold(double* __restrict__ st, int
   const int b = i / C, c = i % C;
   // integer (fixed-point) words: the fold is exact and order-free like the producers' atomics (common.h ST_W)
   long long* d = reinterpret_cast<long long*>(st + ((size_t)b * ld + c) * ST_W);
-  long long w[ST_W] = {0, 0, 0, 0};
+  // (the lo words' poison bit, ST_POISON, is OR-ed, not added: two poisoned words must not cancel it)
+  unsigned long long w[ST_W] = {0, 0, 0, 0}, flag[ST_W] = {0, 0, 0, 0};
+  unsigned long long* du = reinterpret_cast<unsigned long long*>(d);
   for (int k = 1; k < S; ++k) {
-    long long* e = d + (size_t)k * slot_bs;
+    unsigned long long* e = du + (size_t)k * slot_bs;
 #pragma unroll
     for (int j = 0; j < ST_W; ++j) {
-      w[j] += e[j];
+      const unsigned long long v = e[j];
+      if (j & 1) {
+        flag[j] |= v & ST_POISON;
+        w[j] += v & ~ST_POISON;
+      } else {
+        w[j] += v;
+      }
       e[j] = 0;
     }
   }
 #pragma unroll
-  for (int j = 0; j < ST_W; ++j) d[j] += w[j];
+  for (int j = 0; j < ST_W; ++j) {
+    if (j & 1) du[j] = ((du[j] & ~ST_POISON) + w[j]) | (du[j] & ST_POISON) | flag[j];
+    else du[j] += w[j];
+  }
 }
 
 __device__ __forceinline__ void atomic_stats(double* st, double a, double q) { stat_add(st, a, q); }

@@ -97,6 +97,22 @@ def test_decoder_deterministic_repeat(kind, B, T, dtype):
     assert np.array_equal(a, b), np.abs(a - b).max()
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
+def test_nan_utterance_stays_isolated(dtype):
+    """A NaN in one utterance's input makes that utterance's InstanceNorm statistics NaN (the fixed-point entry's
+    poison mark, csrc/common.h ST_POISON) and its output NaN, as the reference's InstanceNorm does; the other
+    utterances of the batch are bitwise the same as in a clean batch (statistics are per utterance and channel)."""
+    asr, f0, n, s, nz = decoder_case(3, 16)
+    d = dec("hifigan")
+    bad = asr.clone()
+    bad[1, 7, 5] = float("nan")
+    with torch.no_grad():
+        clean = d(asr.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=nz.cuda(), dtype=dtype).cpu()
+        out = d(bad.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=nz.cuda(), dtype=dtype).cpu()
+    assert torch.isnan(out[1]).all()
+    assert torch.equal(out[0], clean[0]) and torch.equal(out[2], clean[2])
+
+
 @pytest.mark.parametrize("dtype,B,T", [("bf16", 4, 64), ("bf16x3", 2, 48), ("bf16", 32, 40)])
 def test_bigconv_window_lookahead_bitwise(dtype, B, T):
     """STTS_OPT_BIGLA (the 3-tap / 2-tap bigconv2 launches DMA each window two groups ahead into a third buffer)
