@@ -1073,9 +1073,10 @@ int st_bigconv2_ups(const ConvParams& p, hipStream_t s) {
 }
 
 // ---- C = 64 resblock convs (the generator's stage 2 and the 64-channel noise_res) on this engine with 128-frame
-// wave slices (NF = 4): 8-wave blocks of 4 frame slices x 2 output blocks, 512-frame tiles.  STTS_OPT_BIG64 bit 1:
+// wave slices (NF = 4): 4-wave blocks (two per CU) of 2 frame slices x 2 output blocks, 256-frame tiles (bit 4; else
+// 8-wave blocks, 512-frame tiles).  STTS_OPT_BIG64 bit 1:
 // the accuracy mode's (replacing the two-pass split resblock engine), bit 2: bf16 (replacing resconv)
-int g_opt_big64 = 1;
+int g_opt_big64 = 5;  // (SP on 4-wave blocks: 2-7 % faster per launch than 8-wave, profiles/r05_ab_big64.txt)
 
 bool st_big64_eligible(const ConvParams& p, int dtype) {
   if (!(((g_opt_big64 & 1) && dtype == ST_SPLIT) || ((g_opt_big64 & 2) && dtype == ST_BF16))) return false;
@@ -1092,8 +1093,11 @@ bool st_big64_eligible(const ConvParams& p, int dtype) {
 }
 
 int st_big64(const ConvParams& p, int dtype, hipStream_t s) {
-  if (dtype == ST_SPLIT) return launch_b2_c<64, 8, false, true, 4>(p, s);
-  if (dtype == ST_BF16) return launch_b2_c<64, 8, false, false, 4>(p, s);
+  // (bit 4: 4-wave blocks, two per CU, 256-frame tiles; A/B)
+  if (dtype == ST_SPLIT)
+    return (g_opt_big64 & 4) ? launch_b2_c<64, 4, false, true, 4>(p, s) : launch_b2_c<64, 8, false, true, 4>(p, s);
+  if (dtype == ST_BF16)
+    return (g_opt_big64 & 4) ? launch_b2_c<64, 4, false, false, 4>(p, s) : launch_b2_c<64, 8, false, false, 4>(p, s);
   return ST_EDTYPE;
 }
 

@@ -123,8 +123,8 @@ def test_ressplit_engine_ab(B, T):
     assert err < 2e-5
 
 
-@pytest.mark.parametrize("B,T", [(2, 40), (1, 400), (3, 64)])
-def test_big64_split_engine_ab(B, T):
+@pytest.mark.parametrize("B,T,mode", [(2, 40, 5), (1, 400, 5), (3, 64, 5), (2, 40, 1), (3, 64, 1)])
+def test_big64_split_engine_ab(B, T, mode):
     """The accuracy mode's C = 64 resblock convs on the bigconv2 engine with 128-frame wave slices
     (STTS_OPT_BIG64 bit 1, bigconv2.hip NF = 4) against the two-pass split resblock engine (STTS_OPT_BIG64 0): the
     same split arithmetic in a different summation order; B = 1 at 10 s also against the reference golden."""
@@ -132,13 +132,13 @@ def test_big64_split_engine_ab(B, T):
     try:
         E.set_option(E.OPT_BIG64, 0)
         ref = _run("hifigan", B, T, "bf16x3")
-        E.set_option(E.OPT_BIG64, 1)
+        E.set_option(E.OPT_BIG64, mode)  # (5: 4-wave blocks, the default; 1: 8-wave blocks)
         out = _run("hifigan", B, T, "bf16x3")
     finally:
         E.reset_options()
     err = np.abs(out - ref).max()
     g = golden(f"hifigan_T{T}_B1")["out"][0] if T in (16, 40, 400) and B == 1 else None
-    print(f"big64 split A/B B={B} T={T}: max-abs {err:.3e}"
+    print(f"big64 split A/B B={B} T={T} mode {mode}: max-abs {err:.3e}"
           + (f", vs reference golden {np.abs(out[0] - g).max():.3e}" if g is not None else ""))
     assert np.isfinite(out).all() and err < 2e-5
     if g is not None:
