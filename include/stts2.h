@@ -489,7 +489,8 @@ int stts_abi_version(void);
 #define STTS_OPT_BIGLA 26
 /*   STTS_OPT_BIG64 bit 1 = the accuracy mode's C = 64 resblock convs on the bigconv2 engine with 128-frame wave
  *                     slices (instead of the two-pass split resblock engine); bit 2 = the bf16 C = 64 resblock convs on it
- *                     too (instead of resconv); bit 4 = on 4-wave blocks, two per CU (else 8-wave); default 5; 0 = off. */
+ *                     too (instead of resconv); bit 4 = on 4-wave blocks, two per CU (else 8-wave); bit 8 = the accuracy mode's C = 32
+ *                     convs as well (64-frame slices; slower than the split resblock engine, A/B); default 5; 0 = off. */
 #define STTS_OPT_BIG64 27
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */

@@ -58,7 +58,7 @@ enum { PK_SNAKE = 0, PK_LRELU = 1 };
 template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C, bool UPS = false, int CO = C, bool OFS = false,
           bool LA = false, int NF = 8>
 struct B2 {
-  static_assert(NF == 8 || NF == 4, "fragments per wave");
+  static_assert(NF == 8 || NF == 4 || NF == 2, "fragments per wave");
   static_assert(!(OFS && LA), "one use of the third window buffer");
   static constexpr int NXB = (OFS || LA) ? 3 : 2;  // window buffers
   static constexpr int NCOEF = PRO == PK_SNAKE ? 5 : 2;  // coefficient rows per input channel
@@ -1079,8 +1079,13 @@ int st_bigconv2_ups(const ConvParams& p, hipStream_t s) {
 int g_opt_big64 = 5;  // (SP on 4-wave blocks: 2-7 % faster per launch than 8-wave, profiles/r05_ab_big64.txt)
 
 bool st_big64_eligible(const ConvParams& p, int dtype) {
-  if (!(((g_opt_big64 & 1) && dtype == ST_SPLIT) || ((g_opt_big64 & 2) && dtype == ST_BF16))) return false;
-  if (p.Cout != 64 || p.Cin != 64 || p.N != 64 || p.nchunks * 32 != 64) return false;
+  const int C = p.Cout;
+  if (C == 32) {  // bit 8: the accuracy mode's C = 32 convs too (64-frame wave slices, NF = 2; A/B)
+    if (!((g_opt_big64 & 8) && dtype == ST_SPLIT)) return false;
+  } else if (!(((g_opt_big64 & 1) && dtype == ST_SPLIT) || ((g_opt_big64 & 2) && dtype == ST_BF16))) {
+    return false;
+  }
+  if (!(C == 64 || C == 32) || p.Cin != C || p.N != C || p.nchunks * 32 != C) return false;
   if (!(p.KS == 3 || p.KS == 7 || p.KS == 11) || !(p.dil == 1 || p.dil == 3 || p.dil == 5)) return false;
   if ((p.kw != 0 && p.kw != p.KS) || p.row_off != 0 || p.stride != 1 || p.up != 1 || p.opad != 0) return false;
   if (p.pad != p.dil * (p.KS - 1) / 2 || p.Lq != p.Lout || p.Lq != p.Lin) return false;
@@ -1093,6 +1098,7 @@ bool st_big64_eligible(const ConvParams& p, int dtype) {
 }
 
 int st_big64(const ConvParams& p, int dtype, hipStream_t s) {
+  if (p.Cout == 32) return dtype == ST_SPLIT ? launch_b2_c<32, 4, false, true, 2>(p, s) : ST_EDTYPE;
   // (bit 4: 4-wave blocks, two per CU, 256-frame tiles; A/B)
   if (dtype == ST_SPLIT)
     return (g_opt_big64 & 4) ? launch_b2_c<64, 4, false, true, 4>(p, s) : launch_b2_c<64, 8, false, true, 4>(p, s);
