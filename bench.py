@@ -294,18 +294,22 @@ def main():
         g_in = ([torch.from_numpy(a).to(dev) for a in synth.decoder_inputs(global_batch, T, utt0=0)]
                 if rank == 0 else [None] * 4)
         parts = [shard.scatter_from_rank0(g, world, rank, device=dev) for g in g_in]
-        for got, want in zip(parts, (asr, f0, n, s)):  # the scattered shard is this rank's own inputs
-            if not torch.equal(got, want):
-                raise SystemExit(f"bench.py: rank {rank}: scattered inputs differ from the shard's own")
-
-        def step_sg(i):
-            a_, f_, n_, s_ = (shard.scatter_from_rank0(g, world, rank, device=dev) for g in g_in)
-            eng.forward(a_, f_, n_, s_, noise=None, seed=1234 + i, utt_offset=utt0, out=out)
-            shard.gather_to_rank0(out, world, rank)
-        els, _ = timed(step_sg, args.steps, 1)
-        with_scatter_gather = {"value": samples / els, "ms_per_step": els / args.steps * 1e3,
-                               "scattered_bytes_per_step": sum(g.numel() * 4 for g in g_in) if rank == 0 else None,
-                               "gathered_bytes_per_step": global_batch * 600 * T * 4}
+        # the scattered shard must be this rank's own inputs; the verdict is agreed over all ranks (a collective), so
+        # that a mismatch skips this leg everywhere instead of leaving the other ranks waiting in its collectives
+        bad = torch.tensor([0 if all(torch.equal(a_, b_) for a_, b_ in zip(parts, (asr, f0, n, s))) else 1],
+                           dtype=torch.int32, device=dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if bad.item():
+            with_scatter_gather = {"error": "scattered inputs differ from the shards' own inputs"}
+        else:
+            def step_sg(i):
+                a_, f_, n_, s_ = (shard.scatter_from_rank0(g, world, rank, device=dev) for g in g_in)
+                eng.forward(a_, f_, n_, s_, noise=None, seed=1234 + i, utt_offset=utt0, out=out)
+                shard.gather_to_rank0(out, world, rank)
+            els, _ = timed(step_sg, args.steps, 1)
+            with_scatter_gather = {"value": samples / els, "ms_per_step": els / args.steps * 1e3,
+                                   "scattered_bytes_per_step": sum(g.numel() * 4 for g in g_in) if rank == 0 else None,
+                                   "gathered_bytes_per_step": global_batch * 600 * T * 4}
     if args.dump_checksum is not None:  # tests: the audio of every utterance, gathered to rank 0
         step(0)
         full = shard.gather_to_rank0(out, world, rank) if dist else out
