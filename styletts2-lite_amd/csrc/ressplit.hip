@@ -76,7 +76,11 @@ __device__ __forceinline__ void bstore64(Rsrc r, unsigned off, const float (&v)[
 // PASS: 0 = the whole conv (C = 32), 1 = input channels 0-31 of a C = 64 conv -> fp32 partials in
 // p.splitk_ws, 2 = channels 32-63 + the partials + the epilogue.  ACC: the launch adds into the resblock
 // running sum (p.accb / p.acc_div, hifigan.py:336-342) and keeps no statistics.
-template <int NOUT, int K, int DIL, int PASS, bool ACC>
+// PF: the epilogue's residual / running-sum / partial rows are loaded right after the window barrier, so their
+// latency hides behind the tile's MFMAs instead of being exposed per fragment in the epilogue (default; STTS_OPT_EXP
+// 16384 turns it off for A/B: bit-identical, accuracy-mode step 91.4 -> 90.5 ms, k11 residual launches 928 -> 776 us,
+// profiles/r05_ab_ressplit_prefetch.txt)
+template <int NOUT, int K, int DIL, int PASS, bool ACC, bool PF = false>
 __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_ressplit(const ConvParams p) {
   using G = RS<NOUT, K, DIL>;
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, XP = G::XP, WP = G::WP, FW = G::FW;
@@ -208,6 +212,28 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
     if (t + 2 < tend) issue(t + 2, pre);
     __syncthreads();  // (B) windows complete
 
+    // (PF) the epilogue's input rows of this tile, in flight during the MFMAs
+    const int co0 = wn * 32 + hi * 16;
+    const Rsrc rr = make_rsrc(p.res ? reinterpret_cast<const float*>(p.res) + (size_t)b * p.res_bs : nullptr,
+                              p.res ? (unsigned)((size_t)p.Lq * p.res_ld * 4) : 0u);
+    const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const float*>(p.accb) + (size_t)b * p.acc_bs : nullptr,
+                              ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * 4) : 0u);
+    constexpr int NPF = PF ? MT : 1;
+    float rv_pf[NPF][16], av_pf[NPF][16], pp_pf[NPF][16];
+    if constexpr (PF) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int q = mt * BM + wm * FW + mi * 32 + l32;
+        const bool valid = q < p.Lq;
+        if constexpr (PASS == 2) {
+          const unsigned pe = valid ? (unsigned)((((size_t)b * p.Lq + q) * NOUT + co0) * 4) : OOB;
+          bload64(rpart, pe, pp_pf[mi]);
+        }
+        if (p.res) bload64(rr, valid ? (unsigned)((q * p.res_ld + co0) * 4) : OOB, rv_pf[mi]);
+        if constexpr (ACC) bload64(ra, valid ? (unsigned)((q * p.acc_ld + co0) * 4) : OOB, av_pf[mi]);
+      }
+    }
+
     f32x16 acc[MT];
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
@@ -235,12 +261,7 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
     }
 
     // ---- epilogue: lane = frame l32 of block mi, channels co0 + r
-    const int co0 = wn * 32 + hi * 16;
     const Rsrc ry = make_rsrc(reinterpret_cast<float*>(p.y) + (size_t)b * p.y_bs, (unsigned)((size_t)p.Lq * p.y_ld * 4));
-    const Rsrc rr = make_rsrc(p.res ? reinterpret_cast<const float*>(p.res) + (size_t)b * p.res_bs : nullptr,
-                              p.res ? (unsigned)((size_t)p.Lq * p.res_ld * 4) : 0u);
-    const Rsrc ra = make_rsrc(ACC ? reinterpret_cast<const float*>(p.accb) + (size_t)b * p.acc_bs : nullptr,
-                              ACC ? (unsigned)((size_t)p.Lq * p.acc_ld * 4) : 0u);
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int q = mt * BM + wm * FW + mi * 32 + l32;
@@ -258,7 +279,12 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
       ld8_lds(bias_s + co0 + 8, *reinterpret_cast<float(*)[8]>(&bb[8]));
       if constexpr (PASS == 2) {
         float pp[16];
-        bload64(rpart, pe, pp);
+        if constexpr (PF) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) pp[r] = pp_pf[mi][r];
+        } else {
+          bload64(rpart, pe, pp);
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = (pp[r] + acc[mi][r]) + bb[r];
       } else {
@@ -267,13 +293,23 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
       }
       if (p.res) {
         float rv[16];
-        bload64(rr, valid ? (unsigned)((q * p.res_ld + co0) * 4) : OOB, rv);
+        if constexpr (PF) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) rv[r] = rv_pf[mi][r];
+        } else {
+          bload64(rr, valid ? (unsigned)((q * p.res_ld + co0) * 4) : OOB, rv);
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = (v[r] + rv[r]) * p.out_scale;
       }
       if constexpr (ACC) {
         float av[16];
-        bload64(ra, valid ? (unsigned)((q * p.acc_ld + co0) * 4) : OOB, av);
+        if constexpr (PF) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) av[r] = av_pf[mi][r];
+        } else {
+          bload64(ra, valid ? (unsigned)((q * p.acc_ld + co0) * 4) : OOB, av);
+        }
         if (p.acc_div != 0.f) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) v[r] = (av[r] + v[r]) / p.acc_div;  // the reference divides
@@ -307,10 +343,10 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
 
 int g_num_cu_rs = 0;
 
-template <int NOUT, int K, int DIL, int PASS, bool ACC>
-int launch_rs(const ConvParams& p, hipStream_t stream) {
+template <int NOUT, int K, int DIL, int PASS, bool ACC, bool PF = false>
+int launch_rs_pf(const ConvParams& p, hipStream_t stream) {
   using G = RS<NOUT, K, DIL>;
-  auto kern = k_ressplit<NOUT, K, DIL, PASS, ACC>;
+  auto kern = k_ressplit<NOUT, K, DIL, PASS, ACC, PF>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -329,6 +365,13 @@ int launch_rs(const ConvParams& p, hipStream_t stream) {
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, p);
   return (int)hipGetLastError();
+}
+
+template <int NOUT, int K, int DIL, int PASS, bool ACC>
+int launch_rs(const ConvParams& p, hipStream_t stream) {
+  // (the prefetch only where the epilogue reads rows: a residual, a running sum or the pass-1 partials)
+  if (!(g_opt_exp & 16384) && (p.res || ACC || PASS == 2)) return launch_rs_pf<NOUT, K, DIL, PASS, ACC, true>(p, stream);
+  return launch_rs_pf<NOUT, K, DIL, PASS, ACC>(p, stream);
 }
 
 template <int NOUT, int K, int DIL>
