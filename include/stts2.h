@@ -435,8 +435,9 @@ int stts_abi_version(void);
  *                     2: bigconv2 residual epilogue in one load batch; 4: resconv residual prefetched
  *                     one tile ahead. */
 #define STTS_OPT_EXP 13
-/*   STTS_OPT_UPS      1 = the HiFi-GAN ups[0] / ups[1] polyphase upsamplers (N = 2,560 / 640) on the bigconv2
- *                     engine (default); 0 = on conv1d_igemm. */
+/*   STTS_OPT_UPS      1 = the HiFi-GAN ups[0] / ups[1] / ups[2] polyphase upsamplers (N = 2,560 / 640 / 192) on the
+ *                     bigconv2 engine and ups[3] on resconv (default); 2 = ups[2] on conv1d_igemm (A/B); 0 = all on
+ *                     conv1d_igemm. */
 #define STTS_OPT_UPS 14
 /*   STTS_OPT_WGRAD    1 = the bf16 weight gradient of stride-1 convs (stts_conv1d_bwd, training step) on the
  *                     all-taps window kernel k_wgrad_bf16w (default); 0 = the per-tap kernel. */

@@ -56,13 +56,14 @@ enum { PK_SNAKE = 0, PK_LRELU = 1 };
 // NF: 32-frame accumulator fragments per wave (8: 256 frames; 4: 128 frames, for C = 64, whose two 32-channel
 // output blocks leave 4 frame slices per 8-wave tile: 512-frame windows instead of 1,024)
 template <int C, int NW, int K, int DIL, int PRO = PK_SNAKE, int CINP = C, bool UPS = false, int CO = C, bool OFS = false,
-          bool LA = false, int NF = 8>
+          bool LA = false, int NF = 8, int NCB = 0>
 struct B2 {
   static_assert(NF == 8 || NF == 4 || NF == 2, "fragments per wave");
   static_assert(!(OFS && LA), "one use of the third window buffer");
   static constexpr int NXB = (OFS || LA) ? 3 : 2;  // window buffers
   static constexpr int NCOEF = PRO == PK_SNAKE ? 5 : 2;  // coefficient rows per input channel
-  static constexpr int NCBW = (C / 32 < NW) ? C / 32 : NW;  // 32-channel output blocks per block tile
+  // 32-channel output blocks per block tile (NCB: a smaller count, for column counts no power of two divides: ups[2])
+  static constexpr int NCBW = NCB ? NCB : ((C / 32 < NW) ? C / 32 : NW);
   static constexpr int FH = NW / NCBW;   // frame halves per tile (waves per co block)
   static constexpr int NCO = 32 * NCBW;  // output channels per tile
   static constexpr int NCH = C / NCO;    // output-channel parts per frame tile (tiles per frame range)
@@ -189,9 +190,9 @@ __device__ __forceinline__ uint4 f32_to_bf8v(const float* v) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8, int NCB = 0>
 __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
-  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF, NCB>;
   constexpr int FW = 32 * NF;  // frames per wave
   constexpr int NXB = G::NXB;
   constexpr int TM = G::TM, NWIN = G::NWIN, PD = G::PD, RS = G::RS, NCH = G::NCH, NCO = G::NCO;
@@ -898,10 +899,10 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8, int NCB = 0>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
-  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP, LA, NF>;
+  using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF, NCB>;
+  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP, LA, NF, NCB>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -1056,7 +1057,9 @@ int g_opt_ups = 1;
 
 bool st_ups_eligible(const ConvParams& p, int dtype) {
   if (!g_opt_ups || dtype != ST_BF16 || p.up <= 1 || !p.res || p.accb) return false;
-  const bool shape = (p.N == 2560 && p.Cin == 512 && p.Cout == 256) || (p.N == 640 && p.Cin == 256 && p.Cout == 128);
+  // (ups[2], N = 192: STTS_OPT_UPS 1 takes it too, 2 = ups[0] / ups[1] only)
+  const bool shape = (p.N == 2560 && p.Cin == 512 && p.Cout == 256) || (p.N == 640 && p.Cin == 256 && p.Cout == 128) ||
+                     (g_opt_ups == 1 && p.N == 192 && p.Cin == 128 && p.Cout == 64);
   return shape && p.N == p.up * p.Cout && p.Cout % 16 == 0 && p.KS == 2 && (p.kw == 0 || p.kw == 2) &&
          p.dil == 1 && p.stride == 1 && p.pad == 1 && p.row_off == 0 && p.pro.mode == PRO_SNAKE && p.pro.alpha &&
          p.res_shift == 0 && p.y_row_off == 0 && !p.reflect_front && !p.epi_tanh && !p.epi_lrelu && !p.epi_gelu &&
@@ -1069,6 +1072,9 @@ int st_bigconv2_ups(const ConvParams& p, hipStream_t s) {
     return g_opt_bigla ? launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256, false, false, true>(p, s)
                        : launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256>(p, s);
   if (p.N == 640 && p.Cout == 128) return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128>(p, s);
+  // ups[2]: 4-wave blocks of 2 output blocks (one 64-column phase per tile part) x 2 frame slices of 128 frames
+  if (p.N == 192 && p.Cout == 64)
+    return launch_b2<192, 4, 2, 1, true, false, PK_SNAKE, 128, false, true, 64, false, false, false, 4, 2>(p, s);
   return ST_EINVAL;
 }
 
@@ -1124,6 +1130,8 @@ int st_bigsplit(const ConvParams& p, hipStream_t s) {
       return launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256, false, true>(p, s);
     if (p.N == 640 && p.Cout == 128)
       return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128, false, true>(p, s);
+    if (p.N == 192 && p.Cout == 64)
+      return launch_b2<192, 4, 2, 1, true, false, PK_SNAKE, 128, false, true, 64, false, true, false, 4, 2>(p, s);
     return ST_EINVAL;
   }
   if (st_front_eligible(p, ST_BF16)) {

@@ -2026,7 +2026,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_PW: g_opt_pw = (value >= 0 && value <= 2) ? value : 1; return 0;
     case STTS_OPT_SPLITK: g_opt_splitk = value ? 1 : 0; return 0;
     case STTS_OPT_EXP: g_opt_exp = value; return 0;
-    case STTS_OPT_UPS: g_opt_ups = value ? 1 : 0; return 0;
+    case STTS_OPT_UPS: g_opt_ups = (value >= 0 && value <= 2) ? value : 1; return 0;
     case STTS_OPT_WGRAD: g_opt_wgw = value ? 1 : 0; return 0;
     case STTS_OPT_PLAINRC: g_opt_plainrc = value ? 1 : 0; return 0;
     case STTS_OPT_MSDFOLD: g_opt_msdfold = value ? 1 : 0; return 0;

@@ -284,9 +284,10 @@ def test_pw_engine(case):
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-3, atol=1e-1)
 
 
-UPS_CASES = [c for c in CASES if c[0] in ("ups0_u10", "ups1_u5", "ups3_u2")] + [
+UPS_CASES = [c for c in CASES if c[0] in ("ups0_u10", "ups1_u5", "ups2_u3", "ups3_u2")] + [
     ("ups0_u10_long", 512, 256, 20, 1, 10, 1, 5, 0, 700, 2),
     ("ups1_u5_long", 256, 128, 10, 1, 5, 1, 3, 1, 2500, 2),
+    ("ups2_u3_long", 128, 64, 6, 1, 3, 1, 2, 1, 3000, 2),
     ("ups3_u2_long", 64, 32, 4, 1, 2, 1, 1, 0, 9000, 2),
 ]
 
@@ -294,8 +295,9 @@ UPS_CASES = [c for c in CASES if c[0] in ("ups0_u10", "ups1_u5", "ups3_u2")] + [
 @pytest.mark.parametrize("cap", [0, 3])
 @pytest.mark.parametrize("case", UPS_CASES, ids=[c[0] for c in UPS_CASES])
 def test_ups_engine(case, cap):
-    """bf16: the HiFi-GAN ups[0] / ups[1] polyphase upsamplers (Snake prologue, noise-branch residual) on the
-    bigconv2 engine and ups[3] on the resconv engine (STTS_OPT_UPS) against torch fp32 and against the igemm engine on the same launch (same
+    """bf16: the HiFi-GAN ups[0] / ups[1] / ups[2] polyphase upsamplers (Snake prologue, noise-branch residual) on the
+    bigconv2 engine (ups[2]: 4-wave blocks of 2 output blocks x 2 frame slices of 128 frames) and ups[3] on the resconv
+    engine (STTS_OPT_UPS) against torch fp32 and against the igemm engine on the same launch (same
     bf16 operands); cap = 3 makes every workgroup walk many tiles across output parts and utterances."""
     try:
         E.set_option(E.OPT_UPS, 0)
