@@ -1121,10 +1121,15 @@ int g_opt_bigsplit = 1;
 bool st_bigsplit_eligible(const ConvParams& p, int dtype) {
   if (!g_opt_bigsplit || dtype != ST_SPLIT) return false;
   // the bf16 engines' shape rules (frames ld multiples of 8 elements: 32-B aligned fp32 rows)
-  return st_bigconv_eligible(p, ST_BF16) || st_front_eligible(p, ST_BF16) || st_ups_eligible(p, ST_BF16);
+  // (and ups[3], which bf16 runs on resconv)
+  return st_bigconv_eligible(p, ST_BF16) || st_front_eligible(p, ST_BF16) || st_ups_eligible(p, ST_BF16) ||
+         (g_opt_ups == 1 && st_resconv_ups_eligible(p, ST_BF16));
 }
 
 int st_bigsplit(const ConvParams& p, hipStream_t s) {
+  // ups[3] (64 -> 32, x2, N = 64): 4-wave blocks of one 32-column phase per tile part x 4 frame slices of 64 frames
+  if (g_opt_ups == 1 && st_resconv_ups_eligible(p, ST_BF16))
+    return launch_b2<64, 4, 2, 1, true, false, PK_SNAKE, 64, false, true, 32, false, true, false, 2, 1>(p, s);
   if (st_ups_eligible(p, ST_BF16)) {
     if (p.N == 2560 && p.Cout == 256)
       return launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256, false, true>(p, s);
