@@ -433,7 +433,9 @@ int stts_abi_version(void);
 /*   STTS_OPT_EXP      bit mask of engine experiments under A/B (tools/ab_engine.py); 0 = the measured
  *                     defaults.  1: bigconv2 static MFMA priority for the second half of the waves;
  *                     2: bigconv2 residual epilogue in one load batch; 4: resconv residual prefetched
- *                     one tile ahead. */
+ *                     one tile ahead; 32: ups[2] (N = 192) on 4-wave bigconv2 blocks of one output phase per tile
+ *                     part instead of 12-wave blocks of all three phases; 64: the accuracy mode's ups[3] with one
+ *                     output phase per tile part instead of both. */
 #define STTS_OPT_EXP 13
 /*   STTS_OPT_UPS      1 = the HiFi-GAN ups[0] / ups[1] / ups[2] polyphase upsamplers (N = 2,560 / 640 / 192) on the
  *                     bigconv2 engine and ups[3] on resconv (default); 2 = ups[2] on conv1d_igemm (A/B); 0 = all on

@@ -68,6 +68,9 @@ struct B2 {
   static constexpr int NCO = 32 * NCBW;  // output channels per tile
   static constexpr int NCH = C / NCO;    // output-channel parts per frame tile (tiles per frame range)
   static constexpr int TM = 32 * NF * FH;  // tile rows (frames)
+  // UPS tiles whose NCO columns span several output phases (ups[2] on 12-wave blocks: 192 = 3 x 64): the statistics
+  // words of a channel then get one copy per phase too (one writer per word: deterministic sums)
+  static constexpr int NPH = (UPS && NCO > CO) ? NCO / CO : 1;
   static constexpr int NG = CINP / 32;   // 32-channel input groups per tile (at most)
   static constexpr int PAD = UPS ? DIL * (K - 1) : DIL * (K - 1) / 2;
   static constexpr int R = TM + DIL * (K - 1);                    // window rows a group needs
@@ -83,7 +86,7 @@ struct B2 {
   // [FH][CO][2] f32: one copy per frame half, one writer per word, added in a fixed order by the flush
   // (deterministic statistics, common.h ST_W)
   static constexpr int OFF_ST = OFF_BIAS + CO * 4;
-  static constexpr int OFF_W = (OFF_ST + FH * 2 * CO * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
+  static constexpr int OFF_W = (OFF_ST + FH * NPH * 2 * CO * 4 + 1023) / 1024 * 1024;  // [NW waves][RS][2 KB]
   static constexpr int BPC = NW == 4 ? 2 : 1;                     // blocks per CU
   static constexpr int PDMAX_LDS = ((160 * 1024 / BPC - OFF_W - NXB * WROWS * 64) / (NW * 2048)) - 1;
   static constexpr int PD0 = PDMAX_LDS < K ? PDMAX_LDS : K;
@@ -91,7 +94,8 @@ struct B2 {
   static constexpr int OFF_X = OFF_W + NW * RS * 2048; // [NXB][WROWS][64 B]
   static constexpr int LDS = OFF_X + NXB * WROWS * 64;
   static_assert(FH * NCBW == NW && NCH * NCO == C, "wave grid");
-  static_assert(!UPS || NCO <= CO, "one writer per statistics word and tile");
+  static_assert(!UPS || NCO <= CO || (NCO % CO == 0 && NCH == 1), "one writer per statistics word and tile");
+  static_assert(NW == 4 || NW == 8 || (NW == 12 && UPS), "wave counts (12: the N = 192 upsampler)");
   static_assert(LDS * BPC <= 160 * 1024, "LDS budget");
   static_assert(K >= PD && PD >= 2, "weight prefetch stays within one group");
   static_assert(OFF_W % 1024 == 0 && OFF_X % 1024 == 0, "DMA bases");
@@ -191,7 +195,7 @@ __device__ __forceinline__ uint4 f32_to_bf8v(const float* v) {
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
           bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8, int NCB = 0>
-__global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
+__global__ void __launch_bounds__(64 * NW, NW == 12 ? 3 : 2) k_bigconv2(const ConvParams p) {
   using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF, NCB>;
   constexpr int FW = 32 * NF;  // frames per wave
   constexpr int NXB = G::NXB;
@@ -247,7 +251,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
     while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
   }
   for (int i = tid; i < CO; i += NT) bias_s[i] = p.bias ? p.bias[i] : 0.f;
-  for (int i = tid; i < G::FH * 2 * CO; i += NT) st_lds[i] = 0.f;
+  for (int i = tid; i < G::FH * G::NPH * 2 * CO; i += NT) st_lds[i] = 0.f;
 
   // ---------------- weights: step s = (group, tap) -> this wave's 2 KB slice, slot s % RS
   char* wring = smem + G::OFF_W + wu * RS * 2048;
@@ -485,7 +489,7 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       double* d = stats_slot(p, blockIdx.x) + ((size_t)b * p.stats_ld + ci) * ST_W;
       float a = 0.f, q = 0.f;
 #pragma unroll
-      for (int h = 0; h < G::FH; ++h) {
+      for (int h = 0; h < G::FH * G::NPH; ++h) {
         a += st_lds[(h * CO + ci) * 2];
         q += st_lds[(h * CO + ci) * 2 + 1];
         st_lds[(h * CO + ci) * 2] = st_lds[(h * CO + ci) * 2 + 1] = 0.f;
@@ -625,7 +629,8 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv2(const ConvParams p) {
       // half's, so it has one writer and the totals do not depend on wave timing)
       const float s1 = rs16(ts, l32);
       const float s2 = rs16(tq, l32);
-      atomicAdd(st_lds + 2 * (fh * CO + c0 + (l32 >> 1)) + (l32 & 1), (l32 & 1) ? s2 : s1);  // (ds_add: one writer)
+      const int sc = G::NPH > 1 ? fh * G::NPH + ph : fh;  // (this frame half's / phase's copy)
+      atomicAdd(st_lds + 2 * (sc * CO + c0 + (l32 >> 1)) + (l32 & 1), (l32 & 1) ? s2 : s1);  // (ds_add: one writer)
     }
     lap(9);
   };
@@ -1072,9 +1077,14 @@ int st_bigconv2_ups(const ConvParams& p, hipStream_t s) {
     return g_opt_bigla ? launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256, false, false, true>(p, s)
                        : launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256>(p, s);
   if (p.N == 640 && p.Cout == 128) return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128>(p, s);
-  // ups[2]: 4-wave blocks of 2 output blocks (one 64-column phase per tile part) x 2 frame slices of 128 frames
-  if (p.N == 192 && p.Cout == 64)
-    return launch_b2<192, 4, 2, 1, true, false, PK_SNAKE, 128, false, true, 64, false, false, false, 4, 2>(p, s);
+  // ups[2]: 12-wave blocks (three per SIMD) of all 6 output blocks (the 3 phases) x 2 frame slices of 128 frames, so each
+  // window is DMA'd and transformed once instead of once per phase: 668 -> 479 us (profiles/r05_ab_ups12.txt).
+  // STTS_OPT_EXP bit 32: 4-wave blocks of 2 output blocks (one 64-column phase per tile part), as before (A/B)
+  if (p.N == 192 && p.Cout == 64) {
+    if (g_opt_exp & 32)
+      return launch_b2<192, 4, 2, 1, true, false, PK_SNAKE, 128, false, true, 64, false, false, false, 4, 2>(p, s);
+    return launch_b2<192, 12, 2, 1, true, false, PK_SNAKE, 128, false, true, 64, false, false, false, 4, 6>(p, s);
+  }
   return ST_EINVAL;
 }
 
@@ -1127,16 +1137,24 @@ bool st_bigsplit_eligible(const ConvParams& p, int dtype) {
 }
 
 int st_bigsplit(const ConvParams& p, hipStream_t s) {
-  // ups[3] (64 -> 32, x2, N = 64): 4-wave blocks of one 32-column phase per tile part x 4 frame slices of 64 frames
-  if (g_opt_ups == 1 && st_resconv_ups_eligible(p, ST_BF16))
-    return launch_b2<64, 4, 2, 1, true, false, PK_SNAKE, 64, false, true, 32, false, true, false, 2, 1>(p, s);
+  // ups[3] (64 -> 32, x2, N = 64): 4-wave blocks of 2 output blocks (both 32-column phases) x 2 frame slices of 64 frames
+  // tiles of both phases, 2 output blocks x 2 frame slices of 64 frames, each window transformed once: 1076 -> 908 us
+  // (profiles/r05_ab_ups12.txt; STTS_OPT_EXP bit 64: one phase per tile part, as before)
+  if (g_opt_ups == 1 && st_resconv_ups_eligible(p, ST_BF16)) {
+    if (g_opt_exp & 64)
+      return launch_b2<64, 4, 2, 1, true, false, PK_SNAKE, 64, false, true, 32, false, true, false, 2, 1>(p, s);
+    return launch_b2<64, 4, 2, 1, true, false, PK_SNAKE, 64, false, true, 32, false, true, false, 2, 2>(p, s);
+  }
   if (st_ups_eligible(p, ST_BF16)) {
     if (p.N == 2560 && p.Cout == 256)
       return launch_b2<2560, 8, 2, 1, true, false, PK_SNAKE, 512, false, true, 256, false, true>(p, s);
     if (p.N == 640 && p.Cout == 128)
       return launch_b2<640, 4, 2, 1, true, false, PK_SNAKE, 256, false, true, 128, false, true>(p, s);
-    if (p.N == 192 && p.Cout == 64)
-      return launch_b2<192, 4, 2, 1, true, false, PK_SNAKE, 128, false, true, 64, false, true, false, 4, 2>(p, s);
+    if (p.N == 192 && p.Cout == 64) {  // (12-wave blocks as bf16: 1167 -> 926 us; bit 32: the 4-wave blocks)
+      if (g_opt_exp & 32)
+        return launch_b2<192, 4, 2, 1, true, false, PK_SNAKE, 128, false, true, 64, false, true, false, 4, 2>(p, s);
+      return launch_b2<192, 12, 2, 1, true, false, PK_SNAKE, 128, false, true, 64, false, true, false, 4, 6>(p, s);
+    }
     return ST_EINVAL;
   }
   if (st_front_eligible(p, ST_BF16)) {

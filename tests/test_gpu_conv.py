@@ -314,3 +314,23 @@ def test_ups_engine(case, cap):
     assert err <= 2 ** -7 * scale, f"{case[0]}: ups engine vs igemm differ by {err}"
     # (per-channel fp32 sums over up to 1.4 M outputs, accumulated in a different order by the two engines)
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-3, atol=1e-1)
+
+
+@pytest.mark.parametrize("cap", [0, 5])
+@pytest.mark.parametrize("case", [c for c in UPS_CASES if c[0].startswith("ups2")], ids=lambda c: c[0])
+def test_ups2_wave_layouts(case, cap):
+    """bf16 ups[2] (N = 192 = 3 phases x 64) on bigconv2's 12-wave blocks (all three phases in one tile: each window
+    DMA'd and transformed once, one statistics copy per phase and frame slice) against the 4-wave blocks of one phase
+    per tile part (STTS_OPT_EXP bit 32): every output is the same MFMA chain, so the outputs are bitwise equal; the
+    per-channel statistics are the same sums in another fp32 order.  cap = 5 makes workgroups walk many tiles across
+    utterances."""
+    try:
+        E.set_option(E.OPT_GRID_CAP, cap)
+        E.set_option(E.OPT_EXP, 32)
+        _, y0, s0 = run_case(case, "bf16", res_tr=True)
+        E.set_option(E.OPT_EXP, 0)
+        _, y1, s1 = run_case(case, "bf16", res_tr=True)
+    finally:
+        E.reset_options()
+    assert torch.equal(y1, y0), f"{case[0]}: 12-wave vs 4-wave outputs differ by {(y1 - y0).abs().max().item()}"
+    np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-5, atol=1e-2)

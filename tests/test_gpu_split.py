@@ -168,3 +168,25 @@ def test_bigsplit_engine_ab(B, T, mode, front):
     assert np.isfinite(out).all() and err < 2e-5
     if g is not None:
         assert np.abs(out[0] - g).max() < 1e-3
+
+
+@pytest.mark.parametrize("B,T,exp", [(2, 40, 32), (1, 400, 32), (3, 64, 64), (1, 400, 64)])
+def test_split_ups_wave_layouts(B, T, exp):
+    """The accuracy mode's ups[2] / ups[3] tiles that hold every output phase (the defaults: ups[2] on 12-wave blocks,
+    ups[3] with 2 output blocks x 2 frame slices) against one phase per tile part (STTS_OPT_EXP bit 32: ups[2]; bit 64:
+    ups[3]): outputs are the same MFMA chains, only the InstanceNorm statistics' fp32 order differs."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_EXP, exp)
+        ref = _run("hifigan", B, T, "bf16x3")
+        E.set_option(E.OPT_EXP, 0)
+        out = _run("hifigan", B, T, "bf16x3")
+    finally:
+        E.reset_options()
+    err = np.abs(out - ref).max()
+    g = golden(f"hifigan_T{T}_B1")["out"][0] if T in (16, 40, 400) and B == 1 else None
+    print(f"split ups layouts B={B} T={T} exp {exp}: max-abs {err:.3e}"
+          + (f", vs reference golden {np.abs(out[0] - g).max():.3e}" if g is not None else ""))
+    assert np.isfinite(out).all() and err < 2e-5
+    if g is not None:
+        assert np.abs(out[0] - g).max() < 1e-3
