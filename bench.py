@@ -142,14 +142,16 @@ def roofline(recs, dtype, steps, step_ms, B, T, decoder):
     roof["conv_engines"] = {k: {"ms_per_step": v["ms"] / steps, "launches_per_step": v["launches"] // steps,
                                 "tflops": v["flops"] / (v["ms"] / 1e3) / 1e12,
                                 "alg_GBps": v["bytes"] / (v["ms"] / 1e3) / 1e9} for k, v in sorted(fam.items())}
-    tr = _pmc_traffic(name, dtype, B, T, decoder)
+    tr = _pmc_traffic(name, dtype, B, T, decoder, f["launches"] // steps)
     if tr is not None:
         roof["traffic"] = tr["hbm_bytes_per_launch"]
         roof["traffic_source"] = tr["source"]
     return roof
 
 
-def _pmc_traffic(kernel, dtype, B, T, decoder):
+def _pmc_traffic(kernel, dtype, B, T, decoder, launches_per_step=None):
+    # (a file whose passes counted another number of launches of the family per step was taken on another routing:
+    # skipped, so the traffic figure never describes a different set of launches than `achieved`)
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
         try:
@@ -158,7 +160,8 @@ def _pmc_traffic(kernel, dtype, B, T, decoder):
         except (OSError, ValueError):
             continue
         if (d.get("kernel") == kernel and d.get("decoder") == decoder and d.get("dtype") == dtype
-                and d.get("batch") == B and d.get("frames") == T):
+                and d.get("batch") == B and d.get("frames") == T
+                and (launches_per_step is None or d.get("dispatches", 0) == 2 * launches_per_step)):
             return {"hbm_bytes_per_launch": d["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
     return None
 
