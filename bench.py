@@ -217,10 +217,16 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}")
     cpu = args.selftest_cpu
+    # STTS_BENCH_SHARE_GPU=1 (hardware rehearsal of the N-rank path on a one-GPU box; never a scaling figure): every
+    # rank decodes on cuda:0 and the collectives run on gloo, staged through host memory (shard.py)
+    share = world > 1 and not cpu and os.environ.get("STTS_BENCH_SHARE_GPU") == "1"
     dist = None
     if world > 1:
         import torch.distributed as dist
         if cpu:
+            dist.init_process_group("gloo")
+        elif share:
+            torch.cuda.set_device(0)
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
@@ -228,6 +234,7 @@ def main():
     elif not cpu:
         torch.cuda.set_device(0)
     dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
+    cdev = torch.device("cpu") if (cpu or share) else dev  # where the bench's own small collective tensors live
 
     def sync():
         if not cpu:
@@ -274,7 +281,7 @@ def main():
         el = time.perf_counter() - t0
         per = [evs[i].elapsed_time(evs[i + 1]) for i in range(k)] if evs else [el * 1e3 / k] * k
         if dist:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = t.item()
             dist.barrier()
@@ -300,7 +307,7 @@ def main():
         # the scattered shard must be this rank's own inputs; the verdict is agreed over all ranks (a collective), so
         # that a mismatch skips this leg everywhere instead of leaving the other ranks waiting in its collectives
         bad = torch.tensor([0 if all(torch.equal(a_, b_) for a_, b_ in zip(parts, (asr, f0, n, s))) else 1],
-                           dtype=torch.int32, device=dev)
+                           dtype=torch.int32, device=cdev)
         dist.all_reduce(bad, op=dist.ReduceOp.MAX)
         if bad.item():
             with_scatter_gather = {"error": "scattered inputs differ from the shards' own inputs"}
@@ -403,7 +410,8 @@ def main():
         "config": {"workload": f"{args.decoder} decoder, batch {B_local}/GPU x {T * 600 // 24000}-s utterances "
                                f"({T} asr frames, {600 * T} samples each)",
                    "global_batch": global_batch, "frames": T, "decoder": args.decoder,
-                   "parallelism": f"dp{world} (utterance shards, no collective on the audio path)"},
+                   "parallelism": (f"dp{world} rehearsal: {world} ranks sharing cuda:0 over gloo (STTS_BENCH_SHARE_GPU)" if share
+                                   else f"dp{world} (utterance shards, no collective on the audio path)")},
         "x_realtime_per_gpu": value / world / 24000.0,
         "hbm_fraction": a["bytes"][args.dtype] * value / world / PEAK_HBM,
         "mfma_fraction": a["flops"] * value / world / PEAK_MFMA[args.dtype],

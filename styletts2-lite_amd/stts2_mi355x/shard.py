@@ -20,6 +20,13 @@ def shard_range(global_batch: int, world: int, rank: int):
 _DTYPES = ("float32", "float64", "float16", "bfloat16", "int64", "int32", "uint8")
 
 
+def _staged(group, dev):
+    """gloo runs scatter / gather / all_gather on host tensors only: device tensors are staged through host memory
+    there (the CPU tests and bench.py's shared-GPU rehearsal); RCCL takes them in place."""
+    import torch.distributed as dist
+    return dev.type != "cpu" and dist.get_backend(group) == "gloo"
+
+
 def scatter_from_rank0(t, world, rank, device=None, group=None):
     """Rank 0's [N, ...] tensor `t` (N = the global batch) split into the contiguous utterance shards of
     `shard_range(N, world, r)`: every rank gets its own [count_r, ...] slice (rank r's shard of the global
@@ -29,6 +36,9 @@ def scatter_from_rank0(t, world, rank, device=None, group=None):
     import torch
     import torch.distributed as dist
     dev = torch.device(device) if device is not None else (t.device if t is not None else torch.device("cpu"))
+    out_dev = dev
+    if _staged(group, dev):
+        dev = torch.device("cpu")
     if rank == 0:
         if t is None:
             raise ValueError("scatter_from_rank0: rank 0 must hold the global tensor")
@@ -56,7 +66,7 @@ def scatter_from_rank0(t, world, rank, device=None, group=None):
         dist.scatter(recv, parts, src=0, group=group)
     else:
         dist.scatter(recv, None, src=0, group=group)
-    return recv[: spans[rank][1]]
+    return recv[: spans[rank][1]].to(out_dev)
 
 
 def gather_to_rank0(t, world, rank, group=None):
@@ -64,6 +74,9 @@ def gather_to_rank0(t, world, rank, group=None):
     Uses torch.distributed (RCCL on the GPU box, gloo on CPU) — output gather only."""
     import torch
     import torch.distributed as dist
+    out_dev = t.device
+    if _staged(group, t.device):
+        t = t.cpu()
     sizes = [torch.zeros(1, dtype=torch.long, device=t.device) for _ in range(world)]
     dist.all_gather(sizes, torch.tensor([t.shape[0]], device=t.device), group=group)
     mx = int(max(s.item() for s in sizes))
@@ -72,6 +85,6 @@ def gather_to_rank0(t, world, rank, group=None):
     bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
     if rank == 0:
         dist.gather(pad, bufs, dst=0, group=group)
-        return torch.cat([b[: int(s.item())] for b, s in zip(bufs, sizes)])
+        return torch.cat([b[: int(s.item())] for b, s in zip(bufs, sizes)]).to(out_dev)
     dist.gather(pad, None, dst=0, group=group)
     return None
