@@ -520,6 +520,12 @@ int stts_profile_launch(long long i, int* shape, double* ms_flops_bytes);
 int stts_calib_traffic(int mode, void* buf, long long rows, int ld, int tile, int halo, int grid, float* sink,
                        void* stream);
 
+/* ---- testing hook (not a product path): the InstanceNorm statistics entry of every engine (csrc/common.h fx_add /
+ * fx_get) summing n parts (mode 0: float parts, the MFMA epilogues' form; 1: double parts), each added by its own
+ * lane in no fixed order; out[0] = the total read back (NaN when a part or the total is outside the entry's range).
+ * entry: 4 doubles of device scratch; out: 1 double on the device. */
+int stts_test_fxsum(int mode, const void* parts, long long n, double* entry, double* out, void* stream);
+
 /* ---- testing hook (not a product path): one conv1d_igemm launch on fp32 frames.
  * x [B][Lin][Cin] frames; w in nn.Conv1d [Cout][Cin][K] / nn.ConvTranspose1d [Cin][Cout][K] layout;
  * pro_mode bitmask 1 = AdaIN (instance stats of x, gamma_beta [B][2*Cin]), 2 = Snake (alpha [Cin]),

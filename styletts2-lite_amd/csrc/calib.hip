@@ -96,7 +96,29 @@ __global__ void __launch_bounds__(256) k_calib(int mode, char* buf, long long ro
   if (tid == 0) sink[blockIdx.x] = acc;
 }
 
+// fixed-point statistics entry (common.h fx_add / fx_get): every part added by its own lane, then read back
+__global__ void k_fx_add(int mode, const void* parts, long long n, double* entry) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    if (mode == 0) fx_add(entry, reinterpret_cast<const float*>(parts)[i]);
+    else fx_add(entry, reinterpret_cast<const double*>(parts)[i]);
+  }
+}
+__global__ void k_fx_get(const double* entry, double* out) {
+  if (threadIdx.x == 0) out[0] = fx_get(entry);
+}
+
 }  // namespace
+
+// testing hook (include/stts2.h): the total of n parts through one fixed-point entry
+extern "C" int stts_test_fxsum(int mode, const void* parts, long long n, double* entry, double* out, void* stream) {
+  if ((mode != 0 && mode != 1) || !parts || n <= 0 || !entry || !out) return ST_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  ST_CHECK_HIP(hipMemsetAsync(entry, 0, ST_W * sizeof(double), s));
+  const long long g = (n + 255) / 256;
+  hipLaunchKernelGGL(k_fx_add, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, mode, parts, n, entry);
+  hipLaunchKernelGGL(k_fx_get, dim3(1), dim3(64), 0, s, entry, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int stts_calib_traffic(int mode, void* buf, long long rows, int ld, int tile, int halo, int grid,
                                   float* sink, void* stream) {

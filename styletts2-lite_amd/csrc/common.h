@@ -162,11 +162,16 @@ __device__ __forceinline__ void fx_add(double* w, float v) {
   if (hi) atomicAdd(u, hi);
   if (lo) atomicAdd(u + 1, lo);
 }
+// Read back.  A total outside the range (|sum| >= 2^45: hi beyond +-2^61) reads as NaN too, like a poisoned entry: the
+// int64 hi word only wraps once |sum| passes 2^47, so a total that grew past the range through many in-range partials
+// reads as NaN, not as a wrong mean / variance (unless it ran past 2^47 and wrapped back into range: true |sum| within
+// 2^45 of a non-zero multiple of 2^48, beyond 7 x 10^13)
 __device__ __forceinline__ double fx_get(const double* w) {
   const long long* u = reinterpret_cast<const long long*>(w);
   const long long hi = u[0];
   const long long lo = u[1];
   if (lo < 0) return __builtin_nan("");  // poisoned (ST_POISON)
+  if (hi >= (1ll << 61) || hi < -(1ll << 61)) return __builtin_nan("");  // out of range
   return (double)hi * 0x1p-16 + (double)lo * 0x1p-48;
 }
 // add the partial sums a = sum x, q = sum x^2 into the entry e (ST_W words)

@@ -49,6 +49,38 @@ class AdamW(torch.optim.Optimizer):
                 if p in self.state and "step" in self.state[p]:
                     self.state[p]["step"] = torch.tensor(n)
 
+    def state_dict(self):
+        """torch's layout, with the device step counts folded in first (capturable), so a checkpoint carries the
+        real step and a resume gets the right bias correction."""
+        if self._dev_state:
+            self.sync_steps()
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        """torch's loader; then every group's device step count (capturable) is re-seeded IN PLACE from the loaded
+        state["step"], so a hipGraph recorded against that count keeps its pointer and replays the loaded step."""
+        # (the moments too: torch's loader makes new tensors, while a recorded graph holds the old buffers' pointers;
+        # the loaded values are copied into the existing buffers)
+        old = {p: {k: st[k] for k in ("exp_avg", "exp_avg_sq") if k in st} for p, st in self.state.items()}
+        super().load_state_dict(state_dict)
+        with torch.no_grad():
+            for p, bufs in old.items():
+                st = self.state.get(p)
+                for k, buf in bufs.items():
+                    if st is not None and k in st and st[k].shape == buf.shape and st[k].device == buf.device:
+                        buf.copy_(st[k])
+                        st[k] = buf
+        views = self.__dict__.get("_step_views")
+        if views is not None:
+            views.clear()  # (the loaded step tensors are new objects)
+        for gi, dev in self._dev_state.items():
+            steps = {float(self.state[p]["step"]) for p in self.param_groups[gi]["params"]
+                     if p in self.state and "step" in self.state[p]}
+            if len(steps) > 1:
+                raise ValueError(f"capturable AdamW keeps one step count per group; group {gi} loaded {sorted(steps)}")
+            with torch.no_grad():
+                dev[0].fill_(steps.pop() if steps else 0.0)
+
     def _step_capturable(self, gi, group):
         beta1, beta2 = group["betas"]
         items = []

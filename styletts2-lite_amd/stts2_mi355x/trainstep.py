@@ -53,6 +53,13 @@ from .losses import DiscriminatorLoss, GeneratorLoss, MultiResolutionSTFTLoss, s
 from .optim import AdamW
 
 
+def seed_i64(seed):
+    """The 64 seed bits the eager path passes as an unsigned long long (training._SourceFn), as the int64 the
+    recorded graph's kernel reads (same bits: no seed maps to another stream on one path only)."""
+    v = int(seed) & (2 ** 64 - 1)
+    return v - 2 ** 64 if v >= 2 ** 63 else v
+
+
 class TrainStep:
     def __init__(self, decoder, mpd, msd, lr_dec=1e-5, lr_disc=1e-4, lambda_mel=5.0, lambda_gen=1.0, dtype="fp32",
                  freeze_d_in_g=True, capture=False, predictor=None, style_encoder=None, lr_pred=1e-4, lr_style=1e-5,
@@ -104,6 +111,11 @@ class TrainStep:
         """The recorded step (graph=True): see the module docstring."""
         if seed is None and noise is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # (a CPU draw: no device sync)
+        if self.decoder.training:
+            # train mode draws the F0 / N smoothing with Python's random on the host (hifigan.py:447-455): a recorded
+            # graph would replay the first draw forever
+            raise ValueError("TrainStep(graph=True) needs the decoder in eval mode (its train-mode smoothing is a "
+                             "host-side random draw per step)")
         self._calls += 1
         if self._calls == 1:  # eager: the kernels' one-time setup, the optimizers' device state
             return self._step(en, F0, N, s, wav, noise, seed, None, None, None, None)
@@ -122,23 +134,38 @@ class TrainStep:
                 self._static_out = self._step(st["en"], st["F0"], st["N"], st["s"], st["wav"], st["noise"],
                                               None if st["noise"] is not None else st["seed"], None, None, None, None)
             self._graph = g
+            # the learning rates are host scalars baked into the recorded AdamW launches
+            self._lrs = self._lr_snapshot()
         else:
+            if self._lr_snapshot() != self._lrs:
+                raise ValueError("TrainStep(graph=True): a learning rate changed after the step was recorded (the "
+                                 "replayed AdamW launches carry the recorded values); build a new TrainStep")
             self._fill(en, F0, N, s, wav, noise, seed)
         self._graph.replay()
         return self._static_out
 
+    def _lr_snapshot(self):
+        return [g["lr"] for o in self.opt.values() for g in o.param_groups]
+
     def _fill(self, en, F0, N, s, wav, noise, seed):
         st = self.static_inputs
         with torch.no_grad():
-            for k, t in (("en", en), ("F0", F0), ("N", N), ("s", s), ("wav", wav)):
+            for k, t in (("en", en), ("F0", F0), ("N", N), ("s", s), ("wav", wav), ("noise", noise)):
+                if t is None:
+                    continue
+                if st[k] is None:
+                    raise ValueError("TrainStep(graph=True): the graph was recorded with the device RNG (noise=None)")
+                if tuple(t.shape) != tuple(st[k].shape) or t.dtype != st[k].dtype:
+                    # (copy_ would broadcast a size-1 dimension silently): a batch of another crop length needs
+                    # its own recording
+                    raise ValueError(f"TrainStep(graph=True): input {k} is {tuple(t.shape)} {t.dtype}, the graph "
+                                     f"was recorded for {tuple(st[k].shape)} {st[k].dtype}")
                 if t.data_ptr() != st[k].data_ptr():
                     st[k].copy_(t)
-            if noise is not None:
-                if st["noise"] is None:
-                    raise ValueError("TrainStep(graph=True): the graph was recorded with the device RNG (noise=None)")
-                st["noise"].copy_(noise)
-            else:
-                st["seed"].fill_(int(seed) & (2 ** 63 - 1))
+            if noise is None:
+                if st["noise"] is not None:
+                    raise ValueError("TrainStep(graph=True): the graph was recorded with explicit noise, pass noise=")
+                st["seed"].fill_(seed_i64(seed))
 
     def _text_front(self, text):
         """train.py:217-251: the text encoder, asr, the predictor's forward and the crops."""

@@ -254,8 +254,9 @@ def _decode(case, dtype, sl=slice(None)):
 def test_config3_fp32_batch32_pinned():
     """Config 3's batch (B = 32 x 10 s) on the production path (default options: one statistics slot,
     full persistent grids, multi-GB workspace offsets) in fp32: utterance 0 equals the reference golden
-    within the north-star 1e-3, and every utterance equals its own B = 1 decode within 1e-5 (the
-    batch path changes only the order of fp64 statistics atomics)."""
+    within the north-star 1e-3, and every utterance equals its own B = 1 decode within 1e-5.  (The
+    statistics are order-free fixed-point sums, so the batch and B = 1 paths differ only where B = 1
+    routes launches to other engines: split-K front-end convs, 4-wave tiles, statistics slots.)"""
     case = _cfg3_batch()
     out = _decode(case, "fp32")
     assert out.shape == (32, 1, 240000)
@@ -288,6 +289,33 @@ def test_config3_bf16_batch32_shipped_mode():
     # utterance 0 against the reference golden as well
     g = golden("hifigan_T400_B1")["out"][0]
     print(f"config 3 bf16 utterance 0 vs reference golden: {np.abs(out[0] - g).max():.3e}")
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32", "bf16x3"])
+def test_config4_rank_shard_bitwise(dtype):
+    """Config 4 (BASELINE configs[3]: 256 utterances sharded 8-way, 32 per rank) on one GPU: a B = 64 x 10 s
+    decode with device-RNG noise equals, bit for bit, the two B = 32 decodes that two ranks would run on its
+    halves (utt_offset 0 and 32).  So an N-rank job's audio does not depend on N while every rank's batch routes
+    every launch to the same engine (tiles are per utterance and the InstanceNorm sums are
+    order-free fixed-point integers, so which workgroup computes a tile, and how many statistics slots there
+    are, does not matter; what can change the bits is a small-batch engine such as split-K)."""
+    asr, f0, n, s, _ = decoder_case(64, 400)
+    d = dec("hifigan")
+
+    def go(sl, off):
+        with torch.no_grad():
+            out = d(asr[sl].cuda(), f0[sl].cuda(), n[sl].cuda(), s[sl].cuda(), noise=None, seed=1234,
+                    utt_offset=off, dtype=dtype)
+        torch.cuda.synchronize()
+        return out.cpu()
+
+    full = go(slice(0, 64), 0)
+    lo = go(slice(0, 32), 0)
+    hi = go(slice(32, 64), 32)
+    assert full.shape == (64, 1, 240000)
+    assert torch.isfinite(full).all()
+    assert torch.equal(full[:32], lo), (full[:32] - lo).abs().max().item()
+    assert torch.equal(full[32:], hi), (full[32:] - hi).abs().max().item()
 
 
 def test_default_noise_follows_torch_rng():

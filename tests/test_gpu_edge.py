@@ -9,6 +9,8 @@ computed in the test on the same formula weights, inputs and noise:
 
 Tolerances: fp32 max-abs <= 1e-3 (north star); bf16 correlation >= 0.99 with the fp32 oracle.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -148,3 +150,42 @@ def test_small_tiles_do_not_change_results():
     finally:
         E.set_option(6, 1)
     assert (outs[0] - outs[1]).abs().max().item() < 1e-5
+
+
+def _fxsum(parts, mode):
+    """The total of `parts` through one fixed-point statistics entry (stts_test_fxsum: each part added by its own
+    lane with integer atomics, then read back once)."""
+    from stts2_mi355x import engine as E
+    L = E.lib()
+    L.stts_test_fxsum.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p]
+    L.stts_test_fxsum.restype = ctypes.c_int
+    t = torch.as_tensor(parts, dtype=torch.float32 if mode == 0 else torch.float64).cuda()
+    entry = torch.zeros(4, dtype=torch.float64, device="cuda")
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    rc = L.stts_test_fxsum(mode, t.data_ptr(), t.numel(), entry.data_ptr(), out.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    return float(out.item())
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fixed_point_statistics_range(mode):
+    """The InstanceNorm statistics entries (csrc/common.h fx_add / fx_get): an in-range total is exact to the entry's
+    2^-48 resolution; a part or a total beyond the 2^45 range reads back as NaN (the reference's InstanceNorm then
+    gives NaN / inf as well), never as a silently wrapped, wrong mean or variance."""
+    rng = np.random.default_rng(3)
+    p = rng.standard_normal(50_000).astype(np.float32) * 100.0
+    tot = _fxsum(p, mode)
+    assert abs(tot - float(p.astype(np.float64).sum())) < 1e-6
+    # every part in range (2^40 each), the total 64 x 2^40 = 2^46 beyond it: NaN, not a wrapped value
+    assert np.isnan(_fxsum(np.full(64, 2.0 ** 40), mode))
+    # 2^40 x 1,024 = 2^50: past the int64 word's 2^47 wrap point, far from a multiple of 2^48: NaN too
+    assert np.isnan(_fxsum(np.full(1024, 2.0 ** 40) * np.where(np.arange(1024) % 5 == 0, 1.0, 0.75), mode))
+    # a single out-of-range part, and a NaN part, poison the entry
+    assert np.isnan(_fxsum(np.array([1.0, 2.0 ** 46, -2.0 ** 46]), mode))
+    assert np.isnan(_fxsum(np.array([1.0, np.nan, 3.0]), mode))
+    # negative totals near the edge of the range are still read back
+    q = np.full(16, -(2.0 ** 40))
+    assert _fxsum(q, mode) == -(2.0 ** 44)

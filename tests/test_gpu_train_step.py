@@ -840,3 +840,50 @@ def test_trainstep_graph_matches_eager(dtype):
     graph.opt["decoder"].sync_steps()
     st = graph.opt["decoder"].state[next(mods[1][0].parameters())]["step"]
     assert float(st) == 3.0
+
+
+def test_capturable_adamw_checkpoint_roundtrip():
+    """optim.AdamW(capturable=True) keeps the step count on the device: state_dict() folds it in (a checkpoint
+    carries the real step, not the count at the first step), and load_state_dict() re-seeds the device count in
+    place (a resumed optimizer's bias correction continues from the loaded step), also under TrainStep(graph=True),
+    whose recorded graph keeps replaying with the re-seeded count.  Guards: a changed learning rate, another input
+    shape and a train-mode decoder are refused by the graph path."""
+    from stts2_mi355x.trainstep import TrainStep
+    B, T = 2, 16
+    asr, f0, n, s, wav, _ = _train_inputs(B, T)
+    dec, _ = make_decoder("hifigan")
+    mpd, msd = _discs()
+    dec, mpd, msd = dec.cuda().eval(), mpd.cuda().train(), msd.cuda().train()
+    ins = [t.cuda() for t in (asr, f0, n, s)]
+    step = TrainStep(dec, mpd, msd, dtype="bf16", graph=True)
+    for i in range(3):
+        step(*ins, wav.cuda(), seed=10 + i)
+    opt = step.opt["decoder"]
+    sd = opt.state_dict()  # (no explicit sync_steps(): state_dict does it)
+    steps = {float(v["step"]) for v in sd["state"].values()}
+    assert steps == {3.0}, steps
+    # resume: load a state saved at step 3 into an optimizer that has run 5 steps
+    step(*ins, wav.cuda(), seed=20)
+    step(*ins, wav.cuda(), seed=21)
+    opt.load_state_dict(sd)
+    dev = opt._dev_state[0]
+    assert float(dev[0].item()) == 3.0
+    step(*ins, wav.cuda(), seed=22)  # the recorded graph replays with the re-seeded count
+    assert {float(v["step"]) for v in opt.state_dict()["state"].values()} == {4.0}
+    # guards of the recorded step
+    with pytest.raises(ValueError):
+        step(ins[0][:, :, :8].contiguous(), ins[1][:, :16].contiguous(), ins[2][:, :16].contiguous(), ins[3],
+             wav.cuda()[:, :, :4800].contiguous(), seed=1)
+    opt.param_groups[0]["lr"] *= 2
+    with pytest.raises(ValueError):
+        step(*ins, wav.cuda(), seed=1)
+    opt.param_groups[0]["lr"] /= 2
+    dec.train()
+    with pytest.raises(ValueError):
+        step(*ins, wav.cuda(), seed=1)
+    dec.eval()
+    # the moments the recorded graph updates are the optimizer's state tensors after the load
+    p0 = next(dec.parameters())
+    before = opt.state[p0]["exp_avg"].clone()
+    step(*ins, wav.cuda(), seed=23)
+    assert not torch.equal(before, opt.state[p0]["exp_avg"])
