@@ -495,6 +495,10 @@ int stts_abi_version(void);
  *                     too (instead of resconv); bit 4 = on 4-wave blocks, two per CU (else 8-wave); bit 8 = the accuracy mode's C = 32
  *                     convs as well (64-frame slices; slower than the split resblock engine, A/B); default 5; 0 = off. */
 #define STTS_OPT_BIG64 27
+/*   STTS_OPT_BIG3  bit mask: 1 = the bf16 C = 128 / 256 resblock convs, 2 = the front-end k3 convs, 4 = ups[0] / ups[1] run
+ *                     on the v3 engine (64-channel x 128-frame wave tiles, block-shared weight chunks; bitwise equal to
+ *                     bigconv2); 8 = its C = 128 convs on 8-wave blocks (else two 4-wave blocks per CU); 0 = off. */
+#define STTS_OPT_BIG3 28
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

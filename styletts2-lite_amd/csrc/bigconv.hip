@@ -546,7 +546,8 @@ bool st_bigconv_eligible(const ConvParams& p, int dtype) {
 }
 
 int st_bigconv(const ConvParams& p, hipStream_t stream) {
-  if (st_bigconv2_eligible(p)) return st_bigconv2(p, stream);  // bigconv2.hip (default)
+  if ((g_opt_big3 & 1) && (p.res ? p.dil == 1 : !p.accb)) return st_bigconv3(p, stream);  // bigconv3.hip
+  if (st_bigconv2_eligible(p)) return st_bigconv2(p, stream);  // bigconv2.hip
   if (p.Cout == 128) return launch_bc_k<128>(p, stream);
   if (p.Cout == 256) return launch_bc_k<256>(p, stream);
   return ST_EINVAL;

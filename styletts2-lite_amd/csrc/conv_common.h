@@ -117,4 +117,10 @@ __device__ __forceinline__ void glds16(Rsrc r, void* lds, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
 }
 
+// the same with a wave-uniform byte offset in the instruction's SGPR offset (soff), so the per-lane VGPR part can be
+// shared by every piece a loop issues
+__device__ __forceinline__ void glds16s(Rsrc r, void* lds, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, (int)soff, 0, 0);
+}
+
 }  // namespace

@@ -128,6 +128,12 @@ extern int g_opt_cout1;  // STTS_OPT_COUT1 (convbwd.hip)
 extern int g_opt_plainrc;  // resconv.hip: prologue-free C = 32 / 64 convs (training step) on resconv (STTS_OPT_PLAINRC)  // convbwd.hip: bf16 weight gradient of stride-1 convs on k_wgrad_bf16w (STTS_OPT_WGRAD)
 bool st_ups_eligible(const ConvParams& p, int dtype);
 int st_bigconv2_ups(const ConvParams& p, hipStream_t stream);
+// engine v3 of the same work (bigconv3.hip: 64-channel x 128-frame wave tiles, block-shared weight chunks), routed
+// by STTS_OPT_BIG3 bits from st_bigconv / st_bigconv2_front / st_bigconv2_ups
+int st_bigconv3(const ConvParams& p, hipStream_t stream);
+int st_bigconv3_front(const ConvParams& p, hipStream_t stream);
+int st_bigconv3_ups(const ConvParams& p, hipStream_t stream);
+extern int g_opt_big3;
 extern int g_opt_front;
 // HiFi-GAN output head (head.hip): Snake -> conv_post (C -> 1, 7 taps) -> tanh as one streaming pass;
 // st_conv1d routes eligible launches to it while g_opt_head != 0

@@ -50,9 +50,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     os.makedirs(OBJ, exist_ok=True)
     hipcc = _hipcc()
-    jobs = []
+    jobs, objs = [], []
+    # (incremental: an object newer than its source and every header is reused)
+    hdr_t = max([os.path.getmtime(h) for h in glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))]
+                + [os.path.getmtime(__file__)])
     for src in sources():
         obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), hdr_t):
+            continue
         cmd = [hipcc, *FLAGS, "-x", "hip", "-c", src, "-o", obj]
         jobs.append((src, obj, cmd))
 
@@ -61,7 +67,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         return src, r
 
-    n = min(len(jobs), int(os.environ.get("MAX_JOBS", "8")))
+    n = min(max(len(jobs), 1), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max_workers=max(1, n)) as ex:
         for src, r in ex.map(run, jobs):
             if r.returncode != 0:
@@ -69,7 +75,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             if verbose and (r.stdout or r.stderr):
                 print(r.stdout, r.stderr, file=sys.stderr)
     tmp = LIB + ".tmp"
-    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + [o for _, o, _ in jobs]
+    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

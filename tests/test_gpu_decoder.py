@@ -351,3 +351,34 @@ def test_inplace_weight_update_repacks():
         c = d(asr, f0, n, s, noise=nz).cpu()
     assert (b - a).abs().max() > 1e-3
     assert (a - c).abs().max() < 1e-5  # ((x + 0.25) - 0.25 is not x in every bit: the bias itself moved)
+
+
+@pytest.mark.parametrize("B,T,cap", [(2, 40, 0), (4, 64, 0), (3, 48, 3), (32, 40, 0)])
+@pytest.mark.parametrize("bits", [7, 15])
+def test_bigconv3_decoder_ab(B, T, cap, bits):
+    """bf16 HiFi-GAN decode with the C = 128 / 256 resblock convs, the front-end k3 convs and ups[0] / ups[1] on the v3
+    engine (STTS_OPT_BIG3: 64-channel x 128-frame wave tiles, block-shared weight chunks; bit 8: C = 128 on 8-wave
+    blocks) against bigconv2 (and v1 for C = 128 k3; STTS_OPT_BIGCONV 4 = bigconv2 for every shape).  Each conv's
+    accumulation order is bigconv2's; the InstanceNorm partials are grouped per tile instead of per workgroup, so the
+    decodes agree to bf16 model noise; repeat decodes and a grid capped at 3 workgroups (tiles crossing utterances,
+    coefficient switches) are bitwise stable."""
+    from stts2_mi355x import engine as E
+    try:
+        E.set_option(E.OPT_GRID_CAP, cap)
+        E.set_option(E.OPT_BIGCONV, 4)
+        ref = run("hifigan", B, T, "bf16")
+        E.set_option(E.OPT_BIG3, bits)
+        E.profile_enable(True)
+        out = run("hifigan", B, T, "bf16")
+        kernels = {r["kernel"] for r in E.profile_launches()}
+        E.profile_enable(False)
+        out2 = run("hifigan", B, T, "bf16")
+    finally:
+        E.profile_enable(False)
+        E.reset_options()
+    corr = np.corrcoef(out.ravel(), ref.ravel())[0, 1]
+    err = np.abs(out - ref).max()
+    print(f"bigconv3 A/B bits={bits} B={B} T={T} cap={cap}: max-abs {err:.3e} corr {corr:.7f} ({sorted(kernels)})")
+    assert corr > 0.9995 and err < 5e-2
+    assert np.array_equal(out, out2)
+
