@@ -499,6 +499,11 @@ int stts_abi_version(void);
  *                     on the v3 engine (64-channel x 128-frame wave tiles, block-shared weight chunks; bitwise equal to
  *                     bigconv2); 8 = its C = 128 convs on 8-wave blocks (else two 4-wave blocks per CU); 0 = off. */
 #define STTS_OPT_BIG3 28
+/*   STTS_OPT_SEGPART 1 (default) = batches of 32 k utterances split every persistent conv launch into utterance-relative
+ *                     tile ranges (kernels.h tile_range), so each workgroup's fp32 partial statistics, and with them every
+ *                     output bit, do not depend on the batch size: an N-rank job (256 / N utterances a rank) decodes
+ *                     the same bits for every N; 0 = one even range per workgroup. */
+#define STTS_OPT_SEGPART 29
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

@@ -93,9 +93,13 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   const int wn = wid % F::WAVES_N, wm = wid / F::WAVES_N;
   const int ntm = (p.Lq + BM - 1) / BM;
   const long long total = (long long)ntm * p.B;
-  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
-  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
-  if (tbeg >= tend) return;  // uniform over the block
+  // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments)
+  const int nv = tile_nv(p, p.B);
+  for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
+  long long tb_, te_;
+  tile_range(p, vb, nv, total, ntm, tb_, te_);
+  const int tbeg = (int)tb_, tend = (int)te_;
+  if (tbeg >= tend) continue;  // uniform over the block
   const int nsteps = (tend - tbeg) * NS;
 
   for (int i = tid; i < C; i += NT) bias_s[i] = p.bias ? p.bias[i] : 0.f;
@@ -480,6 +484,8 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   } else if constexpr (!ACC) {
     if (p.stats) flush_lds(cur_b);
   }
+  __syncthreads();  // (the next range re-stages the LDS)
+  }  // tile ranges
 }
 
 int g_num_cu_bc = 0;
@@ -499,10 +505,12 @@ int launch_bc(const ConvParams& p, hipStream_t stream) {
     ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_bc, hipDeviceAttributeMultiprocessorCount, dev));
   }
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
+  ConvParams q = p;
+  q.seg = st_seg_choice(p.B, 1, g_num_cu_bc);
   long long grid = g_num_cu_bc;
-  if (grid > tiles) grid = tiles;
+  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
 

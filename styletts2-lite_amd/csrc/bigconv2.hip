@@ -123,9 +123,13 @@ __global__ void __launch_bounds__(64 * NW, NW == 12 ? 3 : 2) k_bigconv2(const Co
   // tile t -> utterance t / (NCH ntm), output-channel part (t / ntm) % NCH, frame tile t % ntm
   const long long total = (long long)ntm * NCH * p.B;
   const int upb = ntm * NCH;  // tiles per utterance
-  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
-  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
-  if (tbeg >= tend) return;  // uniform over the block
+  // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments)
+  const int nv = tile_nv(p, p.B);
+  for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
+  long long tb_, te_;
+  tile_range(p, vb, nv, total, upb, tb_, te_);
+  const int tbeg = (int)tb_, tend = (int)te_;
+  if (tbeg >= tend) continue;  // uniform over the block
   const int NGG = (tend - tbeg) * NG;  // groups this block walks
   const bool want_stats = !ACC && p.stats != nullptr;
   // STTS_OPT_DEBUG phase skipping (timing attribution only; outputs are wrong while set):
@@ -806,6 +810,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 12 ? 3 : 2) k_bigconv2(const Co
       for (int k = 0; k < 10; ++k) atomicAdd(p.stamps + k, st_acc[k]);
     if (lane == 0 && wu == 0) atomicAdd(p.stamps + 15, 1ull);
   }
+  }  // tile ranges
 }
 
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
@@ -825,10 +830,11 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
     ST_CHECK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   }
   const long long tiles = (long long)((p.Lq + G::TM - 1) / G::TM) * G::NCH * p.B;
-  long long grid = (long long)ncu * G::BPC;
-  if (grid > tiles) grid = tiles;
-  if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
   ConvParams q = p;
+  q.seg = st_seg_choice(p.B, 1, ncu * G::BPC);
+  long long grid = (long long)ncu * G::BPC;
+  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
+  if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
   q.skew = g_opt_skew;
   q.exp = g_opt_exp;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), G::LDS, stream, q);

@@ -117,6 +117,8 @@ __global__ void __launch_bounds__(64 * NW, 2) k_bigconv3(const ConvParams p) {
     // (lane part in one VGPR for every piece, the uniform part through the SGPR offset)
     const unsigned soff = (unsigned)((((size_t)gi * K + t) * C + (size_t)ch * NCO) * 64) + (unsigned)(piece * 1024);
     glds16s(rw, dst, wlane, __builtin_amdgcn_readfirstlane(soff));
+    // (STTS_OPT_EXP bit 131072, a cost probe: every piece DMA'd twice, the same bytes to the same place)
+    if (p.exp & 131072) glds16s(rw, dst, wlane, __builtin_amdgcn_readfirstlane(soff));
   };
 
   // ---------------- window: group gg -> raw rows [gr0, gr0 + WROWS) of its 32 channels, buffer gg & 1.

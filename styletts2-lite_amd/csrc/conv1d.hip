@@ -127,9 +127,14 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
   const long long total = (long long)ntn * ntm * p.B;
   // XCD-aware: the tile ranges of consecutive logical blocks (same column tile, same weights)
   // land on one XCD, so each XCD's L2 holds the weights of ~1/8 of the column tiles
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tbeg = (int)(total * bid / gridDim.x);
-  const int tend = (int)(total * (bid + 1) / gridDim.x);
+  // tile ranges (kernels.h tile_range: one per workgroup, or segments of each (column tile, utterance) unit at
+  // unit-relative bounds); the first is the XCD-remapped one
+  const int nv = tile_nv(p, (long long)ntn * p.B);
+  for (int vb = xcd_remap(blockIdx.x, gridDim.x); vb < nv; vb += gridDim.x) {
+  long long tb_, te_;
+  tile_range(p, vb, nv, total, ntm, tb_, te_);
+  const int tbeg = (int)tb_, tend = (int)te_;
+  if (tbeg >= tend) continue;  // uniform over the block
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
@@ -774,6 +779,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
     }
   }
   if (cur_nt >= 0 && p.stats) flush_stats(cur_nt, cur_b);
+  __syncthreads();  // (the next range re-stages the LDS)
+  }  // tile ranges
 }
 
 int g_num_cu = 0;
@@ -830,10 +837,13 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
   const long long tiles = ntn * ntm * p.B;
   if (tiles <= 0) return ST_OK;
   if (tiles > 0x7fffffffLL) return ST_EINVAL;
+  ConvParams q = p;
+  q.seg = st_seg_choice(p.B, (int)ntn, g_num_cu * per_cu);
+  const long long nvb = q.seg ? ntn * p.B * q.seg : tiles;
   long long grid = (long long)g_num_cu * per_cu;
-  if (grid > tiles) grid = tiles;
+  if (grid > nvb) grid = nvb;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C::NT), lds, stream, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(C::NT), lds, stream, q);
   return (int)hipGetLastError();
 }
 
@@ -882,6 +892,13 @@ int g_opt_resconv = 1;
 int g_opt_small_tiles = 1;
 int g_opt_resfused = 0;
 int g_opt_grid_cap = 0;
+int g_opt_segpart = 1;
+
+int st_seg_choice(int B, int upu, int gmax) {
+  if (!g_opt_segpart || B < 32 || B % 32 || upu <= 0) return 0;
+  const int seg = gmax / (32 * upu);
+  return seg >= 1 ? seg : 0;
+}
 int g_opt_debug = 0;
 int g_opt_head = 1;
 unsigned long long* g_dbg_stamps = nullptr;  // stts_set_debug_buffer

@@ -65,7 +65,35 @@ struct ConvParams {
   // (b mod tx_H) + dh - 1 falls outside [0, tx_H): the K dimension is dh-major (k = dh C + c), and the
   // time-expanded image x3[..][dh C + c] = x[b + dh - 1][..][c] is never materialised
   int tx_H;
+  // segmented persistent partition (set by the launchers from st_seg_choice): seg > 0 splits every unit
+  // (an utterance, or one column tile of an utterance) into seg tile ranges at unit-relative bounds, one virtual
+  // workgroup each; 0 = the B x tiles split evenly over the grid
+  int seg;
 };
+
+// Virtual workgroups of a persistent launch and the tile range [tb, te) of virtual workgroup v < nv.  Segmented: v ->
+// (unit v / seg, segment v % seg), tiles [u upt + s upt / seg, u upt + (s + 1) upt / seg) with upt tiles per unit: a
+// range never spans two units and its bounds are unit-relative, so the fp32 partial statistics a range accumulates
+// (and with them every output bit) do not depend on the batch size, the rank count or the CU count.
+__device__ __forceinline__ int tile_nv(const ConvParams& p, long long nunits) {
+  return p.seg > 0 ? (int)(nunits * p.seg) : (int)gridDim.x;
+}
+__device__ __forceinline__ void tile_range(const ConvParams& p, int v, int nv, long long total, long long upt,
+                                           long long& tb, long long& te) {
+  if (p.seg > 0) {
+    const long long u = v / p.seg, s = v % p.seg;
+    tb = u * upt + upt * s / p.seg;
+    te = u * upt + upt * (s + 1) / p.seg;
+  } else {
+    tb = total * v / nv;
+    te = total * (v + 1) / nv;
+  }
+}
+// host: segments per unit for a launch of B utterances with `upu` units each on a grid of up to gmax workgroups.
+// Segmented when B is a multiple of 32 (every config-4 shard, 256 / W utterances): seg = gmax / (32 upu), so B = 32 k
+// gives every workgroup k ranges of equal size; 0 (the even split) otherwise, or with STTS_OPT_SEGPART 0
+int st_seg_choice(int B, int upu, int gmax);
+extern int g_opt_segpart;
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);
 // slot base of workgroup `g` (see ConvParams::stats_slots)

@@ -1080,10 +1080,11 @@ int st_gap_linear(const void* z, int B, int rows, int Wv, int C, const float* w,
 int st_noise_conv(const float* har, int B, int L, const float* w, const float* bias, int C, int K, int S, int P,
                   int Lout, void* y, double* stats, int dtype, hipStream_t s) {
   if (C % 8 || 256 % (C / 8) || C > 256) return ST_EINVAL;
-  // frames per block: about 2048 blocks over the batch (8 per CU), a multiple of the frames one
-  // block covers per pass (256 / (C/8)); statistics cost one atomic pair per (block, channel)
+  // frames per block: about 2048 blocks over a 32-utterance batch (8 per CU), a multiple of the frames one
+  // block covers per pass (256 / (C/8)); statistics cost one atomic pair per (block, channel).  From Lout alone,
+  // not B, so each block's fp32 partial covers the same frames at every batch size (rank-count invariance, §8(e))
   const int fstep = 256 / (C / 8);
-  long long fpb = ((long long)Lout * B + 2047) / 2048;
+  long long fpb = ((long long)Lout * 32 + 2047) / 2048;
   fpb = (fpb + fstep - 1) / fstep * fstep;
   if (fpb < fstep) fpb = fstep;
   if (fpb > 8192) fpb = 8192;

@@ -43,7 +43,8 @@ __global__ void __launch_bounds__(NT, 2) k_pwgemm(const ConvParams p, int ntm, i
   // leave as one atomic pair per channel (per-tile atomics all hitting the same few addresses
   // serialised: profiles/r02_layers_bf16_b32_pw1.txt)
   const long long total = (long long)ntm * ntn * p.B;
-  const long long tbeg = total * blockIdx.x / gridDim.x, tend = total * (blockIdx.x + 1) / gridDim.x;
+  // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments)
+  const int nv = tile_nv(p, p.B);
   float st_s[2][16], st_q[2][16];
 #pragma unroll
   for (int ni = 0; ni < 2; ++ni)
@@ -64,6 +65,9 @@ __global__ void __launch_bounds__(NT, 2) k_pwgemm(const ConvParams p, int ntm, i
       }
     }
   };
+  for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
+  long long tbeg, tend;
+  tile_range(p, vb, nv, total, (long long)ntm * ntn, tbeg, tend);
   for (long long t = tbeg; t < tend; ++t) {
     const int tm = (int)(t % ntm), tn = (int)((t / ntm) % ntn), b = (int)(t / ((long long)ntm * ntn));
     const int q0 = tm * BM, n0 = tn * BN;
@@ -226,6 +230,8 @@ __global__ void __launch_bounds__(NT, 2) k_pwgemm(const ConvParams p, int ntm, i
     }
   }
   if (cur_key >= 0 && p.stats) flush(cur_b, (cur_key % ntn) * BN);
+  cur_key = -1;  // (flushed at every range end: a range's partial sums never join another range's)
+  }  // tile ranges
 }
 
 
@@ -451,8 +457,10 @@ int st_pw(const ConvParams& p, hipStream_t stream) {
     ST_CHECK_HIP(hipGetDevice(&dev));
     ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_pw, hipDeviceAttributeMultiprocessorCount, dev));
   }
+  ConvParams q = p;
+  q.seg = st_seg_choice(p.B, 1, g_num_cu_pw * 2);
   long long blocks = (long long)g_num_cu_pw * 2;  // 220-238 VGPRs: two 4-wave blocks per CU
-  if (blocks > tiles) blocks = tiles;
+  if (blocks > (q.seg ? (long long)p.B * q.seg : tiles)) blocks = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && blocks > g_opt_grid_cap) blocks = g_opt_grid_cap;
   const size_t lds = p.pro.mode ? (size_t)p.nchunks * 32 * 4 * sizeof(float) : 0;
   static bool attr = false;
@@ -463,9 +471,9 @@ int st_pw(const ConvParams& p, hipStream_t stream) {
   }
   if (lds > 96 * 1024) return ST_EINVAL;
   if (p.KS == 1)
-    hipLaunchKernelGGL(k_pwgemm<1>, dim3((unsigned)blocks), dim3(NT), lds, stream, p, ntm, ntn);
+    hipLaunchKernelGGL(k_pwgemm<1>, dim3((unsigned)blocks), dim3(NT), lds, stream, q, ntm, ntn);
   else
-    hipLaunchKernelGGL(k_pwgemm<2>, dim3((unsigned)blocks), dim3(NT), lds, stream, p, ntm, ntn);
+    hipLaunchKernelGGL(k_pwgemm<2>, dim3((unsigned)blocks), dim3(NT), lds, stream, q, ntm, ntn);
   return (int)hipGetLastError();
 }
 

@@ -87,9 +87,11 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   const int wn = wid % WAVES_N, wm = wid / WAVES_N;
   const int ntm = (p.Lq + BM - 1) / BM;
   const long long total = (long long)ntm * p.B;
-  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
-  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
-  if (tbeg >= tend) return;  // uniform over the block
+  // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments); the lambdas
+  // below read the current range [tbeg, tend) by reference
+  const int nv = tile_nv(p, p.B);
+  if ((int)blockIdx.x >= nv) return;  // uniform over the block
+  int tbeg = 0, tend = 0;
 
   // ---- layer constants -> LDS, once per block
   {
@@ -374,6 +376,14 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     mark(6);
   };
 
+  for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
+  {
+    long long tb_, te_;
+    tile_range(p, vb, nv, total, ntm, tb_, te_);
+    tbeg = (int)tb_;
+    tend = (int)te_;
+  }
+  if (tbeg >= tend) continue;  // uniform over the block
   uint4 preA[MAXU], preB[MAXU];
   EpiRegs eA, eB;
   if constexpr (RPF) issue_epi(tbeg, eA);
@@ -394,6 +404,8 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     }
   }
   if (p.stats) flush(cur_b);
+  cur_b = -1;  // (the range's statistics are out: the next range re-stages its coefficients, flushes nothing twice)
+  }  // tile ranges
   if (stamp) {
     sacc[7] = __builtin_amdgcn_s_memtime() - t_start;
     if (lane == 0)
@@ -423,10 +435,12 @@ int launch_rc(const ConvParams& p, hipStream_t stream) {
   int per_cu = occupancy_cached((const void*)kern, G::NT, G::LDS);
   if (per_cu < 1) per_cu = 1;
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
+  ConvParams q = p;
+  q.seg = st_seg_choice(p.B, 1, g_num_cu_rc * per_cu);
   long long grid = (long long)g_num_cu_rc * per_cu;
-  if (grid > tiles) grid = tiles;
+  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
 
@@ -475,11 +489,10 @@ __global__ void __launch_bounds__(512, 1) k_resconv_pp(const ConvParams p) {
 
   const int ntm = (p.Lq + BM - 1) / BM;
   const long long total = (long long)ntm * p.B;
-  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
-  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
-  if (tbeg >= tend) return;  // uniform over the block
-  const int n0 = (tend - tbeg + 1) / 2, n1 = (tend - tbeg) / 2;
-  const int ng = grp ? n1 : n0;  // this group's tiles: tbeg + grp + 2 j
+  // tile ranges (kernels.h tile_range); the lambdas below read the current range by reference
+  const int nv = tile_nv(p, p.B);
+  if ((int)blockIdx.x >= nv) return;  // uniform over the block
+  int tbeg = 0, tend = 0, n0 = 0, n1 = 0, ng = 0;  // ng: this group's tiles, tbeg + grp + 2 j
   auto utt = [&](int j) { return (tbeg + grp + 2 * j) / ntm; };
 
   {  // weights (copied as packed) and bias, once per block
@@ -695,6 +708,17 @@ __global__ void __launch_bounds__(512, 1) k_resconv_pp(const ConvParams p) {
     }
   };
 
+  for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
+  {
+    long long tb_, te_;
+    tile_range(p, vb, nv, total, ntm, tb_, te_);
+    tbeg = (int)tb_;
+    tend = (int)te_;
+  }
+  if (tbeg >= tend) continue;  // uniform over the block
+  n0 = (tend - tbeg + 1) / 2;
+  n1 = (tend - tbeg) / 2;
+  ng = grp ? n1 : n0;
   // prologue: coefficients of each group's first tile, its window loads; group 0 transforms tile 0
   int coef_b = -1;
   if (ng > 0) {
@@ -731,6 +755,9 @@ __global__ void __launch_bounds__(512, 1) k_resconv_pp(const ConvParams p) {
     __syncthreads();
   }
   if (p.stats && stat_b >= 0) flush(stat_b);
+  stat_b = -1;
+  __syncthreads();  // (the next range re-stages coefficients and windows)
+  }  // tile ranges
 }
 
 int g_num_cu_pp = 0;
@@ -750,10 +777,12 @@ int launch_pp(const ConvParams& p, hipStream_t stream) {
     ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_pp, hipDeviceAttributeMultiprocessorCount, dev));
   }
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
+  ConvParams q = p;
+  q.seg = st_seg_choice(p.B, 1, g_num_cu_pp);
   long long grid = g_num_cu_pp;
-  if (grid > tiles) grid = tiles;
+  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
 

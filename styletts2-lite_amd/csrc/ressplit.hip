@@ -97,9 +97,11 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
   const int wn = wid % WAVES_N, wm = wid / WAVES_N;
   const int ntm = (p.Lq + BM - 1) / BM;
   const long long total = (long long)ntm * p.B;
-  const int tbeg = (int)(total * blockIdx.x / gridDim.x);
-  const int tend = (int)(total * (blockIdx.x + 1) / gridDim.x);
-  if (tbeg >= tend) return;  // uniform over the block
+  // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments); the lambdas
+  // below read the current range by reference
+  const int nv = tile_nv(p, p.B);
+  if ((int)blockIdx.x >= nv) return;  // uniform over the block
+  int tbeg = 0, tend = 0;
 
   {  // this pass's weights (hi and lo), in logical k order, and the bias
     const size_t copy = (size_t)NCHT * K * NOUT * 32;  // elements of one packed copy
@@ -331,6 +333,14 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
     }
   };
 
+  for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
+  {
+    long long tb_, te_;
+    tile_range(p, vb, nv, total, ntm, tb_, te_);
+    tbeg = (int)tb_;
+    tend = (int)te_;
+  }
+  if (tbeg >= tend) continue;  // uniform over the block
   U8 preA[MAXU], preB[MAXU];
   issue(tbeg, preA);
   if (tbeg + 1 < tend) issue(tbeg + 1, preB);
@@ -339,6 +349,9 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
     if (t + 1 < tend) step(t + 1, preB);
   }
   if (p.stats) flush(cur_b);
+  cur_b = -1;  // (flushed: the next range re-stages its coefficients)
+  __syncthreads();
+  }  // tile ranges
 }
 
 int g_num_cu_rs = 0;
@@ -360,10 +373,12 @@ int launch_rs_pf(const ConvParams& p, hipStream_t stream) {
   int per_cu = occupancy_cached((const void*)kern, G::NT, G::LDS);
   if (per_cu < 1) per_cu = 1;
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
+  ConvParams q = p;
+  q.seg = st_seg_choice(p.B, 1, g_num_cu_rs * per_cu);
   long long grid = (long long)g_num_cu_rs * per_cu;
-  if (grid > tiles) grid = tiles;
+  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
 
