@@ -127,12 +127,12 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
   const long long total = (long long)ntn * ntm * p.B;
   // XCD-aware: the tile ranges of consecutive logical blocks (same column tile, same weights)
   // land on one XCD, so each XCD's L2 holds the weights of ~1/8 of the column tiles
-  // tile ranges (kernels.h tile_range: one per workgroup, or segments of each (column tile, utterance) unit at
-  // unit-relative bounds); the first is the XCD-remapped one
-  const int nv = tile_nv(p, (long long)ntn * p.B);
+  // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments); the first is
+  // the XCD-remapped one
+  const int nv = tile_nv(p, p.B);
   for (int vb = xcd_remap(blockIdx.x, gridDim.x); vb < nv; vb += gridDim.x) {
   long long tb_, te_;
-  tile_range(p, vb, nv, total, ntm, tb_, te_);
+  tile_range(p, vb, nv, total, (long long)ntn * ntm, tb_, te_);
   const int tbeg = (int)tb_, tend = (int)te_;
   if (tbeg >= tend) continue;  // uniform over the block
 
@@ -146,9 +146,11 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
   // range stays in one column tile.  (Column-tile-fastest orders, tried for the streamed-weight
   // upsamplers to re-read each input window from L2, measured 10-30 % slower: every tile then
   // re-stages its window's prologue and flushes statistics.)
+  // (segmented ranges, p.seg > 0: utterance-major instead, (utterance, column tile, row tile), so that a range lies
+  // inside one utterance whatever the column-tile count)
   auto t_mt = [&](int t) { return t % ntm; };
-  auto t_b = [&](int t) { return (t / ntm) % p.B; };
-  auto t_nt = [&](int t) { return t / (ntm * p.B); };
+  auto t_b = [&](int t) { return p.seg > 0 ? t / (ntm * ntn) : (t / ntm) % p.B; };
+  auto t_nt = [&](int t) { return p.seg > 0 ? (t / ntm) % ntn : t / (ntm * p.B); };
   constexpr bool FAST_SIN = C::BF;
 
   // statistics partials: lane = column l32 of tile ni, summed over the frames of its half (hi)
@@ -838,8 +840,8 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
   if (tiles <= 0) return ST_OK;
   if (tiles > 0x7fffffffLL) return ST_EINVAL;
   ConvParams q = p;
-  q.seg = st_seg_choice(p.B, (int)ntn, g_num_cu * per_cu);
-  const long long nvb = q.seg ? ntn * p.B * q.seg : tiles;
+  q.seg = st_seg_choice(p.B, 1, g_num_cu * per_cu);
+  const long long nvb = q.seg ? (long long)p.B * q.seg : tiles;
   long long grid = (long long)g_num_cu * per_cu;
   if (grid > nvb) grid = nvb;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;

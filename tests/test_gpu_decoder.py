@@ -293,12 +293,12 @@ def test_config3_bf16_batch32_shipped_mode():
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32", "bf16x3"])
 def test_config4_rank_shard_bitwise(dtype):
-    """Config 4 (BASELINE configs[3]: 256 utterances sharded 8-way, 32 per rank) on one GPU: a B = 64 x 10 s
-    decode with device-RNG noise equals, bit for bit, the two B = 32 decodes that two ranks would run on its
-    halves (utt_offset 0 and 32).  So an N-rank job's audio does not depend on N while every rank's batch routes
-    every launch to the same engine (tiles are per utterance and the InstanceNorm sums are
-    order-free fixed-point integers, so which workgroup computes a tile, and how many statistics slots there
-    are, does not matter; what can change the bits is a small-batch engine such as split-K)."""
+    """Config 4 (BASELINE configs[3]: 256 utterances sharded 8-way, 32 per rank) on one GPU: a B = 64 x 10 s decode with
+    device-RNG noise equals, bit for bit, the two B = 32 decodes that two ranks would run on its halves (utt_offset 0 and
+    32).  What makes it hold: the noise is keyed by the global utterance id, the InstanceNorm totals are
+    order-free fixed-point sums, and for batches of 32 k utterances every persistent conv launch splits its tiles into
+    utterance-relative ranges (STTS_OPT_SEGPART, kernels.h tile_range), so each workgroup's fp32 partial statistics
+    cover the same frames whatever the batch size."""
     asr, f0, n, s, _ = decoder_case(64, 400)
     d = dec("hifigan")
 
@@ -316,6 +316,29 @@ def test_config4_rank_shard_bitwise(dtype):
     assert torch.isfinite(full).all()
     assert torch.equal(full[:32], lo), (full[:32] - lo).abs().max().item()
     assert torch.equal(full[32:], hi), (full[32:] - hi).abs().max().item()
+
+
+def test_config4_every_rank_count_bitwise():
+    """The whole config-4 job in the headline mode (bf16, B = 256 x 10 s, device-RNG noise) decodes the same bits on
+    1, 2, 4 and 8 ranks: the B = 256 decode equals every rank's shard decode (256 / W utterances at utt_offset
+    r 256 / W) for W = 2, 4, 8."""
+    asr, f0, n, s, _ = decoder_case(256, 400)
+    d = dec("hifigan")
+
+    def go(a, b):
+        with torch.no_grad():
+            out = d(asr[a:b].cuda(), f0[a:b].cuda(), n[a:b].cuda(), s[a:b].cuda(), noise=None, seed=99, utt_offset=a,
+                    dtype="bf16")
+        torch.cuda.synchronize()
+        return out.cpu()
+
+    full = go(0, 256)
+    assert torch.isfinite(full).all()
+    for W in (2, 4, 8):
+        per = 256 // W
+        for r in range(W):
+            part = go(r * per, (r + 1) * per)
+            assert torch.equal(full[r * per:(r + 1) * per], part), (W, r)
 
 
 def test_default_noise_follows_torch_rng():
