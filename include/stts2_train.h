@@ -206,6 +206,10 @@ int stts_dur_losses(const float* logits, long long ls_b, long long ls_t, int B, 
  * redrawn, not stored).  The draws are not torch's (no implementation reproduces those); the seed comes from
  * torch's default generator in the Python layer, so torch.manual_seed governs them. */
 int stts_dropout(const float* x, long long n, float p, unsigned long long seed, float* y, void* stream);
+/* The same with the keep mask given: y[i] = mask[i] != 0 ? x[i] / (1 - p) : 0 (backward: the same call on dy).  Used
+ * when a caller injects the masks (training.set_dropout_masks: train-mode parity against the reference run with the
+ * same masks, tests/golden/make_golden_train_text.py). */
+int stts_dropout_mask(const float* x, const float* mask, long long n, float p, float* y, void* stream);
 
 /* ---- StyleEncoder under train.py's G step (train.py:258, 324; models.py:125-150), frames images [B][H][W][C] */
 /* Row expansion for a k x k Conv2d with padding `pad` in H: xe[b][ho][w][c k + dh] = x[b][ho + dh - pad][w][c]

@@ -576,6 +576,12 @@ __global__ void __launch_bounds__(256) k_dropout(const float* __restrict__ x, lo
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
     y[i] = drop_keep(seed, i, p) ? x[i] * scale : 0.f;
 }
+// the same with the keep mask given (1 = kept): train-mode parity against the reference with injected masks
+__global__ void __launch_bounds__(256) k_dropout_mask(const float* __restrict__ x, const float* __restrict__ mask,
+                                                      long long n, float scale, float* __restrict__ y) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
+    y[i] = mask[i] != 0.f ? x[i] * scale : 0.f;
+}
 
 }  // namespace
 
@@ -920,6 +926,15 @@ extern "C" int stts_dropout(const float* x, long long n, float p, unsigned long 
   const long long g = (n + NT - 1) / NT;
   hipLaunchKernelGGL(k_dropout, dim3((unsigned)(g < 65536 ? g : 65536)), dim3(NT), 0, (hipStream_t)stream, x, n, p,
                      1.0f / (1.0f - p), seed, y);
+  return (int)hipGetLastError();
+}
+
+extern "C" int stts_dropout_mask(const float* x, const float* mask, long long n, float p, float* y, void* stream) {
+  if (!x || !mask || !y || n < 0 || !(p >= 0.f && p < 1.f)) return ST_EINVAL;
+  if (n == 0) return 0;
+  const long long g = (n + NT - 1) / NT;
+  hipLaunchKernelGGL(k_dropout_mask, dim3((unsigned)(g < 65536 ? g : 65536)), dim3(NT), 0, (hipStream_t)stream, x, mask,
+                     n, 1.0f / (1.0f - p), y);
   return (int)hipGetLastError();
 }
 

@@ -37,6 +37,15 @@ def hash_u01(name: str, n: int) -> np.ndarray:
     return (z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
 
 
+def dropout_mask(k: int, shape, p: float) -> np.ndarray:
+    """The k-th train-mode dropout call's keep mask (1.0 = kept) for a tensor of `shape` in the REFERENCE module's
+    layout: element i kept when hash_u01 >= p.  The train-mode text / duration fixtures inject these masks into the
+    reference's F.dropout (tests/golden/make_golden_train_text.py) and the HIP path through
+    training.set_dropout_masks, so both drop the same elements."""
+    n = int(np.prod(shape))
+    return (hash_u01(f"dropout:{k}:{tuple(int(v) for v in shape)}", n) >= p).astype(np.float32).reshape(shape)
+
+
 def uniform(name: str, shape, lo: float = -1.0, hi: float = 1.0) -> np.ndarray:
     n = int(np.prod(shape)) if len(shape) else 1
     u = hash_u01(name, n)

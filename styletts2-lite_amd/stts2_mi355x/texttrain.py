@@ -246,7 +246,7 @@ def text_encoder(te, tokens, input_lengths):
         y = conv1d_frames(h, w, conv.bias, 1, conv.padding)
         h = layer_norm_act(y, lnm.gamma, lnm.beta, lnm.eps, te.slope, ln)  # LayerNorm -> LeakyReLU -> mask
         if te.training:
-            h = dropout(h, float(drop.p))
+            h = dropout(h, float(drop.p), ref_transpose=True)  # (the reference's [B, C, T] layout)
     out = bilstm(te.lstm, h, ln)
     return out.transpose(1, 2)
 

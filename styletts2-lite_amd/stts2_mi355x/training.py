@@ -74,6 +74,7 @@ def _tl():
         "stts_bilstm_bwd_workspace_bytes": ([i, i, i, i], ll),
         "stts_bilstm_bwd": ([vp, i, i, i, vp, vp, i, vp, vp, vp, vp, vp, vp, ll, vp], i),
         "stts_dropout": ([vp, ll, f, ull, vp, vp], i),
+        "stts_dropout_mask": ([vp, vp, ll, f, vp, vp], i),
         "stts_rowexp_fwd": ([vp, i, i, i, i, i, i, vp, vp], i),
         "stts_rowexp_bwd": ([vp, i, i, i, i, i, i, vp, vp], i),
         "stts_dwconv2d_s2_fwd": ([vp, vp, vp, i, i, i, i, vp, vp], i),
@@ -1234,8 +1235,57 @@ class _DropoutFn(torch.autograd.Function):
         return dx, None
 
 
-def dropout(x, p):
-    return _DropoutFn.apply(x, float(p)) if p > 0 else x
+class _DropoutMaskFn(torch.autograd.Function):
+    """Train-mode dropout with an injected keep mask (stts_dropout_mask), forward and backward."""
+
+    @staticmethod
+    def forward(ctx, x, mask, p):
+        _require_device()
+        xc, mc = _c(x), _c(mask.to(x.device, torch.float32))
+        if mc.shape != xc.shape:
+            raise ValueError(f"dropout mask {tuple(mc.shape)} for a tensor {tuple(xc.shape)}")
+        y = torch.empty_like(xc)
+        check(_tl().stts_dropout_mask(_ptr(xc), _ptr(mc), xc.numel(), ctypes.c_float(p), _ptr(y), _stream()),
+              "stts_dropout_mask")
+        ctx.save_for_backward(mc)
+        ctx.p = p
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (mc,) = ctx.saved_tensors
+        dyc = _c(dy)
+        dx = torch.empty_like(dyc)
+        check(_tl().stts_dropout_mask(_ptr(dyc), _ptr(mc), dyc.numel(), ctypes.c_float(ctx.p), _ptr(dx), _stream()),
+              "stts_dropout_mask")
+        return dx, None, None
+
+
+_MASKS = {"fn": None, "k": 0}
+
+
+def set_dropout_masks(fn):
+    """Test hook: fn(k, shape, p) -> the keep mask (0 / 1, any device) of the k-th train-mode dropout call from now on,
+    in the REFERENCE module's layout of that tensor (a call site whose layout differs passes ref_transpose); None
+    goes back to the device counter draws.  The train-mode fixtures (tests/golden/make_golden_train_text.py) inject
+    the same masks into the reference's F.dropout, so both sides drop the same elements."""
+    _MASKS["fn"], _MASKS["k"] = fn, 0
+
+
+def dropout(x, p, ref_transpose=False):
+    """nn.Dropout(p) / F.dropout in train mode.  ref_transpose: the reference holds this tensor as x.transpose(1, 2)
+    (the TextEncoder's CNN, channels-first there), which is where an injected mask is laid out."""
+    if p <= 0:
+        return x
+    fn = _MASKS["fn"]
+    if fn is None:
+        return _DropoutFn.apply(x, float(p))
+    shape = tuple(x.transpose(1, 2).shape) if ref_transpose else tuple(x.shape)
+    m = torch.as_tensor(fn(_MASKS["k"], shape, float(p)), dtype=torch.float32, device=x.device)
+    _MASKS["k"] += 1
+    if ref_transpose:
+        m = m.transpose(1, 2)
+    return _DropoutMaskFn.apply(x, m.contiguous(), float(p))
 
 
 # ------------------------------------------------------------------ ProsodyPredictor.F0Ntrain (models.py:448-461)

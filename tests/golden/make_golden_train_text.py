@@ -7,9 +7,14 @@ Run in the survey container only (needs /root/reference; never on the GPU box):
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_train_text.py
 
 One ragged batch (helpers.DURATION_CASES[0]: T = 24 tokens, lengths 24 / 19 / 13) with formula weights, tokens,
-styles and alignments (stts2_mi355x/synth.py, tests/helpers.duration_inputs).  The modules are in eval mode (their
-dropout off: train.py trains them in train mode, whose dropout draws no implementation reproduces; the HIP dropout is
-tested on its own).  The chain is train.py's:
+styles and alignments (stts2_mi355x/synth.py, tests/helpers.duration_inputs), twice:
+  * train_text_T24_B3.npz: the modules in eval mode (dropout off);
+  * train_text_drop_T24_B3.npz: in TRAIN mode, as train.py runs them, with torch.nn.functional.dropout replaced for
+    the run by the injected masks synth.dropout_mask(k, shape, p) of the k-th call (y = x mask / (1 - p), torch's
+    scaling): the three nn.Dropout(0.2) of the TextEncoder's CNN blocks (models.py:250), the DurationEncoder's
+    F.dropout after each LSTM (:512) and the predictor's F.dropout(x, 0.5) before duration_proj (:442), in call
+    order.  The HIP path takes the same masks through training.set_dropout_masks (tests/test_gpu_train_text.py).
+The chain is train.py's:
     t_en = text_encoder(texts, input_lengths, text_mask)                       (train.py:217)
     asr = t_en @ attn                                                          (:220-223)
     d, p = predictor(t_en, s, input_lengths, attn, text_mask)                  (:230-233)
@@ -58,7 +63,21 @@ def dur_losses(d, d_gt, input_lengths):
     return loss_dur, loss_ce
 
 
-def text_case(T, lengths):
+class _InjectedDropout:
+    """torch.nn.functional.dropout replaced by synth.dropout_mask of the k-th call (train mode only)."""
+
+    def __init__(self):
+        self.k = 0
+
+    def __call__(self, x, p=0.5, training=True, inplace=False):
+        if not training or p == 0:
+            return x
+        m = torch.from_numpy(synth.dropout_mask(self.k, tuple(x.shape), p)).to(x.dtype)
+        self.k += 1
+        return x * m / (1 - p)
+
+
+def text_case(T, lengths, train=False):
     models = import_models()
     tok, ln, s, aln = duration_inputs(T, lengths)
     B, F_ = len(lengths), aln.shape[2]
@@ -69,15 +88,21 @@ def text_case(T, lengths):
     for tag, dt in (("f64", torch.float64), ("f32", torch.float32)):
         torch.manual_seed(0)
         torch.set_default_dtype(dt)  # (the reference's x_pad buffers are torch.zeros of the default dtype)
-        te = fill(models.TextEncoder(channels=512, kernel_size=5, depth=3, n_symbols=178), "te.").eval().to(dt)
+        te = fill(models.TextEncoder(channels=512, kernel_size=5, depth=3, n_symbols=178), "te.").train(train).to(dt)
         pp = fill(models.ProsodyPredictor(style_dim=128, d_hid=512, nlayers=3, max_dur=50, dropout=0.2),
-                  "pp.").eval().to(dt)
+                  "pp.").train(train).to(dt)
+        saved = F.dropout
+        F.dropout = _InjectedDropout()  # (eval mode: never called with training=True)
         m = pp.length_to_mask(ln_t)
         sd = torch.from_numpy(s).to(dt).clone().requires_grad_(True)
         attn = torch.from_numpy(aln).to(dt)
         t_en = te(tok_t, ln_t, m)
         asr = t_en @ attn
         d, p = pp(t_en, sd, ln_t, attn, m)
+        ncalls = F.dropout.k
+        F.dropout = saved
+        if train:
+            assert ncalls == 7, ncalls  # 3 CNN blocks + 3 DurationEncoder LSTMs + the duration projection
         d_gt = attn.sum(axis=-1).detach()
         loss_dur, loss_ce = dur_losses(d, d_gt, ln_t)
         loss = ((asr * probes["asr"].to(dt)).sum() + (d * probes["d"].to(dt)).sum() + (p * probes["p"].to(dt)).sum()
@@ -98,10 +123,12 @@ def text_case(T, lengths):
 def main():
     torch.set_num_threads(8)
     T, lengths = DURATION_CASES[0]
-    rec = text_case(T, lengths)
-    name = f"train_text_T{T}_B{len(lengths)}.npz"
-    np.savez_compressed(os.path.join(HERE, name), **rec)
-    print(name, len(rec["names"]), "parameter tensors;", "loss_dur", rec["f64.loss_dur"], "loss_ce", rec["f64.loss_ce"])
+    for train, tag in ((False, "train_text"), (True, "train_text_drop")):
+        rec = text_case(T, lengths, train)
+        name = f"{tag}_T{T}_B{len(lengths)}.npz"
+        np.savez_compressed(os.path.join(HERE, name), **rec)
+        print(name, len(rec["names"]), "parameter tensors;", "loss_dur", rec["f64.loss_dur"], "loss_ce",
+              rec["f64.loss_ce"])
 
 
 if __name__ == "__main__":

@@ -2,8 +2,9 @@
 323, 327) through the C-ABI: the drop-in TextEncoder / ProsodyPredictor.forward (DurationEncoder, packed BiLSTMs,
 AdaLayerNorm, duration_proj, en = d^T @ aln) and the duration losses, against the REFERENCE modules' own autograd
 (tests/golden/train_text_T24_B3.npz from tests/golden/make_golden_train_text.py: fp64 = the truth, fp32 = the
-reference as it runs), eval mode (dropout off), on a ragged batch (lengths 24 / 19 / 13); and each new backward
-kernel separately against torch's fp64 autograd on the CPU.
+reference as it runs), in eval mode (dropout off) and in train mode as train.py runs the modules (dropout on, with the
+same injected keep masks on both sides: train_text_drop_T24_B3.npz, training.set_dropout_masks), on a ragged batch
+(lengths 24 / 19 / 13); and each new backward kernel separately against torch's fp64 autograd on the CPU.
 
 Bound: every parameter / input gradient per tensor within max(2 x the fp32 reference's own error
 vs fp64, 1e-4 of the tensor's scale), and within 1e-4 of the module's largest |g| (normwise)."""
@@ -35,27 +36,40 @@ def _dur_losses_ref(d, d_gt, input_lengths):
     return loss_dur / d.size(0), loss_ce / d.size(0)
 
 
-def test_text_chain_grads_vs_reference():
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_text_chain_grads_vs_reference(mode):
     """t_en = text_encoder(tokens); asr = t_en @ attn; d, p = predictor(t_en, s, lengths, attn); the probe losses +
     loss_dur + loss_ce, backward: every TextEncoder and ProsodyPredictor parameter gradient and the style gradient vs
-    the reference's autograd."""
-    from stts2_mi355x import texttrain
+    the reference's autograd.  train: the modules in train mode with the fixture's injected dropout masks (the seven
+    dropout calls of the chain, in the reference's order and layouts)."""
+    from stts2_mi355x import texttrain, training
     from stts2_mi355x.prosody import matmul
-    fx = golden("train_text_T24_B3")
+    fx = golden("train_text_T24_B3" if mode == "eval" else "train_text_drop_T24_B3")
     T, lengths = DURATION_CASES[0]
     tok, ln, s, aln = duration_inputs(T, lengths)
     B, F_ = len(lengths), aln.shape[2]
     te, pp = make_duration_modules()
-    te, pp = te.cuda().eval(), pp.cuda().eval()
+    te, pp = te.cuda().train(mode == "train"), pp.cuda().train(mode == "train")
+    calls = []
+    if mode == "train":
+        def masks(k, shape, p):
+            calls.append((k, shape, p))
+            return torch.from_numpy(synth.dropout_mask(k, shape, p))
+        training.set_dropout_masks(masks)
     probes = {k: torch.from_numpy(synth.normal(f"tt:probe:{k}:{T}", shp)).float().cuda() for k, shp in
               (("asr", (B, 512, F_)), ("d", (B, T, 50)), ("p", (B, 640, F_)))}
     tok_t, ln_t = torch.from_numpy(tok).cuda(), torch.from_numpy(ln)
     sd = torch.from_numpy(s).cuda().requires_grad_(True)
     attn = torch.from_numpy(aln).cuda()
     m = torch.arange(T)[None, :] + 1 > ln_t[:, None]  # length_to_mask (models.py:463-466)
-    t_en = te(tok_t, ln_t, m)
-    asr = matmul(t_en, attn)
-    d, p = pp(t_en, sd, ln_t, attn, m)
+    try:
+        t_en = te(tok_t, ln_t, m)
+        asr = matmul(t_en, attn)
+        d, p = pp(t_en, sd, ln_t, attn, m)
+    finally:
+        training.set_dropout_masks(None)
+    if mode == "train":  # 3 CNN blocks (p 0.2), 3 DurationEncoder LSTMs (0.2), the duration projection (0.5)
+        assert [c[2] for c in calls] == [0.2] * 6 + [0.5], calls
     loss_dur, loss_ce = texttrain.duration_losses(d, attn.sum(-1), ln_t)
     loss = ((asr * probes["asr"]).sum() + (d * probes["d"]).sum() + (p * probes["p"]).sum()
             + float(fx["lambda_dur"]) * loss_dur + float(fx["lambda_ce"]) * loss_ce)
