@@ -524,7 +524,8 @@ int stts_profile_launch(long long i, int* shape, double* ms_flops_bytes);
  * write every byte of a bf16 frames buffer [rows][ld] exactly once (mode 3: plus `halo` rows per tile
  * side) with the conv engines' access patterns: 0 coalesced 16-B loads, 1 LDS-DMA 1 KiB per instruction,
  * 2 / 3 bigconv2's 64-B window row segments per 32-channel group (tile rows, halo), 4 coalesced 16-B
- * stores, 5 bigconv2's epilogue stores, 6 bigconv2's residual loads (the epilogue's per-lane pieces).  `grid` workgroups of 256 threads; sink[grid] floats.
+ * stores, 5 bigconv2's epilogue stores, 6 bigconv2's residual loads (the epilogue's per-lane pieces), 7 / 8 the
+ * polyphase upsamplers' epilogue stores / residual loads (mode 5 / 6 pieces at rows `halo` apart, phase by phase).  `grid` workgroups of 256 threads; sink[grid] floats.
  * Used by tools/calib_traffic.py under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE. */
 int stts_calib_traffic(int mode, void* buf, long long rows, int ld, int tile, int halo, int grid, float* sink,
                        void* stream);

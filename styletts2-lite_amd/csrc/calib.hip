@@ -15,6 +15,9 @@
 //      (frame l32, half hi) stores 16 B at channels 16 hi + {0, 8} (two instructions fill a 64-B
 //      row segment); every byte written once
 //   6  bigconv2's residual loads: the same per-lane 16-B pieces as mode 5, loaded
+//   7  the polyphase upsamplers' epilogue stores (bigconv2 UPS): mode 5's per-lane pieces at rows q up + ph, the 32
+//      frames of a fragment `up` rows apart (up = the `halo` argument), one output phase ph at a time
+//   8  the upsamplers' residual loads: mode 7's pieces, loaded
 // Each workgroup (256 threads) walks a contiguous range of tiles; the reads are summed into one
 // word per workgroup so nothing is optimised away.
 #include "common.h"
@@ -69,6 +72,30 @@ __global__ void __launch_bounds__(256) k_calib(int mode, char* buf, long long ro
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       }
     }
+  } else if (mode == 7 || mode == 8) {
+    const int up = halo, ncb = ld / 32;
+    const long long nq = rows / up;              // rows = nq up: q = 0 .. nq - 1, phases 0 .. up - 1
+    const long long nfrag = (nq + 31) / 32;
+    const long long items = nfrag * ncb * up;    // (phase, fragment, channel block)
+    const long long i0 = items * (blockIdx.x * 4 + wv) / (gridDim.x * 4);
+    const long long i1 = items * (blockIdx.x * 4 + wv + 1) / (gridDim.x * 4);
+    const int l32 = lane & 31, hi = lane >> 5;
+    for (long long it = i0; it < i1; ++it) {
+      const int ph = (int)(it / (nfrag * ncb));
+      const long long rem = it % (nfrag * ncb);
+      const long long q = (rem / ncb) * 32 + l32;
+      const int co0 = (int)(rem % ncb) * 32 + 16 * hi;
+      const unsigned ey = q < nq ? (unsigned)(((q * up + ph) * ld + co0) * 2) : OOB;
+      if (mode == 8) {
+        const uint4 a = bload16(r, ey), b = bload16(r, ey == OOB ? OOB : ey + 16u);
+        acc += __uint_as_float((a.x ^ b.y) & 0x3fffffffu) * 1e-30f;
+        continue;
+      }
+      const uint4 v = make_uint4((unsigned)it, 1u, 2u, 3u);
+      const auto vv = *reinterpret_cast<const __attribute__((ext_vector_type(4))) unsigned*>(&v);
+      __builtin_amdgcn_raw_buffer_store_b128(vv, r, (int)ey, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(vv, r, (int)(ey == OOB ? OOB : ey + 16u), 0, 0);
+    }
   } else if (mode == 5 || mode == 6) {
     const int ncb = ld / 32;
     const long long nfrag = (rows + 31) / 32;  // 32-frame fragments
@@ -122,7 +149,8 @@ extern "C" int stts_test_fxsum(int mode, const void* parts, long long n, double*
 
 extern "C" int stts_calib_traffic(int mode, void* buf, long long rows, int ld, int tile, int halo, int grid,
                                   float* sink, void* stream) {
-  if (mode < 0 || mode > 6 || !buf || !sink || rows <= 0 || ld <= 0 || ld % 32 || grid <= 0) return ST_EINVAL;
+  if (mode < 0 || mode > 8 || !buf || !sink || rows <= 0 || ld <= 0 || ld % 32 || grid <= 0) return ST_EINVAL;
+  if ((mode == 7 || mode == 8) && (halo < 1 || rows % halo)) return ST_EINVAL;  // (halo = the row stride up)
   if ((mode == 2 || mode == 3) && (tile <= 0 || tile + 2 * halo > 2048)) return ST_EINVAL;
   if (rows * (long long)ld * 2 >= (long long)OOB) return ST_EINVAL;  // buffer offsets are 32-bit
   hipLaunchKernelGGL(k_calib, dim3((unsigned)grid), dim3(256), 8192, (hipStream_t)stream, mode, (char*)buf, rows, ld,

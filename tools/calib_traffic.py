@@ -22,7 +22,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "styletts2-lite_amd")]
 
 MODES = {0: "coalesced 16-B loads", 1: "LDS-DMA 1 KiB", 2: "bigconv2 window 64-B segments",
          3: "bigconv2 window + halo", 4: "coalesced 16-B stores", 5: "bigconv2 epilogue stores",
-         6: "bigconv2 residual loads"}
+         6: "bigconv2 residual loads", 7: "upsampler epilogue stores", 8: "upsampler residual loads"}
 
 
 def expected_bytes(mode, rows, ld, tile, halo):
@@ -46,6 +46,8 @@ def run(a):
     sink = torch.zeros(grid, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     for mode in MODES:
+        if mode in (7, 8) and a.rows % a.halo:
+            raise SystemExit("modes 7 / 8: --rows must be a multiple of --halo (the upsampling factor)")
         for _ in range(2):
             scrub.fill_(1.0)
             r = L.stts_calib_traffic(mode, buf.data_ptr(), a.rows, a.ld, a.tile, a.halo, grid, sink.data_ptr(), s)
@@ -81,7 +83,7 @@ def reduce(a):
         fk = [fetch[2 * i + j][0] for j in range(2)]
         wk = [write[2 * i + j][0] for j in range(2)]
         us = [fetch[2 * i + j][1] / 1e3 for j in range(2)]
-        writes = mode in (4, 5)
+        writes = mode in (4, 5, 7)
         cnt = min(wk) if writes else min(fk)
         res["modes"][mode] = {
             "pattern": MODES[mode], "bytes": exp, "fetch_kib": fk, "write_kib": wk, "dispatch_us_fetch_pass": us,
