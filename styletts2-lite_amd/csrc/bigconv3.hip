@@ -606,7 +606,8 @@ int b3_num_cu() {
 #ifndef B3_ONLY
 // STTS_OPT_BIG3 (bit mask): 1 = the C = 128 / 256 resblock convs, 2 = the front-end k3 convs, 4 = ups[0] / ups[1] run
 // on this engine instead of bigconv2 (and v1 for C = 128 k3); 8 = C = 128 on 8-wave blocks (512-frame tiles, 4-tap
-// chunks) instead of two 4-wave blocks per CU (256-frame tiles, 2-tap chunks)
+// chunks) instead of two 4-wave blocks per CU (256-frame tiles, 2-tap chunks); 16 = C = 256 on two 4-wave blocks per CU
+// (1-tap chunks) at every batch size
 int g_opt_big3 = 0;
 
 int st_bigconv3(const ConvParams& p, hipStream_t s) {
@@ -616,7 +617,8 @@ int st_bigconv3(const ConvParams& p, hipStream_t s) {
   if (p.Cout == 256) {
     // (few tiles, small batches: 4-wave blocks, two per CU, as bigconv2 does)
     const long long tiles8 = (long long)((p.Lq + 255) / 256) * p.B;
-    return tiles8 < b3_num_cu() ? launch_b3_c<256, 4>(p, s) : launch_b3_c<256, 8>(p, s);
+    // (bit 16: 4-wave blocks, two per CU, at every size: one block's chunk barriers beside the other's MFMAs; A/B)
+    return (tiles8 < b3_num_cu() || (g_opt_big3 & 16)) ? launch_b3_c<256, 4>(p, s) : launch_b3_c<256, 8>(p, s);
   }
   return ST_EINVAL;
 }
