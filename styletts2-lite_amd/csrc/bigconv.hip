@@ -506,7 +506,7 @@ int launch_bc(const ConvParams& p, hipStream_t stream) {
   }
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p.B, 1, g_num_cu_bc);
+  q.seg = st_seg_choice(p, 1, g_num_cu_bc);
   long long grid = g_num_cu_bc;
   if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;

@@ -831,7 +831,7 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
   }
   const long long tiles = (long long)((p.Lq + G::TM - 1) / G::TM) * G::NCH * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p.B, 1, ncu * G::BPC);
+  q.seg = st_seg_choice(p, 1, ncu * G::BPC);
   long long grid = (long long)ncu * G::BPC;
   if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;

@@ -98,7 +98,11 @@ __device__ __forceinline__ void pw(float (&v)[16], int i, f2v x) {
 // 16*((m>>2)&1) + (m&3) + 4*(m>>3)), 16 CONSECUTIVE channels 16*(lane>>5) + r.  The epilogue
 // therefore works straight from registers: no LDS transpose, 16-channel vector loads/stores,
 // and per-lane statistics accumulated across tiles (reduced across lanes once per utterance).
-template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW, int CPS, bool SPF = true>
+// SEG: the launch runs segmented tile ranges (p.seg > 0, statistics launches of B = 32 k utterances); the plain
+// instantiation keeps the one-range-per-workgroup code (a range loop in every launch had cost the training step's
+// igemm convs 5-15 %: register allocation and hoisting across the loop)
+template <typename T, typename MT, int WAVES_M, int WAVES_N, int WM, int WN, bool NARROW, int CPS, bool SPF = true,
+          bool SEG = false>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>))
     conv1d_igemm_kernel(const ConvParams p) {
   using C = ConvCfg<T, MT, WAVES_M, WAVES_N, WM, WN, SPF>;
@@ -129,12 +133,17 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
   // land on one XCD, so each XCD's L2 holds the weights of ~1/8 of the column tiles
   // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments); the first is
   // the XCD-remapped one
-  const int nv = tile_nv(p, p.B);
+  const int nv = SEG ? tile_nv(p, p.B) : (int)gridDim.x;
   for (int vb = xcd_remap(blockIdx.x, gridDim.x); vb < nv; vb += gridDim.x) {
   long long tb_, te_;
-  tile_range(p, vb, nv, total, (long long)ntn * ntm, tb_, te_);
+  if constexpr (SEG) {
+    tile_range(p, vb, nv, total, (long long)ntn * ntm, tb_, te_);
+  } else {
+    tb_ = total * vb / gridDim.x;
+    te_ = total * (vb + 1) / gridDim.x;
+  }
   const int tbeg = (int)tb_, tend = (int)te_;
-  if (tbeg >= tend) continue;  // uniform over the block
+  if (SEG && tbeg >= tend) continue;  // uniform over the block
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
@@ -149,8 +158,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
   // (segmented ranges, p.seg > 0: utterance-major instead, (utterance, column tile, row tile), so that a range lies
   // inside one utterance whatever the column-tile count)
   auto t_mt = [&](int t) { return t % ntm; };
-  auto t_b = [&](int t) { return p.seg > 0 ? t / (ntm * ntn) : (t / ntm) % p.B; };
-  auto t_nt = [&](int t) { return p.seg > 0 ? (t / ntm) % ntn : t / (ntm * p.B); };
+  auto t_b = [&](int t) { return SEG ? t / (ntm * ntn) : (t / ntm) % p.B; };
+  auto t_nt = [&](int t) { return SEG ? (t / ntm) % ntn : t / (ntm * p.B); };
   constexpr bool FAST_SIN = C::BF;
 
   // statistics partials: lane = column l32 of tile ni, summed over the frames of its half (hi)
@@ -781,6 +790,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, (kMinWaves<T, MT, SPF>
     }
   }
   if (cur_nt >= 0 && p.stats) flush_stats(cur_nt, cur_b);
+  if constexpr (!SEG) break;  // (one range)
   __syncthreads();  // (the next range re-stages the LDS)
   }  // tile ranges
 }
@@ -818,15 +828,18 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
     p.cps = 2;
   const size_t lds = C::lds_bytes(p, p.w_resident ? nres : p.cps * p.tg, p.cps);
   if (lds > (size_t)LDS_MAX) return ST_EINVAL;
-  auto kern1 = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 1, SPF>;
-  auto kern = kern1;
+  const int sg = st_seg_choice(p, 1, 1 << 20) > 0 ? 1 : 0;  // (a segmented launch; its seg count below)
+  auto kern = sg ? conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 1, SPF, true>
+                 : conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 1, SPF, false>;
   if constexpr (C::LOWP && !NARROW) {
-    if (p.cps == 2) kern = conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 2, SPF>;
+    if (p.cps == 2)
+      kern = sg ? conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 2, SPF, true>
+                : conv1d_igemm_kernel<T, MT, WAVES_M, WAVES_N, WM, WN, NARROW, 2, SPF, false>;
   }
-  static bool attr_set[2] = {false, false};
-  if (!attr_set[p.cps - 1]) {
+  static bool attr_set[2][2] = {{false, false}, {false, false}};
+  if (!attr_set[sg][p.cps - 1]) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
-    attr_set[p.cps - 1] = true;
+    attr_set[sg][p.cps - 1] = true;
   }
   if (!g_num_cu) {
     int dev = 0;
@@ -840,7 +853,7 @@ int launch_cfg(ConvParams p, hipStream_t stream) {
   if (tiles <= 0) return ST_OK;
   if (tiles > 0x7fffffffLL) return ST_EINVAL;
   ConvParams q = p;
-  q.seg = st_seg_choice(p.B, 1, g_num_cu * per_cu);
+  q.seg = sg ? st_seg_choice(p, 1, g_num_cu * per_cu) : 0;
   const long long nvb = q.seg ? (long long)p.B * q.seg : tiles;
   long long grid = (long long)g_num_cu * per_cu;
   if (grid > nvb) grid = nvb;
@@ -896,8 +909,12 @@ int g_opt_resfused = 0;
 int g_opt_grid_cap = 0;
 int g_opt_segpart = 1;
 
-int st_seg_choice(int B, int upu, int gmax) {
-  if (!g_opt_segpart || B < 32 || B % 32 || upu <= 0) return 0;
+// (only launches that keep InstanceNorm statistics: a conv's outputs do not depend on the tile -> workgroup split, its
+// statistics' fp32 partials do.  A plain launch over many short rows — the discriminators' reshaped batches — would
+// otherwise get mostly empty segments, each re-staging the layer's weights: 2.3x slower igemm in the training step)
+int st_seg_choice(const ConvParams& p, int upu, int gmax) {
+  const int B = p.B;
+  if (!g_opt_segpart || !p.stats || B < 32 || B % 32 || upu <= 0) return 0;
   const int seg = gmax / (32 * upu);
   return seg >= 1 ? seg : 0;
 }

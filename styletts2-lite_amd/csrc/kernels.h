@@ -92,7 +92,7 @@ __device__ __forceinline__ void tile_range(const ConvParams& p, int v, int nv, l
 // host: segments per unit for a launch of B utterances with `upu` units each on a grid of up to gmax workgroups.
 // Segmented when B is a multiple of 32 (every config-4 shard, 256 / W utterances): seg = gmax / (32 upu), so B = 32 k
 // gives every workgroup k ranges of equal size; 0 (the even split) otherwise, or with STTS_OPT_SEGPART 0
-int st_seg_choice(int B, int upu, int gmax);
+int st_seg_choice(const ConvParams& p, int upu, int gmax);
 extern int g_opt_segpart;
 
 int st_conv1d(const ConvParams& p, int dtype, hipStream_t stream);

@@ -458,7 +458,7 @@ int st_pw(const ConvParams& p, hipStream_t stream) {
     ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_pw, hipDeviceAttributeMultiprocessorCount, dev));
   }
   ConvParams q = p;
-  q.seg = st_seg_choice(p.B, 1, g_num_cu_pw * 2);
+  q.seg = st_seg_choice(p, 1, g_num_cu_pw * 2);
   long long blocks = (long long)g_num_cu_pw * 2;  // 220-238 VGPRs: two 4-wave blocks per CU
   if (blocks > (q.seg ? (long long)p.B * q.seg : tiles)) blocks = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && blocks > g_opt_grid_cap) blocks = g_opt_grid_cap;

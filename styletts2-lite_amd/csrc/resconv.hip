@@ -72,7 +72,11 @@ __device__ __forceinline__ uint4 f32_to_bf8(const float* v) {
 // STTS_OPT_EXP bit 4), instead of at the start of the tile that consumes them
 // PF: window prefetch depth in tiles (2; 3 keeps a third raw window in flight: one block per CU at
 // C = 64 holds ~40 KB of loads in flight with two, below the ~70 KB an HBM-rate stream needs)
-template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false, int PF = 2, bool UPS = false>
+// IL: the epilogue of tile t - 1 is issued inside tile t's MFMA loop (one basic block: branch-free, the stores go
+// through a buffer descriptor and rows that are not stored get an out-of-range offset), so its VALU work, residual
+// adds and stores fill the gaps between the MFMAs instead of running after them with the MFMA pipe idle
+template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false, int PF = 2, bool UPS = false,
+          bool IL = false>
 __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvParams p) {
   using G = RC<C, K, DIL, WAVES, WAVES_N, UPS>;
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, NTL = G::NTL, NCH = G::NCH, XP = G::XP, WP = G::WP;
@@ -376,6 +380,116 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     mark(6);
   };
 
+  // ---- IL: tile t's MFMAs with the epilogue of tile t - 1 (live = t - 1 is a tile of this range) in one block
+  const float osc_il = p.res ? p.out_scale : 1.0f;  // (the residual of a launch without one reads as 0)
+  const float adiv_il = (ACC && p.acc_div != 0.f) ? 1.0f / p.acc_div : 1.0f;
+  // (a statistics-only launch, y == null, stores through a zero-range descriptor: every store dropped)
+  const size_t ybs_il = p.y ? (size_t)p.y_bs * 2 : 0;
+  const unsigned yrange_il = p.y ? (unsigned)((size_t)p.Lq * p.y_ld * 2) : 0u;
+  // one epilogue unit: 8 channels (half hh of block (mi, ni)) of the lane's frame; NU units per tile
+  constexpr int NU = MT * NTL * 2;
+  auto epi_unit = [&](int t, bool live, const f32x16 (&accp)[MT][NTL], const EpiRegs& er_, int u)
+                      __attribute__((always_inline)) {
+    const int mi = u / (2 * NTL), ni = (u / 2) % NTL, hh = u & 1;
+    const int b = t / ntm, mt = t - b * ntm;
+    const Rsrc ry = make_rsrc(reinterpret_cast<const char*>(p.y) + (size_t)b * ybs_il, yrange_il);
+    const int q = mt * BM + wm * FW + mi * 32 + l32;
+    // (masks, not branches: the region must stay one basic block)
+    const unsigned keep = (live && q < p.Lq) ? 0xffffffffu : 0u;
+    const int co0 = (wn * NTL + ni) * 32 + hi * 16 + 8 * hh;
+    float v[8], bb[8], r0[8];
+    ld8_lds(bias_s + co0, bb);
+    bf8_to_f32(er_.rres[mi][ni][hh], r0);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = (accp[mi][ni][8 * hh + r] + bb[r] + r0[r]) * osc_il;
+    if constexpr (ACC) {
+      bf8_to_f32(er_.racc[mi][ni][hh], r0);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = (r0[r] + v[r]) * adiv_il;
+    }
+    bstore16(ry, ((unsigned)(q * p.y_ld + co0) * 2u) | (~keep & OOB), f32_to_bf8(v));
+    if constexpr (!ACC) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float x = __uint_as_float(__float_as_uint(v[r]) & keep);
+        st_s[ni][8 * hh + r] += x;
+        st_q[ni][8 * hh + r] = __builtin_fmaf(x, x, st_q[ni][8 * hh + r]);
+      }
+    }
+  };
+  auto epi_il = [&](int t, bool live, const f32x16 (&accp)[MT][NTL], const EpiRegs& er_) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) epi_unit(t, live, accp, er_, u);
+  };
+  EpiRegs e_il;  // the residual rows of tile t - 1, loaded at the start of step t
+  auto step_il = [&](int t, uint4 (&pre)[MAXU], f32x16 (&acc)[MT][NTL],
+                     const f32x16 (&accp)[MT][NTL]) __attribute__((always_inline)) {
+    const int b = t / ntm;
+    if (b != cur_b) {  // tile t's coefficients (every wave is past its previous transform: barrier B)
+      for (int ci = tid; ci < C; ci += NT) {
+        if (p.pro.mode == 0) {
+          coef[ci] = 0.f;
+          coef[C + ci] = 1.f;
+          coef[2 * C + ci] = coef[3 * C + ci] = coef[4 * C + ci] = 0.f;
+          continue;
+        }
+        float mm = 0.f, aa = 1.f, be = 0.f;
+        adain_coeffs(p.pro, b, ci, mm, aa, be);
+        const float al = p.pro.alpha[ci];
+        const float m1 = be - mm * aa, ia2 = 0.5f / al, alr = al * 0.31830988618379067f;
+        coef[ci] = m1 + ia2;
+        coef[C + ci] = aa;
+        coef[2 * C + ci] = aa * alr;
+        coef[3 * C + ci] = m1 * alr;
+        coef[4 * C + ci] = -ia2;
+      }
+      cur_b = b;
+    }
+    issue_epi(t > tbeg ? t - 1 : t, e_il);
+    __syncthreads();  // (A)
+    transform(t, pre);
+    if (t + PF < tend) issue(t + PF, pre);
+    __syncthreads();  // (B)
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NTL; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+    const bf16_t* xw = Xs + (size_t)(wm * FW + l32) * XP + hi * 8;
+    const bf16_t* ww = Ws + (size_t)(wn * NTL * 32 + l32) * WP + hi * 8;
+    constexpr int S = K * NCH * 2;
+    auto ldfr = [&](int st, bf16x8 (&wa)[NTL], bf16x8 (&xb)[MT]) __attribute__((always_inline)) {
+      const int tap = st / (NCH * 2), c = (st / 2) % NCH, kk = st & 1;
+      const bf16_t* xt = xw + tap * DIL * XP;
+      const bf16_t* wt = ww + tap * C * WP;
+#pragma unroll
+      for (int ni = 0; ni < NTL; ++ni)
+        wa[ni] = *reinterpret_cast<const bf16x8*>(wt + (c * K * C + ni * 32) * WP + kk * 16);
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+        xb[mi] = *reinterpret_cast<const bf16x8*>(xt + mi * 32 * XP + c * 32 + kk * 16);
+    };
+    bf16x8 wa[2][NTL], xb[2][MT];
+    ldfr(0, wa[0], xb[0]);
+#pragma unroll
+    for (int st = 0; st < S; ++st) {
+      const int cb = st & 1;
+      if (st + 1 < S) ldfr(st + 1, wa[cb ^ 1], xb[cb ^ 1]);
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NTL; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[cb][ni], xb[cb][mi], acc[mi][ni], 0, 0, 0);
+      // epilogue unit u of tile t - 1 after MFMA step (2 u + 1) S / (2 NU): its VALU work fills this step's gaps
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        if (st == ((2 * u + 1) * S) / (2 * NU)) epi_unit(t > tbeg ? t - 1 : t, t > tbeg, accp, e_il, u);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t > tbeg && (t - 1) / ntm != b && p.stats) flush((t - 1) / ntm);  // tile t - 1 closed its utterance
+  };
+
   for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
   {
     long long tb_, te_;
@@ -384,6 +498,29 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     tend = (int)te_;
   }
   if (tbeg >= tend) continue;  // uniform over the block
+  if constexpr (IL) {
+    uint4 preA[MAXU], preB[MAXU];
+    f32x16 accA[MT][NTL], accB[MT][NTL];
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NTL; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accB[mi][ni][r] = 0.f;
+    issue(tbeg, preA);
+    if (tbeg + 1 < tend) issue(tbeg + 1, preB);
+    for (int t = tbeg; t < tend; t += 2) {
+      step_il(t, preA, accA, accB);
+      if (t + 1 < tend) step_il(t + 1, preB, accB, accA);
+    }
+    // the range's last tile: its epilogue alone
+    issue_epi(tend - 1, e_il);
+    if ((tend - 1 - tbeg) % 2 == 0) epi_il(tend - 1, true, accA, e_il);
+    else epi_il(tend - 1, true, accB, e_il);
+    if (p.stats) flush(cur_b);
+    cur_b = -1;
+    continue;
+  }
   uint4 preA[MAXU], preB[MAXU];
   EpiRegs eA, eB;
   if constexpr (RPF) issue_epi(tbeg, eA);
@@ -416,12 +553,14 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
 
 int g_num_cu_rc = 0;
 
-template <int C, int K, int DIL, bool ACC, bool RPF = false, int PF = 2, bool UPS = false>
+// WV / WN: block shape override (0 = the default: 4 x 1 waves at C = 32, 8 x 2 at C = 64)
+template <int C, int K, int DIL, bool ACC, bool RPF = false, int PF = 2, bool UPS = false, int WV = 0, int WN = 0,
+          bool IL = false>
 int launch_rc(const ConvParams& p, hipStream_t stream) {
-  constexpr int WAVES = C == 32 ? 4 : 8;
-  constexpr int WAVES_N = C == 32 ? 1 : 2;
+  constexpr int WAVES = WV ? WV : C == 32 ? 4 : 8;
+  constexpr int WAVES_N = WN ? WN : C == 32 ? 1 : 2;
   using G = RC<C, K, DIL, WAVES, WAVES_N, UPS>;
-  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS>;
+  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS, IL>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -436,7 +575,7 @@ int launch_rc(const ConvParams& p, hipStream_t stream) {
   if (per_cu < 1) per_cu = 1;
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p.B, 1, g_num_cu_rc * per_cu);
+  q.seg = st_seg_choice(p, 1, g_num_cu_rc * per_cu);
   long long grid = (long long)g_num_cu_rc * per_cu;
   if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
@@ -778,7 +917,7 @@ int launch_pp(const ConvParams& p, hipStream_t stream) {
   }
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p.B, 1, g_num_cu_pp);
+  q.seg = st_seg_choice(p, 1, g_num_cu_pp);
   long long grid = g_num_cu_pp;
   if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
@@ -797,6 +936,22 @@ int launch_rc_a(const ConvParams& p, hipStream_t s) {
   if constexpr (C == 64) {
     if (g_opt_rcpp == 2 || (g_opt_rcpp == 1 && K >= 7 && (p.res || p.accb)))
       return p.accb ? launch_pp<K, DIL, true>(p, s) : launch_pp<K, DIL, false>(p, s);
+  }
+  // STTS_OPT_EXP bit 32768: the interleaved epilogue (IL)
+  if (g_opt_exp & 32768)
+    return p.accb ? launch_rc<C, K, DIL, true, false, 2, false, 0, 0, true>(p, s)
+                  : launch_rc<C, K, DIL, false, false, 2, false, 0, 0, true>(p, s);
+  // STTS_OPT_EXP bit 262144 / 524288: C = 64 on 4-wave blocks (two or more per CU, each running its own tile loop,
+  // so one block's MFMAs overlap the other's memory / VALU phases): 4 x 2 waves of 64 frames x 32 channels (128-frame
+  // tiles) / 4 x 1 waves of 64 frames x 64 channels (256-frame tiles); bit 1048576 limits it to K = 3
+  if constexpr (C == 64) {
+    if ((g_opt_exp & (262144 | 524288)) && (K == 3 || !(g_opt_exp & 1048576))) {
+      if (g_opt_exp & 262144)
+        return p.accb ? launch_rc<C, K, DIL, true, false, 2, false, 4, 2>(p, s)
+                      : launch_rc<C, K, DIL, false, false, 2, false, 4, 2>(p, s);
+      return p.accb ? launch_rc<C, K, DIL, true, false, 2, false, 4, 1>(p, s)
+                    : launch_rc<C, K, DIL, false, false, 2, false, 4, 1>(p, s);
+    }
   }
   // STTS_OPT_EXP bit 8 / 16: window prefetch three tiles deep at C = 64 / C = 32 (register budget allows it:
   // 231-249 VGPRs, occupancy unchanged)

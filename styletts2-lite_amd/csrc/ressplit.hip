@@ -374,7 +374,7 @@ int launch_rs_pf(const ConvParams& p, hipStream_t stream) {
   if (per_cu < 1) per_cu = 1;
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p.B, 1, g_num_cu_rs * per_cu);
+  q.seg = st_seg_choice(p, 1, g_num_cu_rs * per_cu);
   long long grid = (long long)g_num_cu_rs * per_cu;
   if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
