@@ -453,8 +453,10 @@ int stts_abi_version(void);
 #define STTS_OPT_MSDFOLD 17
 /*   STTS_OPT_RCPP     resconv's two-group ping-pong kernel at C = 64 (one 4-wave group computes a 128-frame tile
  *                     while the other runs the previous tile's epilogue and the next window's transform):
- *                     1 = for the residual / running-sum launches with K >= 7 (default, where it measured
- *                     faster), 2 = for every C = 64 launch, 0 = never. */
+ *                     1 = for the residual / running-sum launches with K >= 7 (where it measured faster than
+ *                     the lock-step kernel), 2 = for every C = 64 launch, 0 = never; 3 (default, round 6) = those
+ *                     launches on the lock-step kernel with the previous tile's epilogue interleaved into the
+ *                     MFMA loop instead (3-5 % faster than the ping-pong kernel, profiles/r06_ab_rcpp3.txt). */
 #define STTS_OPT_RCPP 18
 /*   STTS_OPT_RESSPLIT 1 (default) = the accuracy mode's (STTS_SPLIT) C = 32 / 64 resblock convs run on the split
  *                     resblock engine (ressplit.hip; C = 64 in two input-channel passes); 0 = conv1d_igemm (A/B). */

@@ -2030,7 +2030,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_WGRAD: g_opt_wgw = value ? 1 : 0; return 0;
     case STTS_OPT_PLAINRC: g_opt_plainrc = value ? 1 : 0; return 0;
     case STTS_OPT_MSDFOLD: g_opt_msdfold = value ? 1 : 0; return 0;
-    case STTS_OPT_RCPP: g_opt_rcpp = (value >= 0 && value <= 2) ? value : 1; return 0;
+    case STTS_OPT_RCPP: g_opt_rcpp = (value >= 0 && value <= 3) ? value : 1; return 0;
     case STTS_OPT_RESSPLIT: g_opt_ressplit = value ? 1 : 0; return 0;
     case STTS_OPT_BIGSPLIT: g_opt_bigsplit = value; return 0;
     case STTS_OPT_BIGLA: g_opt_bigla = value; return 0;

@@ -933,9 +933,13 @@ int launch_rc_a(const ConvParams& p, hipStream_t s) {
   }
   // STTS_OPT_RCPP: the two-group ping-pong kernel at C = 64 (1: residual / running-sum launches with K >= 7,
   // where the in-process A/B measured it faster, profiles/r03_ab_resconv_pp.txt; 2: every launch)
+  // (3: those launches on the lock-step kernel with the interleaved epilogue instead, IL below)
   if constexpr (C == 64) {
     if (g_opt_rcpp == 2 || (g_opt_rcpp == 1 && K >= 7 && (p.res || p.accb)))
       return p.accb ? launch_pp<K, DIL, true>(p, s) : launch_pp<K, DIL, false>(p, s);
+    if (g_opt_rcpp == 3 && K >= 7 && (p.res || p.accb))
+      return p.accb ? launch_rc<C, K, DIL, true, false, 2, false, 0, 0, true>(p, s)
+                    : launch_rc<C, K, DIL, false, false, 2, false, 0, 0, true>(p, s);
   }
   // STTS_OPT_EXP bit 32768: the interleaved epilogue (IL)
   if (g_opt_exp & 32768)
@@ -983,7 +987,7 @@ int launch_rc_k(const ConvParams& p, hipStream_t s) {
 }  // namespace
 
 int g_opt_plainrc = 1;
-int g_opt_rcpp = 1;
+int g_opt_rcpp = 3;
 
 bool st_resconv_eligible(const ConvParams& p, int dtype) {
   if (dtype != ST_BF16) return false;

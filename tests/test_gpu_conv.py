@@ -207,6 +207,28 @@ def test_resconv_pingpong_matches_lockstep(case, cap):
     np.testing.assert_allclose(s1.numpy(), s0.numpy(), rtol=1e-4, atol=1e-2)
 
 
+IL_CASES = PP_CASES + [c for c in RB_CASES if c[1] == 32]
+
+
+@pytest.mark.parametrize("cap", [0, 3])
+@pytest.mark.parametrize("case", IL_CASES, ids=[c[0] for c in IL_CASES])
+def test_resconv_interleaved_epilogue_bitwise(case, cap):
+    """bf16, C = 32 / 64: the lock-step resconv kernel with tile t - 1's epilogue interleaved into tile t's MFMA loop
+    (STTS_OPT_EXP bit 32768; the default for the C = 64 residual / running-sum launches, STTS_OPT_RCPP 3) against the
+    same kernel without it: same tiles, same MFMA chain and per-lane statistics order, so outputs AND statistics are
+    bitwise equal.  cap = 3: ranges across utterances (coefficient switch and flush one step after the tile)."""
+    try:
+        E.set_option(E.OPT_GRID_CAP, cap)
+        E.set_option(E.OPT_RCPP, 0)
+        _, y0, s0 = run_case(case, "bf16")
+        E.set_option(E.OPT_EXP, 32768)
+        _, y1, s1 = run_case(case, "bf16")
+    finally:
+        E.reset_options()
+    assert torch.equal(y1, y0), (case[0], (y1 - y0).abs().max().item())
+    assert torch.equal(s1, s0), case[0]
+
+
 FRONT_CASES = [c for c in CASES if c[0].startswith("front")]
 
 
