@@ -75,7 +75,8 @@ __device__ __forceinline__ uint4 f32_to_bf8(const float* v) {
   return r;
 }
 
-template <int C, int K, int DIL, bool ACC>
+// SEG: several tile ranges per workgroup (bigconv2.hip k_bigconv2: the plain instantiation runs one range)
+template <int C, int K, int DIL, bool ACC, bool SEG = false>
 __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   using G = BG<C, K, DIL>;
   using F = typename G::F;
@@ -94,10 +95,15 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   const int ntm = (p.Lq + BM - 1) / BM;
   const long long total = (long long)ntm * p.B;
   // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments)
-  const int nv = tile_nv(p, p.B);
+  const int nv = SEG ? tile_nv(p, p.B) : (int)gridDim.x;
   for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
   long long tb_, te_;
-  tile_range(p, vb, nv, total, ntm, tb_, te_);
+  if constexpr (SEG) {
+    tile_range(p, vb, nv, total, ntm, tb_, te_);
+  } else {
+    tb_ = total * vb / gridDim.x;
+    te_ = total * (vb + 1) / gridDim.x;
+  }
   const int tbeg = (int)tb_, tend = (int)te_;
   if (tbeg >= tend) continue;  // uniform over the block
   const int nsteps = (tend - tbeg) * NS;
@@ -484,6 +490,7 @@ __global__ void __launch_bounds__(512, 1) k_bigconv(const ConvParams p) {
   } else if constexpr (!ACC) {
     if (p.stats) flush_lds(cur_b);
   }
+  if constexpr (!SEG) break;  // (one range)
   __syncthreads();  // (the next range re-stages the LDS)
   }  // tile ranges
 }
@@ -493,10 +500,12 @@ int g_num_cu_bc = 0;
 template <int C, int K, int DIL, bool ACC>
 int launch_bc(const ConvParams& p, hipStream_t stream) {
   using G = BG<C, K, DIL>;
-  auto kern = k_bigconv<C, K, DIL, ACC>;
+  auto kern0 = k_bigconv<C, K, DIL, ACC, false>;
+  auto kern1 = k_bigconv<C, K, DIL, ACC, true>;
   static bool attr = false;
   if (!attr) {
-    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern0, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern1, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
     attr = true;
   }
   if (!g_num_cu_bc) {
@@ -506,11 +515,13 @@ int launch_bc(const ConvParams& p, hipStream_t stream) {
   }
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p, 1, g_num_cu_bc);
+  const int seg = st_seg_choice(p, 1, g_num_cu_bc);
   long long grid = g_num_cu_bc;
-  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
+  if (grid > (seg ? (long long)p.B * seg : tiles)) grid = seg ? (long long)p.B * seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
+  const bool segk = seg > 0 && grid < (long long)p.B * seg;  // (one segment per workgroup = the plain even split)
+  q.seg = segk ? seg : 0;
+  hipLaunchKernelGGL(segk ? kern1 : kern0, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
 

@@ -98,8 +98,11 @@ struct B2 {
   static_assert(OFF_W % 1024 == 0 && OFF_X % 1024 == 0, "DMA bases");
 };
 
+// SEG: several tile ranges per workgroup (segmented partition, p.seg > 0, with fewer workgroups than segments); the
+// plain instantiation runs the one-range code (a range loop in every launch measured ~0.5 % of the step)
 template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE, int CINP = C, bool EPI1 = false,
-          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8, int NCB = 0>
+          bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8, int NCB = 0,
+          bool SEG = false>
 __global__ void __launch_bounds__(64 * NW, NW == 12 ? 3 : 2) k_bigconv2(const ConvParams p) {
   using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF, NCB>;
   constexpr int FW = 32 * NF;  // frames per wave
@@ -124,10 +127,15 @@ __global__ void __launch_bounds__(64 * NW, NW == 12 ? 3 : 2) k_bigconv2(const Co
   const long long total = (long long)ntm * NCH * p.B;
   const int upb = ntm * NCH;  // tiles per utterance
   // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments)
-  const int nv = tile_nv(p, p.B);
+  const int nv = SEG ? tile_nv(p, p.B) : (int)gridDim.x;
   for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
   long long tb_, te_;
-  tile_range(p, vb, nv, total, upb, tb_, te_);
+  if constexpr (SEG) {
+    tile_range(p, vb, nv, total, upb, tb_, te_);
+  } else {
+    tb_ = total * vb / gridDim.x;
+    te_ = total * (vb + 1) / gridDim.x;
+  }
   const int tbeg = (int)tb_, tend = (int)te_;
   if (tbeg >= tend) continue;  // uniform over the block
   const int NGG = (tend - tbeg) * NG;  // groups this block walks
@@ -810,6 +818,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 12 ? 3 : 2) k_bigconv2(const Co
       for (int k = 0; k < 10; ++k) atomicAdd(p.stamps + k, st_acc[k]);
     if (lane == 0 && wu == 0) atomicAdd(p.stamps + 15, 1ull);
   }
+  if constexpr (!SEG) break;  // (one range)
   }  // tile ranges
 }
 
@@ -817,12 +826,6 @@ template <int C, int NW, int K, int DIL, bool RES, bool ACC, int PRO = PK_SNAKE,
           bool UPS = false, int CO = C, bool OFS = false, bool SP = false, bool LA = false, int NF = 8, int NCB = 0>
 int launch_b2(const ConvParams& p, hipStream_t stream) {
   using G = B2<C, NW, K, DIL, PRO, CINP, UPS, CO, OFS, LA, NF, NCB>;
-  auto kern = k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP, LA, NF, NCB>;
-  static bool attr = false;
-  if (!attr) {
-    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-    attr = true;
-  }
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -831,10 +834,21 @@ int launch_b2(const ConvParams& p, hipStream_t stream) {
   }
   const long long tiles = (long long)((p.Lq + G::TM - 1) / G::TM) * G::NCH * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p, 1, ncu * G::BPC);
+  const int seg = st_seg_choice(p, 1, ncu * G::BPC);
   long long grid = (long long)ncu * G::BPC;
-  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
+  if (grid > (seg ? (long long)p.B * seg : tiles)) grid = seg ? (long long)p.B * seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
+  // one segment per workgroup: the segments are the even split of the plain kernel (every utterance has the same
+  // tile count), so only a launch with more segments than workgroups needs the range loop
+  const bool segk = seg > 0 && grid < (long long)p.B * seg;
+  q.seg = segk ? seg : 0;
+  auto kern = segk ? k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP, LA, NF, NCB, true>
+                   : k_bigconv2<C, NW, K, DIL, RES, ACC, PRO, CINP, EPI1, UPS, CO, OFS, SP, LA, NF, NCB, false>;
+  static bool attr[2] = {false, false};
+  if (!attr[segk]) {
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    attr[segk] = true;
+  }
   q.skew = g_opt_skew;
   q.exp = g_opt_exp;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), G::LDS, stream, q);

@@ -75,8 +75,9 @@ __device__ __forceinline__ uint4 f32_to_bf8(const float* v) {
 // IL: the epilogue of tile t - 1 is issued inside tile t's MFMA loop (one basic block: branch-free, the stores go
 // through a buffer descriptor and rows that are not stored get an out-of-range offset), so its VALU work, residual
 // adds and stores fill the gaps between the MFMAs instead of running after them with the MFMA pipe idle
+// SEG: several tile ranges per workgroup (bigconv2.hip k_bigconv2: the plain instantiation runs one range)
 template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false, int PF = 2, bool UPS = false,
-          bool IL = false>
+          bool IL = false, bool SEG = false>
 __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvParams p) {
   using G = RC<C, K, DIL, WAVES, WAVES_N, UPS>;
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, NTL = G::NTL, NCH = G::NCH, XP = G::XP, WP = G::WP;
@@ -93,7 +94,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   const long long total = (long long)ntm * p.B;
   // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments); the lambdas
   // below read the current range [tbeg, tend) by reference
-  const int nv = tile_nv(p, p.B);
+  const int nv = SEG ? tile_nv(p, p.B) : (int)gridDim.x;
   if ((int)blockIdx.x >= nv) return;  // uniform over the block
   int tbeg = 0, tend = 0;
 
@@ -493,7 +494,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
   {
     long long tb_, te_;
-    tile_range(p, vb, nv, total, ntm, tb_, te_);
+    if constexpr (SEG) {
+      tile_range(p, vb, nv, total, ntm, tb_, te_);
+    } else {
+      tb_ = total * vb / gridDim.x;
+      te_ = total * (vb + 1) / gridDim.x;
+    }
     tbeg = (int)tb_;
     tend = (int)te_;
   }
@@ -519,6 +525,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
     else epi_il(tend - 1, true, accB, e_il);
     if (p.stats) flush(cur_b);
     cur_b = -1;
+    if constexpr (!SEG) break;  // (one range)
     continue;
   }
   uint4 preA[MAXU], preB[MAXU];
@@ -542,6 +549,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvPar
   }
   if (p.stats) flush(cur_b);
   cur_b = -1;  // (the range's statistics are out: the next range re-stages its coefficients, flushes nothing twice)
+  if constexpr (!SEG) break;  // (one range)
   }  // tile ranges
   if (stamp) {
     sacc[7] = __builtin_amdgcn_s_memtime() - t_start;
@@ -560,10 +568,12 @@ int launch_rc(const ConvParams& p, hipStream_t stream) {
   constexpr int WAVES = WV ? WV : C == 32 ? 4 : 8;
   constexpr int WAVES_N = WN ? WN : C == 32 ? 1 : 2;
   using G = RC<C, K, DIL, WAVES, WAVES_N, UPS>;
-  auto kern = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS, IL>;
+  auto kern0 = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS, IL, false>;
+  auto kern1 = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS, IL, true>;
   static bool attr = false;
   if (!attr) {
-    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern0, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern1, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
     attr = true;
   }
   if (!g_num_cu_rc) {
@@ -571,15 +581,17 @@ int launch_rc(const ConvParams& p, hipStream_t stream) {
     ST_CHECK_HIP(hipGetDevice(&dev));
     ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_rc, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  int per_cu = occupancy_cached((const void*)kern, G::NT, G::LDS);
+  int per_cu = occupancy_cached((const void*)kern0, G::NT, G::LDS);
   if (per_cu < 1) per_cu = 1;
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p, 1, g_num_cu_rc * per_cu);
+  const int seg = st_seg_choice(p, 1, g_num_cu_rc * per_cu);
   long long grid = (long long)g_num_cu_rc * per_cu;
-  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
+  if (grid > (seg ? (long long)p.B * seg : tiles)) grid = seg ? (long long)p.B * seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
+  const bool segk = seg > 0 && grid < (long long)p.B * seg;  // (one segment per workgroup = the plain even split)
+  q.seg = segk ? seg : 0;
+  hipLaunchKernelGGL(segk ? kern1 : kern0, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
 
