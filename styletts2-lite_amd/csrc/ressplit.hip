@@ -80,7 +80,8 @@ __device__ __forceinline__ void bstore64(Rsrc r, unsigned off, const float (&v)[
 // latency hides behind the tile's MFMAs instead of being exposed per fragment in the epilogue (default; STTS_OPT_EXP
 // 16384 turns it off for A/B: bit-identical, accuracy-mode step 91.4 -> 90.5 ms, k11 residual launches 928 -> 776 us,
 // profiles/r05_ab_ressplit_prefetch.txt)
-template <int NOUT, int K, int DIL, int PASS, bool ACC, bool PF = false>
+// SEG: several tile ranges per workgroup (bigconv2.hip k_bigconv2: the plain instantiation runs one range)
+template <int NOUT, int K, int DIL, int PASS, bool ACC, bool PF = false, bool SEG = false>
 __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_ressplit(const ConvParams p) {
   using G = RS<NOUT, K, DIL>;
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, XP = G::XP, WP = G::WP, FW = G::FW;
@@ -99,7 +100,7 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
   const long long total = (long long)ntm * p.B;
   // tile ranges (kernels.h tile_range: one per workgroup, or utterance-relative segments); the lambdas
   // below read the current range by reference
-  const int nv = tile_nv(p, p.B);
+  const int nv = SEG ? tile_nv(p, p.B) : (int)gridDim.x;
   if ((int)blockIdx.x >= nv) return;  // uniform over the block
   int tbeg = 0, tend = 0;
 
@@ -336,7 +337,12 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
   for (int vb = blockIdx.x; vb < nv; vb += gridDim.x) {
   {
     long long tb_, te_;
-    tile_range(p, vb, nv, total, ntm, tb_, te_);
+    if constexpr (SEG) {
+      tile_range(p, vb, nv, total, ntm, tb_, te_);
+    } else {
+      tb_ = total * vb / gridDim.x;
+      te_ = total * (vb + 1) / gridDim.x;
+    }
     tbeg = (int)tb_;
     tend = (int)te_;
   }
@@ -350,6 +356,7 @@ __global__ void __launch_bounds__(NOUT == 32 ? 256 : 512, NOUT == 32 ? 2 : 1) k_
   }
   if (p.stats) flush(cur_b);
   cur_b = -1;  // (flushed: the next range re-stages its coefficients)
+  if constexpr (!SEG) break;  // (one range)
   __syncthreads();
   }  // tile ranges
 }
@@ -359,10 +366,12 @@ int g_num_cu_rs = 0;
 template <int NOUT, int K, int DIL, int PASS, bool ACC, bool PF = false>
 int launch_rs_pf(const ConvParams& p, hipStream_t stream) {
   using G = RS<NOUT, K, DIL>;
-  auto kern = k_ressplit<NOUT, K, DIL, PASS, ACC, PF>;
+  auto kern0 = k_ressplit<NOUT, K, DIL, PASS, ACC, PF, false>;
+  auto kern1 = k_ressplit<NOUT, K, DIL, PASS, ACC, PF, true>;
   static bool attr = false;
   if (!attr) {
-    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern0, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern1, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
     attr = true;
   }
   if (!g_num_cu_rs) {
@@ -370,15 +379,17 @@ int launch_rs_pf(const ConvParams& p, hipStream_t stream) {
     ST_CHECK_HIP(hipGetDevice(&dev));
     ST_CHECK_HIP(hipDeviceGetAttribute(&g_num_cu_rs, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  int per_cu = occupancy_cached((const void*)kern, G::NT, G::LDS);
+  int per_cu = occupancy_cached((const void*)kern0, G::NT, G::LDS);
   if (per_cu < 1) per_cu = 1;
   const long long tiles = (long long)((p.Lq + G::BM - 1) / G::BM) * p.B;
   ConvParams q = p;
-  q.seg = st_seg_choice(p, 1, g_num_cu_rs * per_cu);
+  const int seg = st_seg_choice(p, 1, g_num_cu_rs * per_cu);
   long long grid = (long long)g_num_cu_rs * per_cu;
-  if (grid > (q.seg ? (long long)p.B * q.seg : tiles)) grid = q.seg ? (long long)p.B * q.seg : tiles;
+  if (grid > (seg ? (long long)p.B * seg : tiles)) grid = seg ? (long long)p.B * seg : tiles;
   if (g_opt_grid_cap > 0 && grid > g_opt_grid_cap) grid = g_opt_grid_cap;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
+  const bool segk = seg > 0 && grid < (long long)p.B * seg;  // (one segment per workgroup = the plain even split)
+  q.seg = segk ? seg : 0;
+  hipLaunchKernelGGL(segk ? kern1 : kern0, dim3((unsigned)grid), dim3(G::NT), G::LDS, stream, q);
   return (int)hipGetLastError();
 }
 
