@@ -504,7 +504,9 @@ int stts_abi_version(void);
 /*   STTS_OPT_SEGPART 1 (default) = batches of 32 k utterances split every persistent conv launch into utterance-relative
  *                     tile ranges (kernels.h tile_range), so each workgroup's fp32 partial statistics, and with them every
  *                     output bit, do not depend on the batch size: an N-rank job (256 / N utterances a rank) decodes
- *                     the same bits for every N; 0 = one even range per workgroup. */
+ *                     the same bits for every N; 0 = one even range per workgroup.  Only launches
+ *                     that keep InstanceNorm statistics are split (no other result depends on the split); a launch
+ *                     with one segment per workgroup runs the plain one-range kernel (the same ranges). */
 #define STTS_OPT_SEGPART 29
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
