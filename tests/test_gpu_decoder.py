@@ -341,6 +341,31 @@ def test_config4_every_rank_count_bitwise():
             assert torch.equal(full[r * per:(r + 1) * per], part), (W, r)
 
 
+@pytest.mark.parametrize("cap", [100, 37])
+def test_batch32_grid_cap_bitwise(cap):
+    """B = 32 (config 3 / a config-4 rank): the statistics launches split into utterance-relative segments whose count
+    comes from the full grid, so capping the grid (STTS_OPT_GRID_CAP: several segments per workgroup, the segmented
+    kernel instantiations) moves work between workgroups but not a single output bit (device-RNG noise, bf16)."""
+    from stts2_mi355x import engine as E
+    asr, f0, n, s, _ = decoder_case(32, 40)
+    d = dec("hifigan")
+
+    def go():
+        with torch.no_grad():
+            out = d(asr.cuda(), f0.cuda(), n.cuda(), s.cuda(), noise=None, seed=7, dtype="bf16")
+        torch.cuda.synchronize()
+        return out.cpu()
+
+    try:
+        ref = go()
+        E.set_option(E.OPT_GRID_CAP, cap)
+        out = go()
+    finally:
+        E.reset_options()
+    assert torch.isfinite(ref).all()
+    assert torch.equal(out, ref), (out - ref).abs().max().item()
+
+
 def test_default_noise_follows_torch_rng():
     """Decoder.forward without noise / seed draws its noise key from torch's default generator, as the
     reference's randn_like draws (hifigan.py:213): successive calls differ, and torch.manual_seed
