@@ -508,6 +508,9 @@ int stts_abi_version(void);
  *                     that keep InstanceNorm statistics are split (no other result depends on the split); a launch
  *                     with one segment per workgroup runs the plain one-range kernel (the same ranges). */
 #define STTS_OPT_SEGPART 29
+/*   STTS_OPT_RCOCC  1 (default) = resconv's C = 32 launches with K >= 7 and no residual hold their registers to three
+ *                     4-wave blocks per CU (168 VGPRs, three waves per SIMD: 5-6 % faster per launch, round 6); 0 = two. */
+#define STTS_OPT_RCOCC 30
 int stts_set_option(int key, int value);
 /* Current value of an option (STTS_EINVAL for an unknown key). */
 int stts_get_option(int key);

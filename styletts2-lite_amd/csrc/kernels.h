@@ -127,6 +127,7 @@ int st_conv1d_engine(const ConvParams& p, int dtype);
 bool st_resconv_eligible(const ConvParams& p, int dtype);
 int st_resconv(const ConvParams& p, hipStream_t stream);
 extern int g_opt_rcpp;  // STTS_OPT_RCPP
+extern int g_opt_rcocc;  // STTS_OPT_RCOCC
 bool st_resconv_ups_eligible(const ConvParams& p, int dtype);
 int st_resconv_ups(const ConvParams& p, hipStream_t stream);
 extern int g_opt_resconv;

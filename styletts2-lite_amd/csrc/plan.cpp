@@ -2037,6 +2037,7 @@ int stts_set_option(int key, int value) {
     case STTS_OPT_BIG64: g_opt_big64 = value; return 0;
     case STTS_OPT_BIG3: g_opt_big3 = value; return 0;
     case STTS_OPT_SEGPART: g_opt_segpart = value; return 0;
+    case STTS_OPT_RCOCC: g_opt_rcocc = value; return 0;
     case STTS_OPT_BF16F: g_opt_bf16f = value ? 1 : 0; return 0;
     case STTS_OPT_YF32: g_opt_yf32 = value ? 1 : 0; return 0;
     case STTS_OPT_COUT1: g_opt_cout1 = value ? 1 : 0; return 0;
@@ -2083,6 +2084,7 @@ int stts_get_option(int key) {
     case STTS_OPT_BIG64: return g_opt_big64;
     case STTS_OPT_BIG3: return g_opt_big3;
     case STTS_OPT_SEGPART: return g_opt_segpart;
+    case STTS_OPT_RCOCC: return g_opt_rcocc;
     case STTS_OPT_BF16F: return g_opt_bf16f;
     case STTS_OPT_YF32: return g_opt_yf32;
     case STTS_OPT_COUT1: return g_opt_cout1;

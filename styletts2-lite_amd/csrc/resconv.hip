@@ -76,9 +76,10 @@ __device__ __forceinline__ uint4 f32_to_bf8(const float* v) {
 // through a buffer descriptor and rows that are not stored get an out-of-range offset), so its VALU work, residual
 // adds and stores fill the gaps between the MFMAs instead of running after them with the MFMA pipe idle
 // SEG: several tile ranges per workgroup (bigconv2.hip k_bigconv2: the plain instantiation runs one range)
+// MINB: blocks per CU the register allocation is held to (0: 8 / WAVES, two waves per SIMD)
 template <int C, int K, int DIL, int WAVES, int WAVES_N, bool ACC, bool RPF = false, int PF = 2, bool UPS = false,
-          bool IL = false, bool SEG = false>
-__global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) k_resconv(const ConvParams p) {
+          bool IL = false, bool SEG = false, int MINB = 0>
+__global__ void __launch_bounds__(64 * WAVES, MINB ? MINB : 8 / WAVES) k_resconv(const ConvParams p) {
   using G = RC<C, K, DIL, WAVES, WAVES_N, UPS>;
   constexpr int NT = G::NT, BM = G::BM, MT = G::MT, NTL = G::NTL, NCH = G::NCH, XP = G::XP, WP = G::WP;
   constexpr int G8 = G::G8, UNITS = G::UNITS, MAXU = G::MAXU, FW = G::FW;
@@ -563,13 +564,13 @@ int g_num_cu_rc = 0;
 
 // WV / WN: block shape override (0 = the default: 4 x 1 waves at C = 32, 8 x 2 at C = 64)
 template <int C, int K, int DIL, bool ACC, bool RPF = false, int PF = 2, bool UPS = false, int WV = 0, int WN = 0,
-          bool IL = false>
+          bool IL = false, int MINB = 0>
 int launch_rc(const ConvParams& p, hipStream_t stream) {
   constexpr int WAVES = WV ? WV : C == 32 ? 4 : 8;
   constexpr int WAVES_N = WN ? WN : C == 32 ? 1 : 2;
   using G = RC<C, K, DIL, WAVES, WAVES_N, UPS>;
-  auto kern0 = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS, IL, false>;
-  auto kern1 = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS, IL, true>;
+  auto kern0 = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS, IL, false, MINB>;
+  auto kern1 = k_resconv<C, K, DIL, WAVES, WAVES_N, ACC, RPF, PF, UPS, IL, true, MINB>;
   static bool attr = false;
   if (!attr) {
     ST_CHECK_HIP(hipFuncSetAttribute((const void*)kern0, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -953,6 +954,11 @@ int launch_rc_a(const ConvParams& p, hipStream_t s) {
       return p.accb ? launch_rc<C, K, DIL, true, false, 2, false, 0, 0, true>(p, s)
                     : launch_rc<C, K, DIL, false, false, 2, false, 0, 0, true>(p, s);
   }
+  // STTS_OPT_RCOCC: C = 32, K >= 7, no residual: registers held to three 4-wave blocks per CU (168 VGPRs, three waves
+  // per SIMD; 5-6 % faster per launch, profiles/r06_ab_rc3b.txt; the k3 and residual launches measured 0-3 % slower)
+  if constexpr (C == 32 && K >= 7) {
+    if (g_opt_rcocc && !p.res && !p.accb) return launch_rc<C, K, DIL, false, false, 2, false, 0, 0, false, 3>(p, s);
+  }
   // STTS_OPT_EXP bit 32768: the interleaved epilogue (IL)
   if (g_opt_exp & 32768)
     return p.accb ? launch_rc<C, K, DIL, true, false, 2, false, 0, 0, true>(p, s)
@@ -1000,6 +1006,7 @@ int launch_rc_k(const ConvParams& p, hipStream_t s) {
 
 int g_opt_plainrc = 1;
 int g_opt_rcpp = 3;
+int g_opt_rcocc = 1;
 
 bool st_resconv_eligible(const ConvParams& p, int dtype) {
   if (dtype != ST_BF16) return false;

@@ -199,12 +199,13 @@ OPT_BIGLA = 26
 OPT_BIG64 = 27
 OPT_BIG3 = 28
 OPT_SEGPART = 29
+OPT_RCOCC = 30
 # the production defaults of every STTS_OPT_* (include/stts2.h)
 OPT_DEFAULTS = {OPT_RESCONV: 1, OPT_GRID_CAP: 0, OPT_RESFUSED: 0, OPT_DEBUG: 0, OPT_STATS_SLOTS: 0,
                 OPT_SMALL_TILES: 1, OPT_BIGCONV: 2, OPT_HEAD: 1, OPT_SKEW: 0, OPT_FRONT: 1, OPT_PW: 1, OPT_SPLITK: 1,
                 OPT_EXP: 0, OPT_UPS: 1, OPT_WGRAD: 1, OPT_PLAINRC: 1, OPT_MSDFOLD: 1,
                 OPT_RCPP: 3, OPT_RESSPLIT: 1, OPT_BF16F: 0, OPT_YF32: 1, OPT_COUT1: 1, OPT_BRANCHES: 8, OPT_NBRANCH: 64,
-                OPT_BIGSPLIT: 1, OPT_BIGLA: 0, OPT_BIG64: 5, OPT_BIG3: 0, OPT_SEGPART: 1}
+                OPT_BIGSPLIT: 1, OPT_BIGLA: 0, OPT_BIG64: 5, OPT_BIG3: 0, OPT_SEGPART: 1, OPT_RCOCC: 1}
 # STTS_OPTS="KEY=VALUE,..." (A/B runs of whole suites): option values that replace the defaults for the process,
 # applied when the library loads and by reset_options()
 for _kv in filter(None, os.environ.get("STTS_OPTS", "").split(",")):
